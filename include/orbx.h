@@ -1,0 +1,130 @@
+/*
+ * orbx.h — C ABI of the MI355X-native ORB front-end (liborbx.so).
+ *
+ * Drop-in boundary for the ORB-SLAM2 hot path.  Plain C types
+ * only; no OpenCV, no torch.  Every entry point names the reference interface
+ * it replaces.  All functions return an orbx_status and never throw.
+ *
+ * Threading: a handle is single-threaded and owns one HIP stream plus its
+ * device workspace (one extractor per thread, like the reference's left/right
+ * extractors, src/Frame.cc:94-103).  The orbm_* matchers keep no global
+ * mutable state and are re-entrant.
+ */
+#ifndef ORBX_H
+#define ORBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    ORBX_OK = 0,
+    ORBX_EMPTY = 1,        /* empty input image: outputs untouched (src/ORBextractor.cc:1252) */
+    ORBX_EINVAL = -22,
+    ORBX_ENOMEM = -12,
+    ORBX_EDEVICE = -5,
+    ORBX_ENOSPC = -28      /* caller capacity too small */
+} orbx_status;
+
+/* Layout-identical to cv::KeyPoint {Point2f pt; float size, angle, response; int octave, class_id;} */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbx_keypoint;
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+ * include/ORBextractor.h:51-52; YAML keys ORBextractor.* (src/Tracking.cc:118-122). */
+typedef struct {
+    int nfeatures;
+    float scale_factor;
+    int nlevels;
+    int ini_th_fast;
+    int min_th_fast;
+} orbx_params;
+
+typedef struct orbx_handle orbx_handle;
+
+/* Replaces ORBextractor::ORBextractor (src/ORBextractor.cc:466-540). device = HIP ordinal. */
+orbx_status orbx_create(const orbx_params* params, int device, orbx_handle** out);
+void orbx_destroy(orbx_handle* h);
+
+/* Getters GetLevels/GetScaleFactor/GetScaleFactors/GetInverseScaleFactors/
+ * GetScaleSigmaSquares/GetInverseScaleSigmaSquares (include/ORBextractor.h:63-83).
+ * Each array has nlevels entries. Any pointer may be NULL. */
+orbx_status orbx_get_tables(const orbx_handle* h, int* nlevels, float* scale_factor,
+                            float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                            int* features_per_level);
+
+/* Per-frame keypoint capacity the extractor may need (nfeatures + slack per level). */
+int orbx_capacity(const orbx_handle* h, int rows, int cols);
+
+/* Replaces ORBextractor::operator()(image, mask, keypoints, descriptors)
+ * (include/ORBextractor.h:58-61, src/ORBextractor.cc:1248-1334).
+ * Host image in, host keypoints/descriptors out (desc: cap x 32 bytes, row i
+ * belongs to kps[i]).  Synchronous on the handle's stream.  Mask is ignored,
+ * as in the reference. */
+orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols, size_t step,
+                         orbx_keypoint* kps, int cap, uint8_t* desc, int* n_out);
+
+/* The public ORBextractor::mvImagePyramid (include/ORBextractor.h:85): level l of
+ * the last orbx_extract, copied to host lazily; valid until the next extract. */
+orbx_status orbx_get_level(orbx_handle* h, int level, const uint8_t** data, int* rows, int* cols,
+                           size_t* step);
+
+/* Batched device-resident replay (config 2/4): `batch` frames of rows x cols u8 at
+ * d_imgs + f*frame_stride (row pitch `step`), already in HBM.  Outputs per frame f:
+ * d_kps[f*cap + i], d_desc[(f*cap + i)*32], d_counts[f].  Asynchronous on `stream`
+ * (a hipStream_t; NULL = the handle's own stream). */
+orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int batch, int rows,
+                                      int cols, size_t step, size_t frame_stride,
+                                      orbx_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int cap,
+                                      void* stream);
+
+/* Wait for the work queued by the last extract on `stream` (NULL = handle stream) and
+ * return the device-side status (ORBX_ENOSPC when a frame exceeded `cap`). */
+orbx_status orbx_sync(orbx_handle* h, void* stream);
+
+/* Per-stage device timing of the last extract (ms, HIP events on the launch stream).
+ * Stages: 0 pyramid, 1 fast, 2 quadtree, 3 describe.  Enable before extracting. */
+orbx_status orbx_set_timing(orbx_handle* h, int enable);
+orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n);
+
+/* Test hooks: device stage dumps of the last batch, frame f (host buffers).
+ * pyramid: concatenated levels w_l*h_l; cand: per level (x_rel,y_rel,score) triples in
+ * reference order (vToDistributeKeys); cand_counts[l]. */
+orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t out_size);
+orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys, int cap, int* n);
+
+/* ---- Matcher (ORBmatcher Hamming inner loops, include/ORBmatcher.h:37-102) ---- */
+
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1728-1744), host helper. */
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+enum { ORBM_TOP2 = 0, ORBM_FULL_U16 = 1 };
+
+/* Config-5 brute force over device descriptors (32 B rows).  TOP2: per query the
+ * first-min index and the best/second distances (SearchByBoW tie rule,
+ * src/ORBmatcher.cc:214-224).  FULL_U16: the nq x nt distance matrix. */
+orbx_status orbm_allpairs_device(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int mode,
+                                 int* d_best_idx, int* d_best, int* d_second, uint16_t* d_full,
+                                 void* stream);
+
+/* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:417-588) for `npairs`
+ * frame pairs (F1 = pair_a[p], F2 = pair_b[p]) of a device batch produced by
+ * orbx_extract_batch_device (kps/desc/counts, per-frame capacity `cap`).  Grid
+ * and window follow Frame::GetFeaturesInArea (src/Frame.cc:410-495) for
+ * undistorted rows x cols frames; vbPrevMatched = F1 keypoint positions.
+ * Outputs: d_matches12[p*cap + i1] (-1 = none), d_nmatches[p]. */
+orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                                          const int* d_counts, int cap, const int* d_pair_a,
+                                          const int* d_pair_b, int npairs, int rows, int cols,
+                                          int window, float nnratio, int check_ori,
+                                          int* d_matches12, int* d_nmatches, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

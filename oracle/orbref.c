@@ -1,0 +1,852 @@
+/*
+ * orbref.c — CPU parity oracle (TEST INFRASTRUCTURE ONLY, see orbref.h).
+ *
+ * Every function names the reference file:line it restates.  Compiled with
+ * -ffp-contract=off; the two FMAs that GCC -O3 -march=native forms in the
+ * reference's BRIEF sampling (re-checked on this host's g++ 11)
+ * are written out with fmaf().
+ */
+#include "orbref.h"
+
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+static const int kPattern[1024] = {
+#include "../orb-slam-_amd/csrc/orb_pattern.inc"
+};
+
+enum { PATCH_SIZE = 31, HALF_PATCH_SIZE = 15, EDGE_THRESHOLD = 19 };
+
+/* ---- OpenCV scalar helpers -------------------------------- */
+static inline int cv_round_f(float v) { return (int)lrintf(v); }   /* cvtss2si, ties-to-even */
+static inline int cv_round_d(double v) { return (int)lrint(v); }
+static inline int cv_floor_f(float v) { int i = (int)v; return i - (i > v); }
+static inline int cv_ceil_f(float v) { int i = (int)v; return i + (i < v); }
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+static inline short sat_s16_f(float v) { int i = cv_round_f(v); return (short)clampi(i, SHRT_MIN, SHRT_MAX); }
+
+/* ---- a1: tables, src/ORBextractor.cc:466-540 ---------------------------- */
+int orbref_make_tables(const orbref_params* p, orbref_tables* t)
+{
+    if (!p || !t || p->nlevels < 1 || p->nlevels > ORBREF_MAX_LEVELS || p->nfeatures < 0 ||
+        !(p->scale_factor > 1.0f))
+        return -22;
+    memset(t, 0, sizeof(*t));
+    t->nlevels = p->nlevels;
+    t->nfeatures = p->nfeatures;
+    const double scaleFactor = (double)p->scale_factor; /* double member, include/ORBextractor.h:98 */
+    t->scale[0] = 1.0f;
+    t->sigma2[0] = 1.0f;
+    for (int i = 1; i < p->nlevels; i++) {          /* :478-482 */
+        t->scale[i] = (float)((double)t->scale[i - 1] * scaleFactor);
+        t->sigma2[i] = t->scale[i] * t->scale[i];
+    }
+    for (int i = 0; i < p->nlevels; i++) {          /* :486-490 */
+        t->inv_scale[i] = 1.0f / t->scale[i];
+        t->inv_sigma2[i] = 1.0f / t->sigma2[i];
+    }
+    /* :497-510 per-level feature budget */
+    const float factor = (float)(1.0f / scaleFactor);
+    float desired = (float)p->nfeatures * (1 - factor) /
+                    (1 - (float)pow((double)factor, (double)p->nlevels));
+    int sum = 0;
+    for (int l = 0; l < p->nlevels - 1; l++) {
+        t->nfeat_level[l] = cv_round_f(desired);
+        sum += t->nfeat_level[l];
+        desired *= factor;
+    }
+    t->nfeat_level[p->nlevels - 1] = p->nfeatures - sum > 0 ? p->nfeatures - sum : 0;
+
+    /* :522-539 umax */
+    const int vmax = cv_floor_f(HALF_PATCH_SIZE * sqrtf(2.f) / 2 + 1);
+    const int vmin = cv_ceil_f(HALF_PATCH_SIZE * sqrtf(2.f) / 2);
+    const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+    for (int v = 0; v <= vmax; ++v) t->umax[v] = cv_round_d(sqrt(hp2 - v * v));
+    for (int v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+        while (t->umax[v0] == t->umax[v0 + 1]) ++v0;
+        t->umax[v] = v0;
+        ++v0;
+    }
+    return 0;
+}
+
+void orbref_level_size(const orbref_tables* t, int level, int cols, int rows, int* w, int* h)
+{
+    /* src/ORBextractor.cc:1347-1348 */
+    const float s = t->inv_scale[level];
+    *w = cv_round_f((float)cols * s);
+    *h = cv_round_f((float)rows * s);
+}
+
+/* ---- a3: cv::resize INTER_LINEAR, u8, generic fixed-point path ---------- */
+void orbref_resize_linear(const uint8_t* src, int sw, int sh, size_t sstep,
+                          uint8_t* dst, int dw, int dh, size_t dstep)
+{
+    const double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+    const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    int* xofs = (int*)malloc(sizeof(int) * (size_t)dw);
+    short* alpha = (short*)malloc(sizeof(short) * 2 * (size_t)dw);
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor_f(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        xofs[dx] = sx;
+        alpha[2 * dx] = sat_s16_f((1.f - fx) * 2048);
+        alpha[2 * dx + 1] = sat_s16_f(fx * 2048);
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor_f(fy);
+        fy -= sy;
+        const int b0 = sat_s16_f((1.f - fy) * 2048), b1 = sat_s16_f(fy * 2048);
+        const int y0 = clampi(sy, 0, sh - 1), y1 = clampi(sy + 1, 0, sh - 1);
+        const uint8_t* r0 = src + (size_t)y0 * sstep;
+        const uint8_t* r1 = src + (size_t)y1 * sstep;
+        uint8_t* d = dst + (size_t)dy * dstep;
+        for (int dx = 0; dx < dw; dx++) {
+            const int x0 = xofs[dx], x1 = x0 + 1 < sw ? x0 + 1 : sw - 1;
+            const int a0 = alpha[2 * dx], a1 = alpha[2 * dx + 1];
+            const int h0 = r0[x0] * a0 + r0[x1] * a1;
+            const int h1 = r1[x0] * a0 + r1[x1] * a1;
+            d[dx] = sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);
+        }
+    }
+    free(xofs);
+    free(alpha);
+}
+
+/* ---- a5: cv::FAST TYPE_9_16 with NMS (FAST_t<16> + cornerScore<16>) ----- */
+static const int kRingX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+static const int kRingY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+static int corner_score16(const uint8_t* ptr, const int* pixel, int threshold)
+{
+    const int K = 8, N = K * 3 + 1;
+    int v = ptr[0];
+    short d[25];
+    for (int k = 0; k < N; k++) d[k] = (short)(v - ptr[pixel[k]]);
+    int a0 = threshold;
+    for (int k = 0; k < 16; k += 2) {
+        int a = d[k + 1] < d[k + 2] ? d[k + 1] : d[k + 2];
+        if (d[k + 3] < a) a = d[k + 3];
+        if (a <= a0) continue;
+        for (int m = 4; m <= 8; m++) if (d[k + m] < a) a = d[k + m];
+        int t0 = a < d[k] ? a : d[k];
+        if (t0 > a0) a0 = t0;
+        int t1 = a < d[k + 9] ? a : d[k + 9];
+        if (t1 > a0) a0 = t1;
+    }
+    int b0 = -a0;
+    for (int k = 0; k < 16; k += 2) {
+        int b = d[k + 1] > d[k + 2] ? d[k + 1] : d[k + 2];
+        for (int m = 3; m <= 5; m++) if (d[k + m] > b) b = d[k + m];
+        if (b >= b0) continue;
+        for (int m = 6; m <= 8; m++) if (d[k + m] > b) b = d[k + m];
+        int t0 = b > d[k] ? b : d[k];
+        if (t0 < b0) b0 = t0;
+        int t1 = b > d[k + 9] ? b : d[k + 9];
+        if (t1 < b0) b0 = t1;
+    }
+    return -b0 - 1;
+}
+
+int orbref_fast(const uint8_t* img, size_t step, int rows, int cols, int threshold, int* out, int cap)
+{
+    const int K = 8, N = 16 + K + 1;
+    int pixel[25];
+    for (int k = 0; k < 16; k++) pixel[k] = kRingX[k] + kRingY[k] * (int)step;
+    for (int k = 16; k < N; k++) pixel[k] = pixel[k - 16];
+    threshold = clampi(threshold, 0, 255);
+    uint8_t tab[512];
+    for (int i = -255; i <= 255; i++) tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+    if (rows < 7 || cols < 7) return 0;
+
+    uint8_t* buf = (uint8_t*)calloc((size_t)cols * 3, 1);
+    int* cp = (int*)malloc(sizeof(int) * 3 * ((size_t)cols + 1));
+    int n = 0;
+    for (int i = 3; i < rows - 2; i++) {
+        const uint8_t* ptr = img + (size_t)i * step + 3;
+        uint8_t* curr = buf + (size_t)((i - 3) % 3) * cols;
+        int* cornerpos = cp + (size_t)((i - 3) % 3) * (cols + 1) + 1;
+        memset(curr, 0, (size_t)cols);
+        int ncorners = 0;
+        if (i < rows - 3) {
+            for (int j = 3; j < cols - 3; j++, ptr++) {
+                const int v = ptr[0];
+                const uint8_t* t = tab - v + 255;
+                int d = t[ptr[pixel[0]]] | t[ptr[pixel[8]]];
+                if (d == 0) continue;
+                d &= t[ptr[pixel[2]]] | t[ptr[pixel[10]]];
+                d &= t[ptr[pixel[4]]] | t[ptr[pixel[12]]];
+                d &= t[ptr[pixel[6]]] | t[ptr[pixel[14]]];
+                if (d == 0) continue;
+                d &= t[ptr[pixel[1]]] | t[ptr[pixel[9]]];
+                d &= t[ptr[pixel[3]]] | t[ptr[pixel[11]]];
+                d &= t[ptr[pixel[5]]] | t[ptr[pixel[13]]];
+                d &= t[ptr[pixel[7]]] | t[ptr[pixel[15]]];
+                if (d & 1) {
+                    const int vt = v - threshold;
+                    for (int k = 0, count = 0; k < N; k++) {
+                        if (ptr[pixel[k]] < vt) {
+                            if (++count > K) {
+                                cornerpos[ncorners++] = j;
+                                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                                break;
+                            }
+                        } else count = 0;
+                    }
+                }
+                if (d & 2) {
+                    const int vt = v + threshold;
+                    for (int k = 0, count = 0; k < N; k++) {
+                        if (ptr[pixel[k]] > vt) {
+                            if (++count > K) {
+                                cornerpos[ncorners++] = j;
+                                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                                break;
+                            }
+                        } else count = 0;
+                    }
+                }
+            }
+        }
+        cornerpos[-1] = ncorners;
+        if (i == 3) continue;
+        const uint8_t* prev = buf + (size_t)((i - 4 + 3) % 3) * cols;
+        const uint8_t* pprev = buf + (size_t)((i - 5 + 3) % 3) * cols;
+        cornerpos = cp + (size_t)((i - 4 + 3) % 3) * (cols + 1) + 1;
+        ncorners = cornerpos[-1];
+        for (int k = 0; k < ncorners; k++) {
+            const int j = cornerpos[k];
+            const int score = prev[j];
+            if (score > prev[j + 1] && score > prev[j - 1] && score > pprev[j - 1] &&
+                score > pprev[j] && score > pprev[j + 1] && score > curr[j - 1] &&
+                score > curr[j] && score > curr[j + 1]) {
+                if (n >= cap) { free(buf); free(cp); return -1; }
+                out[3 * n] = j;
+                out[3 * n + 1] = i - 1;
+                out[3 * n + 2] = score;
+                n++;
+            }
+        }
+    }
+    free(buf);
+    free(cp);
+    return n;
+}
+
+/* ---- a4: per-level cell loop, src/ORBextractor.cc:932-1002 --------------- */
+int orbref_level_candidates(const uint8_t* level, size_t step, int w, int h, int ini_th, int min_th,
+                            int* out, int cap)
+{
+    const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+    const int maxBorderX = w - EDGE_THRESHOLD + 3, maxBorderY = h - EDGE_THRESHOLD + 3;
+    const float W = 30;
+    const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+    const int nCols = (int)(width / W), nRows = (int)(height / W);
+    if (nCols <= 0 || nRows <= 0) return 0; /* reference divides by zero here */
+    const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+    int n = 0;
+    int* cell = (int*)malloc(sizeof(int) * 3 * 4096);
+    for (int i = 0; i < nRows; i++) {
+        const float iniY = (float)(minBorderY + i * hCell);
+        float maxY = iniY + hCell + 6;
+        if (iniY >= maxBorderY - 3) continue;
+        if (maxY > maxBorderY) maxY = (float)maxBorderY;
+        for (int j = 0; j < nCols; j++) {
+            const float iniX = (float)(minBorderX + j * wCell);
+            float maxX = iniX + wCell + 6;
+            if (iniX >= maxBorderX - 6) continue;
+            if (maxX > maxBorderX) maxX = (float)maxBorderX;
+            const int y0 = (int)iniY, x0 = (int)iniX;
+            const int rr = (int)maxY - y0, cc = (int)maxX - x0;
+            const uint8_t* roi = level + (size_t)y0 * step + x0;
+            int k = orbref_fast(roi, step, rr, cc, ini_th, cell, 4096);
+            if (k == 0) k = orbref_fast(roi, step, rr, cc, min_th, cell, 4096);
+            if (k < 0) { free(cell); return -1; }
+            for (int q = 0; q < k; q++) {
+                if (n >= cap) { free(cell); return -1; }
+                out[3 * n] = cell[3 * q] + j * wCell;
+                out[3 * n + 1] = cell[3 * q + 1] + i * hCell;
+                out[3 * n + 2] = cell[3 * q + 2];
+                n++;
+            }
+        }
+    }
+    free(cell);
+    return n;
+}
+
+/* ---- a6: DistributeOctTree, src/ORBextractor.cc:569-907 ------------------ */
+typedef struct {
+    int x0, x1, y0, y1;       /* UL.x, UR.x, UL.y, BL.y */
+    int* keys;                /* indices into the candidate array, reference order */
+    int nkeys;
+    int no_more;
+    int prev, next;           /* std::list links */
+    long seq;                 /* creation order: canonical tie-break for the size sort */
+} qnode;
+
+typedef struct {
+    qnode* a;
+    int n, cap, head, tail, size;
+    long seq;
+} qlist;
+
+static int ql_new(qlist* L)
+{
+    if (L->n == L->cap) {
+        L->cap = L->cap ? L->cap * 2 : 256;
+        L->a = (qnode*)realloc(L->a, sizeof(qnode) * (size_t)L->cap);
+    }
+    qnode* q = &L->a[L->n];
+    memset(q, 0, sizeof(*q));
+    q->prev = q->next = -1;
+    return L->n++;
+}
+
+static void ql_push_front(qlist* L, int i)
+{
+    L->a[i].prev = -1;
+    L->a[i].next = L->head;
+    if (L->head >= 0) L->a[L->head].prev = i; else L->tail = i;
+    L->head = i;
+    L->a[i].seq = L->seq++;
+    L->size++;
+}
+
+static void ql_push_back(qlist* L, int i)
+{
+    L->a[i].next = -1;
+    L->a[i].prev = L->tail;
+    if (L->tail >= 0) L->a[L->tail].next = i; else L->head = i;
+    L->tail = i;
+    L->a[i].seq = L->seq++;
+    L->size++;
+}
+
+static int ql_erase(qlist* L, int i)
+{
+    qnode* q = &L->a[i];
+    const int nx = q->next;
+    if (q->prev >= 0) L->a[q->prev].next = q->next; else L->head = q->next;
+    if (q->next >= 0) L->a[q->next].prev = q->prev; else L->tail = q->prev;
+    free(q->keys);
+    q->keys = NULL;
+    L->size--;
+    return nx;
+}
+
+/* ExtractorNode::DivideNode, src/ORBextractor.cc:569-629.  Creates the four
+ * children (not yet linked) and returns their indices in ch[0..3]. */
+static void divide_node(qlist* L, int pi, const int* xys, int ch[4])
+{
+    for (int q = 0; q < 4; q++) ch[q] = ql_new(L);
+    qnode* p = &L->a[pi];
+    const int halfX = (int)ceilf((float)(p->x1 - p->x0) / 2);
+    const int halfY = (int)ceilf((float)(p->y1 - p->y0) / 2);
+    const int mx = p->x0 + halfX, my = p->y0 + halfY;
+    const int rx0[4] = {p->x0, mx, p->x0, mx}, rx1[4] = {mx, p->x1, mx, p->x1};
+    const int ry0[4] = {p->y0, p->y0, my, my}, ry1[4] = {my, my, p->y1, p->y1};
+    for (int q = 0; q < 4; q++) {
+        qnode* c = &L->a[ch[q]];
+        c->x0 = rx0[q]; c->x1 = rx1[q]; c->y0 = ry0[q]; c->y1 = ry1[q];
+        c->keys = (int*)malloc(sizeof(int) * (size_t)(p->nkeys > 0 ? p->nkeys : 1));
+        c->nkeys = 0;
+    }
+    for (int k = 0; k < p->nkeys; k++) {
+        const int id = p->keys[k];
+        const float kx = (float)xys[3 * id], ky = (float)xys[3 * id + 1];
+        int q;
+        if (kx < (float)mx) q = ky < (float)my ? 0 : 2;
+        else q = ky < (float)my ? 1 : 3;
+        qnode* c = &L->a[ch[q]];
+        c->keys[c->nkeys++] = id;
+    }
+    for (int q = 0; q < 4; q++)
+        if (L->a[ch[q]].nkeys == 1) L->a[ch[q]].no_more = 1;
+}
+
+typedef struct { int size; long seq; int node; } size_node;
+
+static int cmp_size_node(const void* A, const void* B)
+{
+    const size_node* a = (const size_node*)A;
+    const size_node* b = (const size_node*)B;
+    if (a->size != b->size) return a->size < b->size ? -1 : 1;
+    return a->seq < b->seq ? -1 : (a->seq > b->seq);   /* canonical: creation order */
+}
+
+/* Link the non-empty children of a split node (push_front in n1..n4 order) and
+ * record the expandable ones; returns how many had more than one key. */
+static int link_children(qlist* L, const int ch[4], size_node** vec, int* nvec, int* capvec)
+{
+    int nexp = 0;
+    for (int q = 0; q < 4; q++) {
+        qnode* c = &L->a[ch[q]];
+        if (c->nkeys > 0) {
+            ql_push_front(L, ch[q]);
+            if (L->a[ch[q]].nkeys > 1) {
+                nexp++;
+                if (*nvec == *capvec) {
+                    *capvec = *capvec ? *capvec * 2 : 256;
+                    *vec = (size_node*)realloc(*vec, sizeof(size_node) * (size_t)*capvec);
+                }
+                (*vec)[*nvec].size = L->a[ch[q]].nkeys;
+                (*vec)[*nvec].seq = L->a[ch[q]].seq;
+                (*vec)[*nvec].node = ch[q];
+                (*nvec)++;
+            }
+        } else {
+            free(c->keys);
+            c->keys = NULL;
+        }
+    }
+    return nexp;
+}
+
+int orbref_distribute(const int* xys, int n, int minX, int maxX, int minY, int maxY, int N,
+                      int* out, int cap)
+{
+    /* :650-653 */
+    const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
+    if (nIni <= 0) return -1;          /* reference divides by zero */
+    const float hX = (float)(maxX - minX) / nIni;
+
+    qlist L;
+    memset(&L, 0, sizeof(L));
+    L.head = L.tail = -1;
+    int* ini = (int*)malloc(sizeof(int) * (size_t)nIni);
+    for (int i = 0; i < nIni; i++) {   /* :663-675 */
+        const int id = ql_new(&L);
+        qnode* q = &L.a[id];
+        q->x0 = (int)(hX * (float)i);
+        q->x1 = (int)(hX * (float)(i + 1));
+        q->y0 = 0;
+        q->y1 = maxY - minY;
+        q->keys = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+        ql_push_back(&L, id);
+        ini[i] = id;
+    }
+    for (int k = 0; k < n; k++) {      /* :679-683 */
+        size_t r = (size_t)((float)xys[3 * k] / hX);
+        if (r >= (size_t)nIni) r = (size_t)nIni - 1;   /* unreachable for in-border keypoints */
+        qnode* q = &L.a[ini[r]];
+        q->keys[q->nkeys++] = k;
+    }
+    free(ini);
+    for (int it = L.head; it >= 0;) {  /* :688-699 */
+        if (L.a[it].nkeys == 1) { L.a[it].no_more = 1; it = L.a[it].next; }
+        else if (L.a[it].nkeys == 0) it = ql_erase(&L, it);
+        else it = L.a[it].next;
+    }
+
+    size_node* vec = NULL;
+    int nvec = 0, capvec = 0;
+    size_node* prevv = NULL;
+    int capprev = 0;
+    int finish = 0;
+    while (!finish) {                  /* :710-876 */
+        int prevSize = L.size;
+        int nToExpand = 0;
+        nvec = 0;
+        for (int it = L.head; it >= 0;) {
+            if (L.a[it].no_more) { it = L.a[it].next; continue; }
+            int ch[4];
+            divide_node(&L, it, xys, ch);
+            nToExpand += link_children(&L, ch, &vec, &nvec, &capvec);
+            it = ql_erase(&L, it);
+        }
+        if (L.size >= N || L.size == prevSize) {
+            finish = 1;
+        } else if (L.size + nToExpand * 3 > N) {
+            while (!finish) {          /* :805-874 */
+                prevSize = L.size;
+                if (capprev < nvec) {
+                    capprev = nvec;
+                    prevv = (size_node*)realloc(prevv, sizeof(size_node) * (size_t)capprev);
+                }
+                const int nprev = nvec;
+                if (nprev) memcpy(prevv, vec, sizeof(size_node) * (size_t)nprev);
+                nvec = 0;
+                qsort(prevv, (size_t)nprev, sizeof(size_node), cmp_size_node);
+                for (int j = nprev - 1; j >= 0; j--) {
+                    int ch[4];
+                    divide_node(&L, prevv[j].node, xys, ch);
+                    link_children(&L, ch, &vec, &nvec, &capvec);
+                    ql_erase(&L, prevv[j].node);
+                    if (L.size >= N) break;
+                }
+                if (L.size >= N || L.size == prevSize) finish = 1;
+            }
+        }
+    }
+
+    /* :882-906 retain the best keypoint per node (first max wins) */
+    int m = 0, status = 0;
+    for (int it = L.head; it >= 0; it = L.a[it].next) {
+        const qnode* q = &L.a[it];
+        int best = q->keys[0];
+        int bestResp = xys[3 * best + 2];
+        for (int k = 1; k < q->nkeys; k++) {
+            const int id = q->keys[k];
+            if (xys[3 * id + 2] > bestResp) { best = id; bestResp = xys[3 * id + 2]; }
+        }
+        if (m >= cap) { status = -1; break; }
+        out[m++] = best;
+    }
+    for (int i = 0; i < L.n; i++) free(L.a[i].keys);
+    free(L.a);
+    free(vec);
+    free(prevv);
+    return status < 0 ? -1 : m;
+}
+
+/* ---- a7: IC_Angle + cv::fastAtan2 --------------------------------------- */
+float orbref_fast_atan2(float y, float x)
+{
+    /* OpenCV 3.x mathfuncs atan_f32; float arithmetic, no FMA */
+    static const float k180pi = (float)(180 / 3.1415926535897932384626433832795);
+    const float p1 = 0.9997878412794807f * k180pi;
+    const float p3 = -0.3258083974640975f * k180pi;
+    const float p5 = 0.1555786518463281f * k180pi;
+    const float p7 = -0.04432655554792128f * k180pi;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+float orbref_ic_angle(const uint8_t* img, size_t step, int cx, int cy, const int* umax)
+{
+    /* src/ORBextractor.cc:84-128 */
+    const uint8_t* center = img + (size_t)cy * step + cx;
+    const int s = (int)step;
+    int m01 = 0, m10 = 0;
+    for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m10 += u * center[u];
+    for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+        int vsum = 0;
+        const int d = umax[v];
+        for (int u = -d; u <= d; ++u) {
+            const int vp = center[u + v * s], vm = center[u - v * s];
+            vsum += vp - vm;
+            m10 += u * (vp + vm);
+        }
+        m01 += v * vsum;
+    }
+    return orbref_fast_atan2((float)m01, (float)m10);
+}
+
+/* ---- a8: GaussianBlur 7x7 sigma 2 BORDER_REFLECT_101, u8 integer path --- */
+static inline int reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+
+void orbref_gaussian_blur7(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, size_t dstep)
+{
+    /* getGaussianKernel(7, 2, CV_32F) scaled by 256 and rounded */
+    static const int k[7] = {18, 34, 49, 55, 49, 34, 18};
+    int* rows = (int*)malloc(sizeof(int) * (size_t)w * (size_t)h);
+    for (int y = 0; y < h; y++) {
+        const uint8_t* s = src + (size_t)y * sstep;
+        for (int x = 0; x < w; x++) {
+            int acc = 0;
+            for (int i = 0; i < 7; i++) acc += k[i] * s[reflect101(x + i - 3, w)];
+            rows[(size_t)y * w + x] = acc;
+        }
+    }
+    for (int y = 0; y < h; y++) {
+        uint8_t* d = dst + (size_t)y * dstep;
+        for (int x = 0; x < w; x++) {
+            int acc = 0;
+            for (int j = 0; j < 7; j++) acc += k[j] * rows[(size_t)reflect101(y + j - 3, h) * w + x];
+            d[x] = sat_u8((acc + (1 << 15)) >> 16);
+        }
+    }
+    free(rows);
+}
+
+/* ---- a9: computeOrbDescriptor, src/ORBextractor.cc:141-192 --------------- */
+void orbref_brief(const uint8_t* blur, size_t step, float kx, float ky, float angle_deg, uint8_t desc[32])
+{
+    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+    const float angle = angle_deg * factorPI;
+    const float a = cosf(angle), b = sinf(angle);
+    const uint8_t* center = blur + (ptrdiff_t)cv_round_f(ky) * (ptrdiff_t)step + cv_round_f(kx);
+    const int s = (int)step;
+    for (int i = 0; i < 32; ++i) {
+        int val = 0;
+        for (int k = 0; k < 8; ++k) {
+            const int* pr = &kPattern[4 * (8 * i + k)];
+            int t[2];
+            for (int e = 0; e < 2; e++) {
+                const float px = (float)pr[2 * e], py = (float)pr[2 * e + 1];
+                const int yy = cv_round_f(fmaf(px, b, py * a));
+                const int xx = cv_round_f(fmaf(px, a, -(py * b)));
+                t[e] = center[yy * s + xx];
+            }
+            val |= (t[0] < t[1]) << k;
+        }
+        desc[i] = (uint8_t)val;
+    }
+}
+
+/* ---- a2: ORBextractor::operator(), src/ORBextractor.cc:1248-1334 --------- */
+int orbref_extract(const orbref_params* p, const uint8_t* img, int rows, int cols, size_t step,
+                   orbref_keypoint* kps, int cap, uint8_t* desc, int* n_out,
+                   uint8_t* pyramid, int* level_counts, int* cand_counts)
+{
+    if (!p || !n_out) return -22;
+    if (!img || rows <= 0 || cols <= 0) return 1; /* :1252 empty image: no-op */
+    orbref_tables t;
+    if (orbref_make_tables(p, &t) != 0) return -22;
+    const int L = t.nlevels;
+
+    /* a3 ComputePyramid :1342-1377 */
+    int lw[ORBREF_MAX_LEVELS], lh[ORBREF_MAX_LEVELS];
+    uint8_t* lev[ORBREF_MAX_LEVELS];
+    for (int l = 0; l < L; l++) {
+        orbref_level_size(&t, l, cols, rows, &lw[l], &lh[l]);
+        if (lw[l] <= 0 || lh[l] <= 0) return -22;
+        lev[l] = (uint8_t*)malloc((size_t)lw[l] * lh[l]);
+        if (l == 0) {
+            for (int y = 0; y < rows; y++) memcpy(lev[0] + (size_t)y * cols, img + (size_t)y * step, (size_t)cols);
+        } else {
+            orbref_resize_linear(lev[l - 1], lw[l - 1], lh[l - 1], (size_t)lw[l - 1], lev[l], lw[l], lh[l], (size_t)lw[l]);
+        }
+    }
+
+    /* a4/a6 ComputeKeyPointsOctTree :915-1026 */
+    int* lvl_kx[ORBREF_MAX_LEVELS];
+    int* lvl_ky[ORBREF_MAX_LEVELS];
+    int* lvl_sc[ORBREF_MAX_LEVELS];
+    int lvl_n[ORBREF_MAX_LEVELS];
+    int status = 0;
+    for (int l = 0; l < L; l++) {
+        const int cap_c = lw[l] * lh[l] / 2 + 16;
+        int* cand = (int*)malloc(sizeof(int) * 3 * (size_t)cap_c);
+        int nc = orbref_level_candidates(lev[l], (size_t)lw[l], lw[l], lh[l], p->ini_th_fast, p->min_th_fast, cand, cap_c);
+        if (cand_counts) cand_counts[l] = nc;
+        const int minB = EDGE_THRESHOLD - 3;
+        const int capd = nc + 4 * 64 + 8;
+        int* idx = (int*)malloc(sizeof(int) * (size_t)capd);
+        int nd = nc < 0 ? -1
+                        : orbref_distribute(cand, nc, minB, lw[l] - EDGE_THRESHOLD + 3, minB,
+                                            lh[l] - EDGE_THRESHOLD + 3, t.nfeat_level[l], idx, capd);
+        if (nd < 0) { status = -22; nd = 0; }
+        lvl_n[l] = nd;
+        lvl_kx[l] = (int*)malloc(sizeof(int) * (size_t)(nd + 1));
+        lvl_ky[l] = (int*)malloc(sizeof(int) * (size_t)(nd + 1));
+        lvl_sc[l] = (int*)malloc(sizeof(int) * (size_t)(nd + 1));
+        for (int i = 0; i < nd; i++) {   /* :1019-1025 add border */
+            lvl_kx[l][i] = cand[3 * idx[i]] + minB;
+            lvl_ky[l][i] = cand[3 * idx[i] + 1] + minB;
+            lvl_sc[l][i] = cand[3 * idx[i] + 2];
+        }
+        free(cand);
+        free(idx);
+    }
+    int total = 0;
+    for (int l = 0; l < L; l++) total += lvl_n[l];
+    if (status == 0 && total > cap) status = -28;
+
+    if (status == 0) {
+        int off = 0;
+        for (int l = 0; l < L; l++) {
+            if (level_counts) level_counts[l] = lvl_n[l];
+            const int nl = lvl_n[l];
+            if (nl == 0) continue;
+            const float size = (float)(int)(PATCH_SIZE * t.scale[l]);   /* :1013 */
+            uint8_t* blur = (uint8_t*)malloc((size_t)lw[l] * lh[l]);
+            orbref_gaussian_blur7(lev[l], lw[l], lh[l], (size_t)lw[l], blur, (size_t)lw[l]);   /* :1300-1306 */
+            for (int i = 0; i < nl; i++) {
+                orbref_keypoint* k = &kps[off + i];
+                const float ang = orbref_ic_angle(lev[l], (size_t)lw[l], lvl_kx[l][i], lvl_ky[l][i], t.umax);  /* :1030-1033 */
+                orbref_brief(blur, (size_t)lw[l], (float)lvl_kx[l][i], (float)lvl_ky[l][i], ang, desc + 32 * (size_t)(off + i));
+                float x = (float)lvl_kx[l][i], y = (float)lvl_ky[l][i];
+                if (l != 0) { x *= t.scale[l]; y *= t.scale[l]; }   /* :1322-1329 */
+                k->x = x; k->y = y; k->size = size; k->angle = ang;
+                k->response = (float)lvl_sc[l][i];
+                k->octave = l; k->class_id = -1;
+            }
+            free(blur);
+            off += nl;
+        }
+        *n_out = total;
+    }
+    if (pyramid) {
+        size_t o = 0;
+        for (int l = 0; l < L; l++) { memcpy(pyramid + o, lev[l], (size_t)lw[l] * lh[l]); o += (size_t)lw[l] * lh[l]; }
+    }
+    for (int l = 0; l < L; l++) { free(lev[l]); free(lvl_kx[l]); free(lvl_ky[l]); free(lvl_sc[l]); }
+    return status;
+}
+
+/* ---- a11: DescriptorDistance, src/ORBmatcher.cc:1728-1744 ---------------- */
+int orbref_descriptor_distance(const uint8_t* a, const uint8_t* b)
+{
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t wa, wb;
+        memcpy(&wa, a + 4 * i, 4);
+        memcpy(&wb, b + 4 * i, 4);
+        uint32_t v = wa ^ wb;
+        v = v - ((v >> 1) & 0x55555555u);
+        v = (v & 0x33333333u) + ((v >> 2) & 0x33333333u);
+        dist += (int)((((v + (v >> 4)) & 0xF0F0F0Fu) * 0x1010101u) >> 24);
+    }
+    return dist;
+}
+
+/* ---- a14 + a16: SearchForInitialization over the Frame grid ------------- */
+enum { GRID_COLS = 64, GRID_ROWS = 48, TH_LOW = 50, HISTO_LENGTH = 30 };
+
+static void three_maxima(const int* hist, int* i1, int* i2, int* i3)
+{
+    /* src/ORBmatcher.cc:1679-1723 */
+    int max1 = 0, max2 = 0, max3 = 0;
+    *i1 = *i2 = *i3 = -1;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = hist[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; *i3 = *i2; *i2 = *i1; *i1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; *i3 = *i2; *i2 = i; }
+        else if (s > max3) { max3 = s; *i3 = i; }
+    }
+    if ((float)max2 < 0.1f * (float)max1) { *i2 = -1; *i3 = -1; }
+    else if ((float)max3 < 0.1f * (float)max1) { *i3 = -1; }
+}
+
+int orbref_search_for_initialization(const orbref_keypoint* k1, const uint8_t* d1, int n1,
+                                     const orbref_keypoint* k2, const uint8_t* d2, int n2,
+                                     int cols, int rows, float* prev_xy, int* matches12,
+                                     int window, float nnratio, int check_ori)
+{
+    /* Frame::ComputeImageBounds (undistorted) + grid scale, src/Frame.cc:202-209, 614-620 */
+    const float minX = 0.0f, maxX = (float)cols, minY = 0.0f, maxY = (float)rows;
+    const float invW = (float)GRID_COLS / (maxX - minX);
+    const float invH = (float)GRID_ROWS / (maxY - minY);
+
+    /* AssignFeaturesToGrid / PosInGrid, src/Frame.cc:292-311, 504-518 */
+    int* cnt = (int*)calloc(GRID_COLS * GRID_ROWS + 1, sizeof(int));
+    int* cellOf = (int*)malloc(sizeof(int) * (size_t)(n2 + 1));
+    for (int i = 0; i < n2; i++) {
+        const int px = (int)roundf((k2[i].x - minX) * invW);
+        const int py = (int)roundf((k2[i].y - minY) * invH);
+        cellOf[i] = (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) ? -1 : px * GRID_ROWS + py;
+        if (cellOf[i] >= 0) cnt[cellOf[i] + 1]++;
+    }
+    for (int c = 0; c < GRID_COLS * GRID_ROWS; c++) cnt[c + 1] += cnt[c];
+    int* cells = (int*)malloc(sizeof(int) * (size_t)(n2 + 1));
+    int* fill = (int*)calloc(GRID_COLS * GRID_ROWS, sizeof(int));
+    for (int i = 0; i < n2; i++)
+        if (cellOf[i] >= 0) cells[cnt[cellOf[i]] + fill[cellOf[i]]++] = i;
+
+    /* src/ORBmatcher.cc:417-588 */
+    int nmatches = 0;
+    for (int i = 0; i < n1; i++) matches12[i] = -1;
+    int* matchedDist = (int*)malloc(sizeof(int) * (size_t)(n2 + 1));
+    int* matches21 = (int*)malloc(sizeof(int) * (size_t)(n2 + 1));
+    int* binOf = (int*)malloc(sizeof(int) * (size_t)(n1 + 1));
+    for (int i = 0; i < n2; i++) { matchedDist[i] = INT_MAX; matches21[i] = -1; }
+    int hist[HISTO_LENGTH] = {0};
+    const float factor = 1.0f / HISTO_LENGTH;
+    const float r = (float)window;
+
+    for (int i1 = 0; i1 < n1; i1++) {
+        binOf[i1] = -1;
+        if (k1[i1].octave > 0) continue;
+        const float x = prev_xy[2 * i1], y = prev_xy[2 * i1 + 1];
+        /* Frame::GetFeaturesInArea(x, y, r, 0, 0), src/Frame.cc:410-495 */
+        const int nMinCellX = (int)floorf((x - minX - r) * invW) > 0 ? (int)floorf((x - minX - r) * invW) : 0;
+        if (nMinCellX >= GRID_COLS) continue;
+        const int cxm = (int)ceilf((x - minX + r) * invW);
+        const int nMaxCellX = cxm < GRID_COLS - 1 ? cxm : GRID_COLS - 1;
+        if (nMaxCellX < 0) continue;
+        const int nMinCellY = (int)floorf((y - minY - r) * invH) > 0 ? (int)floorf((y - minY - r) * invH) : 0;
+        if (nMinCellY >= GRID_ROWS) continue;
+        const int cym = (int)ceilf((y - minY + r) * invH);
+        const int nMaxCellY = cym < GRID_ROWS - 1 ? cym : GRID_ROWS - 1;
+        if (nMaxCellY < 0) continue;
+
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1, any = 0;
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+                const int c = ix * GRID_ROWS + iy;
+                for (int j = cnt[c]; j < cnt[c + 1]; j++) {
+                    const int i2 = cells[j];
+                    const orbref_keypoint* kp = &k2[i2];
+                    if (kp->octave < 0 || kp->octave > 0) continue;
+                    const float distx = kp->x - x, disty = kp->y - y;
+                    if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+                    any = 1;
+                    const int dist = orbref_descriptor_distance(d1 + 32 * (size_t)i1, d2 + 32 * (size_t)i2);
+                    if (matchedDist[i2] <= dist) continue;
+                    if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx2 = i2; }
+                    else if (dist < bestDist2) bestDist2 = dist;
+                }
+            }
+        }
+        if (!any) continue;
+        if (bestDist <= TH_LOW && (float)bestDist < (float)bestDist2 * nnratio) {
+            if (matches21[bestIdx2] >= 0) { matches12[matches21[bestIdx2]] = -1; nmatches--; }
+            matches12[i1] = bestIdx2;
+            matches21[bestIdx2] = i1;
+            matchedDist[bestIdx2] = bestDist;
+            nmatches++;
+            if (check_ori) {
+                float rot = k1[i1].angle - k2[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == HISTO_LENGTH) bin = 0;
+                binOf[i1] = bin;
+                hist[bin]++;
+            }
+        }
+    }
+    if (check_ori) {
+        int a, b, c;
+        three_maxima(hist, &a, &b, &c);
+        for (int i1 = 0; i1 < n1; i1++) {
+            const int bin = binOf[i1];
+            if (bin < 0 || bin == a || bin == b || bin == c) continue;
+            if (matches12[i1] >= 0) { matches12[i1] = -1; nmatches--; }
+        }
+    }
+    for (int i1 = 0; i1 < n1; i1++)
+        if (matches12[i1] >= 0) { prev_xy[2 * i1] = k2[matches12[i1]].x; prev_xy[2 * i1 + 1] = k2[matches12[i1]].y; }
+    free(cnt); free(cellOf); free(cells); free(fill); free(matchedDist); free(matches21); free(binOf);
+    return nmatches;
+}
+
+void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,
+                          int* best_idx, int* best_d, int* second_d)
+{
+    for (int i = 0; i < nq; i++) {
+        int b1 = 256, b2 = 256, bi = -1;
+        for (int j = 0; j < nt; j++) {
+            const int d = orbref_descriptor_distance(q + 32 * (size_t)i, t + 32 * (size_t)j);
+            if (d < b1) { b2 = b1; b1 = d; bi = j; }
+            else if (d < b2) b2 = d;
+        }
+        best_idx[i] = bi; best_d[i] = b1; second_d[i] = b2;
+    }
+}

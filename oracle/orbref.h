@@ -1,0 +1,138 @@
+/*
+ * orbref — CPU restatement of the ORB-SLAM2 ORB front-end hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity oracle for the
+ * MI355X (HIP) implementation in orb-slam-_amd/.  Only tests/, the
+ * __graft_entry__.smoke() check and bench.py's cpu_baseline leg may load it.
+ * The product path never calls into it.
+ *
+ * It restates, line by line, the behaviour of
+ *   /root/reference/src/ORBextractor.cc   (ORB_SLAM2::ORBextractor)
+ *   /root/reference/src/ORBmatcher.cc     (DescriptorDistance, SearchForInitialization,
+ *                                          ComputeThreeMaxima)
+ *   /root/reference/src/Frame.cc          (AssignFeaturesToGrid / PosInGrid /
+ *                                          GetFeaturesInArea)
+ * with the OpenCV 3.x primitives the reference calls (FAST, resize INTER_LINEAR,
+ * GaussianBlur, fastAtan2, cvRound) restated from their published generic
+ * scalar code paths, and glibc 2.35 cosf/sinf taken
+ * from the host libm.
+ *
+ * Parity status (see DESIGN.md "Oracle"): the reference cannot be built here
+ * (OpenCV absent; src/ORBextractor.cc:160-162 does not compile) and ships no
+ * tests or golden vectors.  Pinned: every constant table the
+ * reference holds (bit_pattern_31_, umax, level scales, per-level budgets,
+ * level sizes, cell grids) via known-answer tests.  Pixel arithmetic at the
+ * OpenCV boundary (FAST / resize / GaussianBlur / fastAtan2): PARITY UNPINNED
+ * against real OpenCV; restated from its generic scalar path.
+ *
+ * Determinism: DistributeOctTree breaks size ties by heap address in the
+ * reference (src/ORBextractor.cc:815).  This oracle uses the canonical
+ * tie-break "creation order" (what a monotone allocator would give).
+ */
+#ifndef ORBREF_H
+#define ORBREF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBREF_MAX_LEVELS 16
+
+/* Layout-identical to cv::KeyPoint (28 bytes). */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbref_keypoint;
+
+typedef struct {
+    int nfeatures;
+    float scale_factor;
+    int nlevels;
+    int ini_th_fast;
+    int min_th_fast;
+} orbref_params;
+
+typedef struct {
+    int nlevels;
+    int nfeatures;
+    float scale[ORBREF_MAX_LEVELS];
+    float inv_scale[ORBREF_MAX_LEVELS];
+    float sigma2[ORBREF_MAX_LEVELS];
+    float inv_sigma2[ORBREF_MAX_LEVELS];
+    int nfeat_level[ORBREF_MAX_LEVELS];
+    int umax[16];
+} orbref_tables;
+
+/* a1: ORBextractor::ORBextractor  (src/ORBextractor.cc:466-540) */
+int orbref_make_tables(const orbref_params* p, orbref_tables* t);
+
+/* a3: level size, src/ORBextractor.cc:1347-1348 */
+void orbref_level_size(const orbref_tables* t, int level, int cols, int rows, int* w, int* h);
+
+/* OpenCV resize(INTER_LINEAR) u8 generic path. */
+void orbref_resize_linear(const uint8_t* src, int sw, int sh, size_t sstep,
+                          uint8_t* dst, int dw, int dh, size_t dstep);
+
+/* OpenCV FAST_t<16> with non-max suppression on a ROI.
+ * Writes (x, y, score) triples in OpenCV emission order; returns the count,
+ * or -1 if more than cap keypoints. */
+int orbref_fast(const uint8_t* roi, size_t step, int rows, int cols, int threshold,
+                int* out_xys, int cap);
+
+/* a4: ComputeKeyPointsOctTree cell loop (src/ORBextractor.cc:932-1002) for one
+ * level: returns vToDistributeKeys as (x_rel, y_rel, score) triples. */
+int orbref_level_candidates(const uint8_t* level, size_t step, int w, int h,
+                            int ini_th, int min_th, int* out_xys, int cap);
+
+/* a6: DistributeOctTree (src/ORBextractor.cc:644-907), canonical tie-break.
+ * Input triples are relative to (minX, minY).  Writes the indices of the
+ * retained keypoints in output (list) order; returns the count, -1 if > cap. */
+int orbref_distribute(const int* xys, int n, int minX, int maxX, int minY, int maxY,
+                      int N, int* out_idx, int cap);
+
+/* a7: IC_Angle (src/ORBextractor.cc:84-128) + fastAtan2. */
+float orbref_fast_atan2(float y, float x);
+float orbref_ic_angle(const uint8_t* img, size_t step, int cx, int cy, const int* umax);
+
+/* a8: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) u8. */
+void orbref_gaussian_blur7(const uint8_t* src, int w, int h, size_t sstep,
+                           uint8_t* dst, size_t dstep);
+
+/* a9: computeOrbDescriptor (src/ORBextractor.cc:141-192), explicit FMA per F6. */
+void orbref_brief(const uint8_t* blur, size_t step, float kx, float ky, float angle_deg,
+                  uint8_t desc[32]);
+
+/* a2: ORBextractor::operator() (src/ORBextractor.cc:1248-1334).
+ * Returns 0 ok, 1 empty image (outputs untouched), -22 bad args, -28 cap too small.
+ * Optional stage dumps (may be NULL):
+ *   pyramid:       concatenation of the nlevels level images, each w_l*h_l bytes
+ *   level_counts:  keypoints retained per level
+ *   cand_counts:   FAST candidates (vToDistributeKeys.size()) per level */
+int orbref_extract(const orbref_params* p, const uint8_t* img, int rows, int cols, size_t step,
+                   orbref_keypoint* kps, int cap, uint8_t* desc, int* n_out,
+                   uint8_t* pyramid, int* level_counts, int* cand_counts);
+
+/* a11: ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1728-1744). */
+int orbref_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* a14: ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:417-588) with
+ * Frame::AssignFeaturesToGrid/PosInGrid/GetFeaturesInArea (src/Frame.cc:292-518)
+ * for an undistorted frame of size cols x rows (ComputeImageBounds, k1 == 0).
+ * prev_xy: vbPrevMatched (2*n1 floats), updated in place.  matches12: n1 ints.
+ * Returns nmatches. */
+int orbref_search_for_initialization(const orbref_keypoint* k1, const uint8_t* d1, int n1,
+                                     const orbref_keypoint* k2, const uint8_t* d2, int n2,
+                                     int cols, int rows, float* prev_xy, int* matches12,
+                                     int window, float nnratio, int check_ori);
+
+/* Config-5 brute force: per query best index (first min), best and second distance. */
+void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,
+                          int* best_idx, int* best_d, int* second_d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

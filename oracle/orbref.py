@@ -1,0 +1,232 @@
+"""ctypes binding of the CPU parity oracle (TEST INFRASTRUCTURE ONLY).
+
+Loaded by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg to
+check (never to produce) the MI355X results.  See orbref.h for what it
+restates and its parity status.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liborbref.so")
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+MAX_LEVELS = 16
+
+
+class Params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+class Tables(C.Structure):
+    _fields_ = [("nlevels", C.c_int), ("nfeatures", C.c_int),
+                ("scale", C.c_float * MAX_LEVELS), ("inv_scale", C.c_float * MAX_LEVELS),
+                ("sigma2", C.c_float * MAX_LEVELS), ("inv_sigma2", C.c_float * MAX_LEVELS),
+                ("nfeat_level", C.c_int * MAX_LEVELS), ("umax", C.c_int * 16)]
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(_LIB_PATH)
+        P = C.POINTER
+        u8p, i32p, f32p = P(C.c_uint8), P(C.c_int), P(C.c_float)
+        L.orbref_make_tables.argtypes = [P(Params), P(Tables)]
+        L.orbref_resize_linear.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_int, C.c_int, C.c_size_t]
+        L.orbref_fast.argtypes = [u8p, C.c_size_t, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
+        L.orbref_level_candidates.argtypes = [u8p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
+        L.orbref_distribute.argtypes = [i32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
+        L.orbref_fast_atan2.argtypes = [C.c_float, C.c_float]
+        L.orbref_fast_atan2.restype = C.c_float
+        L.orbref_ic_angle.argtypes = [u8p, C.c_size_t, C.c_int, C.c_int, i32p]
+        L.orbref_ic_angle.restype = C.c_float
+        L.orbref_gaussian_blur7.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_size_t]
+        L.orbref_brief.argtypes = [u8p, C.c_size_t, C.c_float, C.c_float, C.c_float, u8p]
+        L.orbref_extract.argtypes = [P(Params), u8p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
+                                     u8p, i32p, u8p, i32p, i32p]
+        L.orbref_descriptor_distance.argtypes = [u8p, u8p]
+        L.orbref_search_for_initialization.argtypes = [C.c_void_p, u8p, C.c_int, C.c_void_p, u8p, C.c_int,
+                                                       C.c_int, C.c_int, f32p, i32p, C.c_int, C.c_float, C.c_int]
+        L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
+        _lib = L
+    return _lib
+
+
+def _u8(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def _i32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def _f32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def make_params(nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7) -> Params:
+    return Params(nfeatures, scale_factor, nlevels, ini_th_fast, min_th_fast)
+
+
+def tables(p: Params) -> Tables:
+    t = Tables()
+    rc = lib().orbref_make_tables(C.byref(p), C.byref(t))
+    if rc != 0:
+        raise ValueError("bad params")
+    return t
+
+
+def level_sizes(p: Params, cols: int, rows: int):
+    t = tables(p)
+    out = []
+    for l in range(p.nlevels):
+        s = np.float32(t.inv_scale[l])
+        w = int(np.rint(np.float32(cols) * s))
+        h = int(np.rint(np.float32(rows) * s))
+        out.append((w, h))
+    return out
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    dst = np.empty((dh, dw), np.uint8)
+    lib().orbref_resize_linear(_u8(src), src.shape[1], src.shape[0], src.strides[0], _u8(dst), dw, dh, dw)
+    return dst
+
+
+def fast(roi: np.ndarray, threshold: int) -> np.ndarray:
+    roi = np.ascontiguousarray(roi, dtype=np.uint8)
+    cap = roi.size
+    out = np.empty((cap, 3), np.int32)
+    n = lib().orbref_fast(_u8(roi), roi.strides[0], roi.shape[0], roi.shape[1], threshold, _i32(out), cap)
+    assert n >= 0
+    return out[:n].copy()
+
+
+def level_candidates(level: np.ndarray, ini_th=20, min_th=7) -> np.ndarray:
+    level = np.ascontiguousarray(level, dtype=np.uint8)
+    cap = level.size // 2 + 16
+    out = np.empty((cap, 3), np.int32)
+    n = lib().orbref_level_candidates(_u8(level), level.strides[0], level.shape[1], level.shape[0],
+                                      ini_th, min_th, _i32(out), cap)
+    assert n >= 0
+    return out[:n].copy()
+
+
+def distribute(cands: np.ndarray, w: int, h: int, N: int) -> np.ndarray:
+    cands = np.ascontiguousarray(cands, dtype=np.int32)
+    cap = len(cands) + 8
+    out = np.empty(cap, np.int32)
+    n = lib().orbref_distribute(_i32(cands), len(cands), 16, w - 16, 16, h - 16, N, _i32(out), cap)
+    assert n >= 0
+    return out[:n].copy()
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return lib().orbref_fast_atan2(y, x)
+
+
+def ic_angle(img: np.ndarray, cx: int, cy: int, umax) -> float:
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    um = np.ascontiguousarray(np.asarray(list(umax), np.int32))
+    return lib().orbref_ic_angle(_u8(img), img.strides[0], cx, cy, _i32(um))
+
+
+def gaussian_blur7(img: np.ndarray) -> np.ndarray:
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    dst = np.empty_like(img)
+    lib().orbref_gaussian_blur7(_u8(img), img.shape[1], img.shape[0], img.strides[0], _u8(dst), dst.strides[0])
+    return dst
+
+
+def brief(blur: np.ndarray, x: float, y: float, angle: float) -> np.ndarray:
+    blur = np.ascontiguousarray(blur, dtype=np.uint8)
+    d = np.zeros(32, np.uint8)
+    lib().orbref_brief(_u8(blur), blur.strides[0], x, y, angle, _u8(d))
+    return d
+
+
+class ExtractResult:
+    def __init__(self, kps, desc, pyramid_levels, level_counts, cand_counts):
+        self.keypoints = kps
+        self.descriptors = desc
+        self.pyramid = pyramid_levels
+        self.level_counts = level_counts
+        self.cand_counts = cand_counts
+
+
+def extract(img: np.ndarray, p: Params, want_pyramid: bool = True) -> ExtractResult:
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    rows, cols = img.shape
+    sizes = level_sizes(p, cols, rows)
+    cap = p.nfeatures + 64 * p.nlevels + 64
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(0)
+    pyr = np.zeros(sum(w * h for w, h in sizes), np.uint8) if want_pyramid else None
+    lc = np.zeros(MAX_LEVELS, np.int32)
+    cc = np.zeros(MAX_LEVELS, np.int32)
+    rc = lib().orbref_extract(C.byref(p), _u8(img), rows, cols, img.strides[0], kps.ctypes.data, cap,
+                              _u8(desc), C.byref(n), _u8(pyr) if pyr is not None else None, _i32(lc), _i32(cc))
+    if rc != 0:
+        raise RuntimeError("orbref_extract failed: %d" % rc)
+    levels = None
+    if pyr is not None:
+        levels, o = [], 0
+        for w, h in sizes:
+            levels.append(pyr[o:o + w * h].reshape(h, w))
+            o += w * h
+    k = n.value
+    return ExtractResult(kps[:k].copy(), desc[:k].copy(), levels, lc[:p.nlevels].copy(), cc[:p.nlevels].copy())
+
+
+def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().orbref_descriptor_distance(_u8(a), _u8(b))
+
+
+def search_for_initialization(kps1, desc1, kps2, desc2, cols, rows, window=100, nnratio=0.9, check_ori=True,
+                              prev_xy=None):
+    kps1 = np.ascontiguousarray(kps1, KEYPOINT_DTYPE)
+    kps2 = np.ascontiguousarray(kps2, KEYPOINT_DTYPE)
+    desc1 = np.ascontiguousarray(desc1, np.uint8)
+    desc2 = np.ascontiguousarray(desc2, np.uint8)
+    n1, n2 = len(kps1), len(kps2)
+    if prev_xy is None:
+        prev_xy = np.stack([kps1["x"], kps1["y"]], axis=1).astype(np.float32)
+    prev_xy = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.full(max(n1, 1), -1, np.int32)
+    nm = lib().orbref_search_for_initialization(kps1.ctypes.data, _u8(desc1), n1, kps2.ctypes.data, _u8(desc2),
+                                                n2, cols, rows, _f32(prev_xy), _i32(m12), window, nnratio,
+                                                1 if check_ori else 0)
+    return nm, m12[:n1].copy(), prev_xy
+
+
+def allpairs_top2(q: np.ndarray, t: np.ndarray):
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    bi = np.empty(len(q), np.int32)
+    b1 = np.empty(len(q), np.int32)
+    b2 = np.empty(len(q), np.int32)
+    lib().orbref_allpairs_top2(_u8(q), len(q), _u8(t), len(t), _i32(bi), _i32(b1), _i32(b2))
+    return bi, b1, b2

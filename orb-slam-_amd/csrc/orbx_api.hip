@@ -1,0 +1,641 @@
+// liborbx C ABI (include/orbx.h): handle, geometry, workspace and launch
+// sequencing.  Host code; the kernels are in orbx_extract.hip / orbx_match.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/orbx.h"
+#include "orbx_kernels.hpp"
+
+using namespace orbx;
+
+namespace {
+
+inline int cv_round(float v) { return (int)std::lrint(v); }
+inline int cv_floor(float v) { int i = (int)v; return i - (i > v); }
+inline int cv_ceil(float v) { int i = (int)v; return i + (i < v); }
+
+struct Tables {
+    int nlevels = 0;
+    float scale[kMaxLevels], inv_scale[kMaxLevels], sigma2[kMaxLevels], inv_sigma2[kMaxLevels];
+    int nfeat[kMaxLevels];
+    int umax[16];
+};
+
+// ORBextractor::ORBextractor, src/ORBextractor.cc:466-540
+bool make_tables(const orbx_params& p, Tables& t)
+{
+    if (p.nlevels < 1 || p.nlevels > kMaxLevels || p.nfeatures < 0 || !(p.scale_factor > 1.0f)) return false;
+    t.nlevels = p.nlevels;
+    const double sf = (double)p.scale_factor;
+    t.scale[0] = 1.0f;
+    t.sigma2[0] = 1.0f;
+    for (int i = 1; i < p.nlevels; i++) {
+        t.scale[i] = (float)((double)t.scale[i - 1] * sf);
+        t.sigma2[i] = t.scale[i] * t.scale[i];
+    }
+    for (int i = 0; i < p.nlevels; i++) {
+        t.inv_scale[i] = 1.0f / t.scale[i];
+        t.inv_sigma2[i] = 1.0f / t.sigma2[i];
+    }
+    const float factor = (float)(1.0f / sf);
+    float desired = (float)p.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)p.nlevels));
+    int sum = 0;
+    for (int l = 0; l < p.nlevels - 1; l++) {
+        t.nfeat[l] = cv_round(desired);
+        sum += t.nfeat[l];
+        desired *= factor;
+    }
+    t.nfeat[p.nlevels - 1] = std::max(p.nfeatures - sum, 0);
+    const int vmax = cv_floor(15 * std::sqrt(2.f) / 2 + 1);
+    const int vmin = cv_ceil(15 * std::sqrt(2.f) / 2);
+    const double hp2 = 15 * 15;
+    for (int v = 0; v <= vmax; ++v) t.umax[v] = (int)std::lrint(std::sqrt(hp2 - v * v));
+    for (int v = 15, v0 = 0; v >= vmin; --v) {
+        while (t.umax[v0] == t.umax[v0 + 1]) ++v0;
+        t.umax[v] = v0;
+        ++v0;
+    }
+    return true;
+}
+
+short sat_s16(float v)
+{
+    const int i = cv_round(v);
+    return (short)std::min(std::max(i, -32768), 32767);
+}
+
+// cv::resize INTER_LINEAR coefficient tables: x: {x0 | x1<<16, a0 | a1<<16},
+// y: {y0 | y1<<16, b0 | b1<<16}
+void resize_tables(int sw, int sh, int dw, int dh, std::vector<int2>& xt, std::vector<int2>& yt)
+{
+    const double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+    const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        const int x1 = sx + 1 < sw ? sx + 1 : sw - 1;
+        const int a0 = sat_s16((1.f - fx) * 2048), a1 = sat_s16(fx * 2048);
+        xt.push_back(make_int2(sx | (x1 << 16), (a0 & 0xFFFF) | (a1 << 16)));
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor(fy);
+        fy -= sy;
+        const int b0 = sat_s16((1.f - fy) * 2048), b1 = sat_s16(fy * 2048);
+        const int y0 = std::min(std::max(sy, 0), sh - 1), y1 = std::min(std::max(sy + 1, 0), sh - 1);
+        yt.push_back(make_int2(y0 | (y1 << 16), (b0 & 0xFFFF) | (b1 << 16)));
+    }
+}
+
+template <class T>
+void dfree(T*& p)
+{
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+template <class T>
+bool dalloc(T*& p, size_t count)
+{
+    dfree(p);
+    if (count == 0) count = 1;
+    return hipMalloc((void**)&p, sizeof(T) * count) == hipSuccess;
+}
+
+}  // namespace
+
+struct orbx_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    orbx_params params{};
+    Tables tab;
+
+    // geometry (per rows x cols)
+    bool geom_ok = false;
+    int grows = -1, gcols = -1;
+    Geometry geom{};
+    std::vector<Cell> cells;
+    Geometry* d_geom = nullptr;
+    Cell* d_cells = nullptr;
+    int2* d_xtab = nullptr;
+    int2* d_ytab = nullptr;
+
+    // batch workspace
+    int batch_cap = 0;
+    uint8_t* d_pyr = nullptr;
+    uint32_t* d_slots = nullptr;
+    int* d_cell_counts = nullptr;
+    uint32_t* d_spill = nullptr;
+    uint32_t* d_spill_node = nullptr;
+    uint32_t* d_qt_out = nullptr;
+    int* d_qt_cnt = nullptr;
+    int* d_status = nullptr;
+
+    // host-image path
+    uint8_t* d_img = nullptr;
+    size_t img_bytes = 0;
+    int img_pitch = 0;
+    orbx_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int* d_counts = nullptr;
+    int single_cap = 0;
+
+    // last batch (for pyramid / debug readback)
+    FramePtrs last{};
+    int last_batch = 0;
+    std::vector<std::vector<uint8_t>> h_levels;
+    std::vector<bool> level_cached;
+
+    // timing
+    bool timing = false;
+    hipEvent_t ev[5] = {};
+    bool timed = false;
+};
+
+namespace {
+
+orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
+{
+    if (h->geom_ok && h->grows == rows && h->gcols == cols) return ORBX_OK;
+    if (rows <= 0 || cols <= 0 || rows > kMaxDim || cols > kMaxDim) return ORBX_EINVAL;
+    const Tables& t = h->tab;
+    Geometry g{};
+    g.rows = rows;
+    g.cols = cols;
+    g.nlevels = t.nlevels;
+    g.ini_th = std::min(std::max(h->params.ini_th_fast, 0), 255);
+    g.min_th = std::min(std::max(h->params.min_th_fast, 0), 255);
+    std::memcpy(g.umax, t.umax, sizeof(g.umax));
+    std::vector<Cell> cells;
+    std::vector<int2> xt, yt;
+    long long pyr = 0;
+    int slot = 0, out = 0, maxcells = 1, lcap = 8;
+    int prev_w = cols, prev_h = rows;
+    for (int l = 0; l < t.nlevels; ++l) {
+        LevelGeom& L = g.lv[l];
+        // src/ORBextractor.cc:1347-1348
+        L.w = cv_round((float)cols * t.inv_scale[l]);
+        L.h = cv_round((float)rows * t.inv_scale[l]);
+        L.pitch = (L.w + 63) & ~63;
+        if (l > 0) {
+            L.pyr_off = pyr;
+            pyr += (long long)L.pitch * L.h;
+            L.xtab_off = (int)xt.size();
+            L.ytab_off = (int)yt.size();
+            resize_tables(prev_w, prev_h, L.w, L.h, xt, yt);
+        }
+        prev_w = L.w;
+        prev_h = L.h;
+        // FAST cell grid, src/ORBextractor.cc:932-972
+        const int minB = kMinBorder;
+        const int maxBX = L.w - kEdge + 3, maxBY = L.h - kEdge + 3;
+        const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+        const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
+        if (nCols <= 0 || nRows <= 0) return ORBX_EINVAL;
+        const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+        L.cell_begin = (int)cells.size();
+        L.slot_begin = slot;
+        for (int i = 0; i < nRows; i++) {
+            const float iniY = (float)(minB + i * hCell);
+            float maxY = iniY + hCell + 6;
+            if (iniY >= maxBY - 3) continue;
+            if (maxY > maxBY) maxY = (float)maxBY;
+            for (int j = 0; j < nCols; j++) {
+                const float iniX = (float)(minB + j * wCell);
+                float maxX = iniX + wCell + 6;
+                if (iniX >= maxBX - 6) continue;
+                if (maxX > maxBX) maxX = (float)maxBX;
+                Cell c{};
+                c.level = (int16_t)l;
+                c.roi_x0 = (int)iniX;
+                c.roi_y0 = (int)iniY;
+                c.roi_w = (int16_t)((int)maxX - (int)iniX);
+                c.roi_h = (int16_t)((int)maxY - (int)iniY);
+                if (c.roi_w > 66 || c.roi_h > 66) return ORBX_EINVAL;
+                const int dw = c.roi_w - 6, dh = c.roi_h - 6;
+                c.slot_base = slot;
+                c.slot_cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
+                slot += c.slot_cap;
+                cells.push_back(c);
+            }
+        }
+        L.ncells = (int)cells.size() - L.cell_begin;
+        L.slot_cap = slot - L.slot_begin;
+        maxcells = std::max(maxcells, L.ncells);
+        // DistributeOctTree roots, src/ORBextractor.cc:650-653
+        L.qw = L.w - 2 * kMinBorder;
+        L.qh = L.h - 2 * kMinBorder;
+        L.nIni = (int)std::round((float)L.qw / L.qh);
+        if (L.nIni <= 0) return ORBX_EINVAL;
+        L.hX = (float)L.qw / L.nIni;
+        L.nfeat = t.nfeat[l];
+        L.cap = std::max(L.nfeat + 2, 4 * L.nIni);
+        L.out_off = out;
+        out += L.cap;
+        lcap = std::max(lcap, L.cap + 4);
+        L.scale = t.scale[l];
+        L.patch_size = (float)(int)(31 * t.scale[l]);   // :1013
+    }
+    g.ncells = (int)cells.size();
+    g.slots_per_frame = slot;
+    g.out_per_frame = out;
+    g.max_cells_level = maxcells;
+    g.lcap = lcap;
+    g.pyr_bytes = (pyr + 255) & ~255LL;
+    int spill = 0;
+    for (int l = 0; l < t.nlevels; ++l) spill += std::max(0, g.lv[l].slot_cap - 512 * 24);
+    g.spill_per_frame = std::max(spill, 1);
+    if (lcap >= 65535 || quadtree_smem_bytes(g) > 160 * 1024) return ORBX_EINVAL;
+
+    hipSetDevice(h->device);
+    if (!dalloc(h->d_geom, 1) || !dalloc(h->d_cells, cells.size()) || !dalloc(h->d_xtab, xt.size()) ||
+        !dalloc(h->d_ytab, yt.size()))
+        return ORBX_ENOMEM;
+    hipMemcpy(h->d_geom, &g, sizeof(g), hipMemcpyHostToDevice);
+    hipMemcpy(h->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice);
+    if (!xt.empty()) hipMemcpy(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice);
+    if (!yt.empty()) hipMemcpy(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice);
+    h->geom = g;
+    h->cells = std::move(cells);
+    h->grows = rows;
+    h->gcols = cols;
+    h->geom_ok = true;
+    h->batch_cap = 0;   // force workspace re-allocation
+    h->single_cap = 0;
+    return ORBX_OK;
+}
+
+orbx_status ensure_batch(orbx_handle* h, int batch)
+{
+    if (batch <= h->batch_cap) return ORBX_OK;
+    const Geometry& g = h->geom;
+    const size_t B = (size_t)batch;
+    if (!dalloc(h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h->d_slots, (size_t)g.slots_per_frame * B) ||
+        !dalloc(h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h->d_spill, (size_t)g.spill_per_frame * B) ||
+        !dalloc(h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h->d_qt_out, (size_t)g.out_per_frame * B) ||
+        !dalloc(h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h->d_status, 1)) {
+        h->batch_cap = 0;
+        return ORBX_ENOMEM;
+    }
+    h->batch_cap = batch;
+    return ORBX_OK;
+}
+
+ExtractBufs bufs(orbx_handle* h)
+{
+    ExtractBufs b;
+    b.geom = h->d_geom;
+    b.cells = h->d_cells;
+    b.xtab = h->d_xtab;
+    b.ytab = h->d_ytab;
+    b.slots = h->d_slots;
+    b.cell_counts = h->d_cell_counts;
+    b.spill = h->d_spill;
+    b.spill_node = h->d_spill_node;
+    b.qt_out = h->d_qt_out;
+    b.qt_cnt = h->d_qt_cnt;
+    b.status = h->d_status;
+    return b;
+}
+
+orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoint* kps, uint8_t* desc,
+                         int* counts, int cap, hipStream_t s)
+{
+    const Geometry& g = h->geom;
+    ExtractBufs b = bufs(h);
+    hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
+    hipMemsetAsync(h->d_status, 0, sizeof(int), s);
+    if (h->timing) hipEventRecord(h->ev[0], s);
+    launch_pyramid(g, b, P, batch, s);
+    if (h->timing) hipEventRecord(h->ev[1], s);
+    launch_fast(g, b, P, batch, s);
+    if (h->timing) hipEventRecord(h->ev[2], s);
+    launch_quadtree(g, b, counts, batch, s);
+    if (h->timing) hipEventRecord(h->ev[3], s);
+    launch_describe(g, b, P, kps, desc, cap, batch, s);
+    if (h->timing) hipEventRecord(h->ev[4], s);
+    h->timed = h->timing;
+    h->last = P;
+    h->last_batch = batch;
+    std::fill(h->level_cached.begin(), h->level_cached.end(), false);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+orbx_status status_from_device(orbx_handle* h)
+{
+    int st = 0;
+    if (hipMemcpyAsync(&st, h->d_status, sizeof(int), hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+        return ORBX_EDEVICE;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBX_EDEVICE;
+    if (st & kStatusCapOverflow) return ORBX_ENOSPC;
+    if (st) return ORBX_EDEVICE;
+    return ORBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+orbx_status orbx_create(const orbx_params* params, int device, orbx_handle** out)
+{
+    if (!params || !out) return ORBX_EINVAL;
+    *out = nullptr;
+    orbx_handle* h = new (std::nothrow) orbx_handle();
+    if (!h) return ORBX_ENOMEM;
+    h->params = *params;
+    if (!make_tables(*params, h->tab)) {
+        delete h;
+        return ORBX_EINVAL;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        delete h;
+        return ORBX_EDEVICE;
+    }
+    h->device = device;
+    hipSetDevice(device);
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return ORBX_EDEVICE;
+    }
+    for (auto& e : h->ev) hipEventCreate(&e);
+    h->h_levels.resize(kMaxLevels);
+    h->level_cached.assign(kMaxLevels, false);
+    *out = h;
+    return ORBX_OK;
+}
+
+void orbx_destroy(orbx_handle* h)
+{
+    if (!h) return;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    dfree(h->d_geom);
+    dfree(h->d_cells);
+    dfree(h->d_xtab);
+    dfree(h->d_ytab);
+    dfree(h->d_pyr);
+    dfree(h->d_slots);
+    dfree(h->d_cell_counts);
+    dfree(h->d_spill);
+    dfree(h->d_spill_node);
+    dfree(h->d_qt_out);
+    dfree(h->d_qt_cnt);
+    dfree(h->d_status);
+    dfree(h->d_img);
+    dfree(h->d_kps);
+    dfree(h->d_desc);
+    dfree(h->d_counts);
+    for (auto& e : h->ev)
+        if (e) hipEventDestroy(e);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+}
+
+orbx_status orbx_get_tables(const orbx_handle* h, int* nlevels, float* scale_factor, float* scale, float* inv_scale,
+                            float* sigma2, float* inv_sigma2, int* features_per_level)
+{
+    if (!h) return ORBX_EINVAL;
+    const Tables& t = h->tab;
+    if (nlevels) *nlevels = t.nlevels;
+    if (scale_factor) *scale_factor = h->params.scale_factor;
+    for (int l = 0; l < t.nlevels; ++l) {
+        if (scale) scale[l] = t.scale[l];
+        if (inv_scale) inv_scale[l] = t.inv_scale[l];
+        if (sigma2) sigma2[l] = t.sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = t.inv_sigma2[l];
+        if (features_per_level) features_per_level[l] = t.nfeat[l];
+    }
+    return ORBX_OK;
+}
+
+int orbx_capacity(const orbx_handle* h, int rows, int cols)
+{
+    if (!h) return -1;
+    orbx_handle* m = const_cast<orbx_handle*>(h);
+    if (ensure_geometry(m, rows, cols) != ORBX_OK) return -1;
+    return m->geom.out_per_frame;
+}
+
+orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols, size_t step, orbx_keypoint* kps,
+                         int cap, uint8_t* desc, int* n_out)
+{
+    if (!h || !n_out) return ORBX_EINVAL;
+    if (!img || rows <= 0 || cols <= 0) return ORBX_EMPTY;   // src/ORBextractor.cc:1252
+    if (step < (size_t)cols || !kps || !desc || cap < 0) return ORBX_EINVAL;
+    hipSetDevice(h->device);
+    orbx_status st = ensure_geometry(h, rows, cols);
+    if (st != ORBX_OK) return st;
+    if ((st = ensure_batch(h, 1)) != ORBX_OK) return st;
+    const int pitch = (cols + 63) & ~63;
+    const size_t need = (size_t)pitch * rows;
+    if (need > h->img_bytes) {
+        if (!dalloc(h->d_img, need)) return ORBX_ENOMEM;
+        h->img_bytes = need;
+    }
+    const int ocap = h->geom.out_per_frame;
+    if (ocap > h->single_cap) {
+        if (!dalloc(h->d_kps, ocap) || !dalloc(h->d_desc, (size_t)ocap * 32) || !dalloc(h->d_counts, 1))
+            return ORBX_ENOMEM;
+        h->single_cap = ocap;
+    }
+    hipStream_t s = h->stream;
+    hipMemcpy2DAsync(h->d_img, pitch, img, step, cols, rows, hipMemcpyHostToDevice, s);
+    FramePtrs P{h->d_img, need, pitch, h->d_pyr, (size_t)h->geom.pyr_bytes};
+    st = run_pipeline(h, P, 1, h->d_kps, h->d_desc, h->d_counts, ocap, s);
+    if (st != ORBX_OK) return st;
+    int n = 0;
+    hipMemcpyAsync(&n, h->d_counts, sizeof(int), hipMemcpyDeviceToHost, s);
+    if ((st = status_from_device(h)) != ORBX_OK) return st;
+    if (n > cap) return ORBX_ENOSPC;
+    if (n > 0) {
+        hipMemcpyAsync(kps, h->d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(desc, h->d_desc, (size_t)n * 32, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    }
+    *n_out = n;
+    return ORBX_OK;
+}
+
+orbx_status orbx_get_level(orbx_handle* h, int level, const uint8_t** data, int* rows, int* cols, size_t* step)
+{
+    if (!h || !h->geom_ok || h->last_batch <= 0 || level < 0 || level >= h->geom.nlevels) return ORBX_EINVAL;
+    const LevelGeom& L = h->geom.lv[level];
+    if (!h->level_cached[level]) {
+        std::vector<uint8_t>& v = h->h_levels[level];
+        v.resize((size_t)L.w * L.h);
+        const uint8_t* src;
+        size_t sp;
+        if (level == 0) {
+            src = h->last.in;
+            sp = (size_t)h->last.in_pitch;
+        } else {
+            src = h->last.pyr + L.pyr_off;
+            sp = (size_t)L.pitch;
+        }
+        if (hipMemcpy2DAsync(v.data(), L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess)
+            return ORBX_EDEVICE;
+        h->level_cached[level] = true;
+    }
+    if (data) *data = h->h_levels[level].data();
+    if (rows) *rows = L.h;
+    if (cols) *cols = L.w;
+    if (step) *step = (size_t)L.w;
+    return ORBX_OK;
+}
+
+orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int batch, int rows, int cols,
+                                      size_t step, size_t frame_stride, orbx_keypoint* d_kps, uint8_t* d_desc,
+                                      int* d_counts, int cap, void* stream)
+{
+    if (!h || !d_imgs || batch <= 0 || !d_kps || !d_desc || !d_counts || cap <= 0) return ORBX_EINVAL;
+    if (step < (size_t)cols || frame_stride < step * (size_t)rows) return ORBX_EINVAL;
+    hipSetDevice(h->device);
+    orbx_status st = ensure_geometry(h, rows, cols);
+    if (st != ORBX_OK) return st;
+    if ((st = ensure_batch(h, batch)) != ORBX_OK) return st;
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    FramePtrs P{d_imgs, frame_stride, (int)step, h->d_pyr, (size_t)h->geom.pyr_bytes};
+    return run_pipeline(h, P, batch, d_kps, d_desc, d_counts, cap, s);
+}
+
+orbx_status orbx_sync(orbx_handle* h, void* stream)
+{
+    if (!h) return ORBX_EINVAL;
+    hipSetDevice(h->device);
+    if (stream && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return ORBX_EDEVICE;
+    if (!h->d_status) return ORBX_OK;
+    return status_from_device(h);
+}
+
+orbx_status orbx_set_timing(orbx_handle* h, int enable)
+{
+    if (!h) return ORBX_EINVAL;
+    h->timing = enable != 0;
+    return ORBX_OK;
+}
+
+orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n)
+{
+    if (!h || !ms || !h->timed) return ORBX_EINVAL;
+    if (hipEventSynchronize(h->ev[4]) != hipSuccess) return ORBX_EDEVICE;
+    for (int i = 0; i < n && i < 4; ++i) hipEventElapsedTime(&ms[i], h->ev[i], h->ev[i + 1]);
+    return ORBX_OK;
+}
+
+orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t out_size)
+{
+    if (!h || !out || frame < 0 || frame >= h->last_batch) return ORBX_EINVAL;
+    hipSetDevice(h->device);
+    size_t o = 0;
+    for (int l = 0; l < h->geom.nlevels; ++l) {
+        const LevelGeom& L = h->geom.lv[l];
+        if (o + (size_t)L.w * L.h > out_size) return ORBX_ENOSPC;
+        const uint8_t* src;
+        size_t sp;
+        if (l == 0) {
+            src = h->last.in + (size_t)frame * h->last.in_fstride;
+            sp = (size_t)h->last.in_pitch;
+        } else {
+            src = h->last.pyr + (size_t)frame * h->last.pyr_fstride + L.pyr_off;
+            sp = (size_t)L.pitch;
+        }
+        hipMemcpy2DAsync(out + o, L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, h->stream);
+        o += (size_t)L.w * L.h;
+    }
+    return hipStreamSynchronize(h->stream) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys, int cap, int* n)
+{
+    if (!h || !n || frame < 0 || frame >= h->last_batch || level < 0 || level >= h->geom.nlevels) return ORBX_EINVAL;
+    hipSetDevice(h->device);
+    const Geometry& g = h->geom;
+    std::vector<int> cnt(g.ncells);
+    std::vector<uint32_t> sl(g.slots_per_frame);
+    hipMemcpyAsync(cnt.data(), h->d_cell_counts + (size_t)frame * g.ncells, sizeof(int) * g.ncells,
+                   hipMemcpyDeviceToHost, h->stream);
+    hipMemcpyAsync(sl.data(), h->d_slots + (size_t)frame * g.slots_per_frame, sizeof(uint32_t) * g.slots_per_frame,
+                   hipMemcpyDeviceToHost, h->stream);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBX_EDEVICE;
+    const LevelGeom& L = g.lv[level];
+    int k = 0;
+    for (int c = L.cell_begin; c < L.cell_begin + L.ncells; ++c) {
+        for (int i = 0; i < cnt[c]; ++i) {
+            const uint32_t v = sl[h->cells[c].slot_base + i];
+            if (k < cap && xys) {
+                xys[3 * k] = (int)(v & 0xFFF);
+                xys[3 * k + 1] = (int)((v >> 12) & 0xFFF);
+                xys[3 * k + 2] = (int)(v >> 24);
+            }
+            ++k;
+        }
+    }
+    *n = k;
+    return k > cap ? ORBX_ENOSPC : ORBX_OK;
+}
+
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b)
+{
+    int d = 0;
+    for (int i = 0; i < 4; ++i) {
+        uint64_t x, y;
+        std::memcpy(&x, a + 8 * i, 8);
+        std::memcpy(&y, b + 8 * i, 8);
+        d += __builtin_popcountll(x ^ y);
+    }
+    return d;
+}
+
+orbx_status orbm_allpairs_device(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int mode, int* d_best_idx,
+                                 int* d_best, int* d_second, uint16_t* d_full, void* stream)
+{
+    if (!d_q || !d_t || nq < 0 || nt < 0) return ORBX_EINVAL;
+    if (nq == 0 || nt == 0) return ORBX_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (mode == ORBM_TOP2) {
+        if (!d_best_idx || !d_best || !d_second) return ORBX_EINVAL;
+        int nsplit = std::max(1, std::min(64, (256 * 4) / std::max(1, (nq + 255) / 256)));
+        nsplit = std::min(nsplit, (nt + 255) / 256);
+        int* part = nullptr;
+        if (hipMallocAsync((void**)&part, sizeof(int) * 3 * (size_t)nq * nsplit, s) != hipSuccess) return ORBX_ENOMEM;
+        launch_allpairs_top2(d_q, nq, d_t, nt, d_best_idx, d_best, d_second, part, nsplit, s);
+        hipFreeAsync(part, s);
+    } else if (mode == ORBM_FULL_U16) {
+        if (!d_full) return ORBX_EINVAL;
+        launch_allpairs_full(d_q, nq, d_t, nt, d_full, s);
+    } else {
+        return ORBX_EINVAL;
+    }
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const int* d_counts,
+                                          int cap, const int* d_pair_a, const int* d_pair_b, int npairs, int rows,
+                                          int cols, int window, float nnratio, int check_ori, int* d_matches12,
+                                          int* d_nmatches, void* stream)
+{
+    if (!d_kps || !d_desc || !d_counts || cap <= 0 || cap > 65535 || npairs < 0 || rows <= 0 || cols <= 0)
+        return ORBX_EINVAL;
+    if (npairs == 0) return ORBX_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int per = std::max(65536, 48 * cap);
+    uint32_t* cand = nullptr;
+    if (hipMallocAsync((void**)&cand, sizeof(uint32_t) * (size_t)per * npairs, s) != hipSuccess) return ORBX_ENOMEM;
+    launch_search_init(d_kps, d_desc, d_counts, cap, d_pair_a, d_pair_b, npairs, rows, cols, window, nnratio,
+                       check_ori, cand, per, d_matches12, d_nmatches, s);
+    hipFreeAsync(cand, s);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+}  // extern "C"

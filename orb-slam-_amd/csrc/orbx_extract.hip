@@ -1,0 +1,849 @@
+// gfx950 kernels of the ORB extractor (ORB_SLAM2::ORBextractor::operator(),
+// src/ORBextractor.cc:1248-1334).  Integer/bitwise path: no MFMA.
+//
+//   K1 k_pyramid_level  ComputePyramid, src/ORBextractor.cc:1342-1377
+//   K2 k_fast_cells     per-cell FAST-9 + NMS + threshold retry, :952-1000
+//   K3 k_quadtree       DistributeOctTree, :644-907 (one workgroup per frame x level)
+//   K4 k_describe       IC_Angle + GaussianBlur + rBRIEF + scale/pack,
+//                       :84-128, :1300-1332, :141-192
+#include <hip/hip_runtime.h>
+
+#include "orbx_kernels.hpp"
+#include "orbx_math.hpp"
+
+namespace orbx {
+
+__constant__ int c_pattern[1024] = {
+#include "orb_pattern.inc"
+};
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lanes_below(unsigned long long mask)
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ const uint8_t* level_base(const FramePtrs& P, const Geometry* G, int f, int l,
+                                                     int& pitch)
+{
+    if (l == 0) {
+        pitch = P.in_pitch;
+        return P.in + (size_t)f * P.in_fstride;
+    }
+    pitch = G->lv[l].pitch;
+    return P.pyr + (size_t)f * P.pyr_fstride + G->lv[l].pyr_off;
+}
+
+// ---------------------------------------------------------------------------
+// K1: level l from level l-1, cv::resize INTER_LINEAR u8 fixed point
+// (11-bit coefficients, 22-bit vertical rounding) — SURVEY.md A.2.
+// Coefficient tables are built on the host exactly like OpenCV builds them.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
+                                                       const int2* __restrict__ xtab,
+                                                       const int2* __restrict__ ytab)
+{
+    const int f = blockIdx.z, dy = blockIdx.y;
+    const LevelGeom& D = G->lv[l];
+    int spitch;
+    const uint8_t* src = level_base(P, G, f, l - 1, spitch);
+    uint8_t* dst = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy * D.pitch;
+    const int2 yt = ytab[D.ytab_off + dy];
+    const uint8_t* r0 = src + (size_t)(yt.x & 0xFFFF) * spitch;
+    const uint8_t* r1 = src + (size_t)((uint32_t)yt.x >> 16) * spitch;
+    const int b0 = yt.y & 0xFFFF, b1 = (int)((uint32_t)yt.y >> 16);
+    for (int dx = blockIdx.x * 256 + threadIdx.x; dx < D.w; dx += gridDim.x * 256) {
+        const int2 xt = xtab[D.xtab_off + dx];
+        const int x0 = xt.x & 0xFFFF, x1 = (int)((uint32_t)xt.x >> 16);
+        const int a0 = xt.y & 0xFFFF, a1 = (int)((uint32_t)xt.y >> 16);
+        const int h0 = r0[x0] * a0 + r0[x1] * a1;
+        const int h1 = r1[x0] * a0 + r1[x1] * a1;
+        const int v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+        dst[dx] = (uint8_t)(v > 255 ? 255 : v);
+    }
+}
+
+void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
+{
+    for (int l = 1; l < g.nlevels; ++l) {
+        const int w = g.lv[l].w, h = g.lv[l].h;
+        dim3 grid((w + 255) / 256, h, batch);
+        hipLaunchKernelGGL(k_pyramid_level, grid, dim3(256), 0, s, b.geom, p, l, b.xtab, b.ytab);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2: FAST-9/16 on one cell ROI per wave (cv::FAST(roi, kps, th, true)).
+// s = max(A, -B) with A = max over 9-arcs of min(v - ring), B = min of max:
+// a pixel is a corner at t iff s > t, and cornerScore = s - 1.
+// NMS is evaluated inside the cell with scores masked by the cell threshold;
+// the cell falls back to minThFAST iff NMS at iniThFAST keeps nothing
+// (src/ORBextractor.cc:982-987).  Survivors are emitted row-major, i.e. in
+// OpenCV's emission order.
+// ---------------------------------------------------------------------------
+constexpr int kRoiMax = 66;
+constexpr int kTileP = 68;
+constexpr int kMapMax = (kRoiMax - 4) * (kRoiMax - 4);
+
+__device__ __forceinline__ int fast_strength(const uint8_t* c, int st)
+{
+    const int v = c[0];
+    int d[16];
+    d[0] = v - c[3 * st];
+    d[1] = v - c[3 * st + 1];
+    d[2] = v - c[2 * st + 2];
+    d[3] = v - c[st + 3];
+    d[4] = v - c[3];
+    d[5] = v - c[-st + 3];
+    d[6] = v - c[-2 * st + 2];
+    d[7] = v - c[-3 * st + 1];
+    d[8] = v - c[-3 * st];
+    d[9] = v - c[-3 * st - 1];
+    d[10] = v - c[-2 * st - 2];
+    d[11] = v - c[-st - 3];
+    d[12] = v - c[-3];
+    d[13] = v - c[st - 3];
+    d[14] = v - c[2 * st - 2];
+    d[15] = v - c[3 * st - 1];
+    int mn[16], mx[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mn[k] = min(d[k], d[(k + 1) & 15]);
+        mx[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mn4[k] = min(mn[k], mn[(k + 2) & 15]);
+        mx4[k] = max(mx[k], mx[(k + 2) & 15]);
+    }
+    int A = -1000, B = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int m8 = min(mn4[k], mn4[(k + 4) & 15]);
+        const int M8 = max(mx4[k], mx4[(k + 4) & 15]);
+        A = max(A, min(m8, d[(k + 8) & 15]));
+        B = min(B, max(M8, d[(k + 8) & 15]));
+    }
+    return max(A, -B);
+}
+
+__device__ __forceinline__ bool nms_keep(const uint8_t* m, int p, int W2, int t)
+{
+    const int s = m[p];
+    if (s <= t) return false;
+    const int sc = s - 1;
+    const int nb[8] = {m[p - W2 - 1], m[p - W2], m[p - W2 + 1], m[p - 1],
+                       m[p + 1],      m[p + W2 - 1], m[p + W2], m[p + W2 + 1]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int mm = nb[k] > t ? nb[k] - 1 : 0;
+        if (!(sc > mm)) return false;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
+                                                    const Cell* __restrict__ cells,
+                                                    uint32_t* __restrict__ slots,
+                                                    int* __restrict__ cell_counts)
+{
+    __shared__ uint8_t s_tile[4][kRoiMax * kTileP];
+    __shared__ uint8_t s_map[4][kMapMax];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int c = blockIdx.x * 4 + wave;
+    if (c >= G->ncells) return;   // wave-uniform; no block barriers below
+    const Cell C = cells[c];
+    int pitch;
+    const uint8_t* img = level_base(P, G, f, C.level, pitch);
+    uint8_t* tile = s_tile[wave];
+    uint8_t* map = s_map[wave];
+    const int rw = C.roi_w, rh = C.roi_h;
+    const int dw = rw - 6, dh = rh - 6;
+    int* out_count = cell_counts + (size_t)f * G->ncells + c;
+    if (dw <= 0 || dh <= 0) {
+        if (lane == 0) *out_count = 0;
+        return;
+    }
+    const uint8_t* src = img + (size_t)C.roi_y0 * pitch + C.roi_x0;
+    for (int i = lane; i < rw * rh; i += 64) {
+        const int r = i / rw, q = i - r * rw;
+        tile[r * kTileP + q] = src[(size_t)r * pitch + q];
+    }
+    const int W2 = dw + 2;
+    for (int i = lane; i < W2 * (dh + 2); i += 64) map[i] = 0;
+    wave_lds_sync();
+
+    const int npx = dw * dh;
+    for (int k = lane; k < npx; k += 64) {
+        const int ii = k / dw, jj = k - ii * dw;
+        const int s = fast_strength(tile + (ii + 3) * kTileP + (jj + 3), kTileP);
+        map[(ii + 1) * W2 + jj + 1] = (uint8_t)(s > 0 ? s : 0);
+    }
+    wave_lds_sync();
+
+    const int rounds = (npx + 63) >> 6;
+    int t = G->ini_th;
+    int kept = 0;
+    for (int r = 0; r < rounds; ++r) {
+        const int k = lane + (r << 6);
+        bool keep = false;
+        if (k < npx) {
+            const int ii = k / dw, jj = k - ii * dw;
+            keep = nms_keep(map, (ii + 1) * W2 + jj + 1, W2, t);
+        }
+        kept += __popcll(__ballot(keep));
+    }
+    if (kept == 0) t = G->min_th;
+
+    uint32_t* out = slots + (size_t)f * G->slots_per_frame + C.slot_base;
+    const int xr0 = C.roi_x0 + 3 - kMinBorder, yr0 = C.roi_y0 + 3 - kMinBorder;
+    int base = 0;
+    for (int r = 0; r < rounds; ++r) {
+        const int k = lane + (r << 6);
+        bool keep = false;
+        int ii = 0, jj = 0, p = 0;
+        if (k < npx) {
+            ii = k / dw;
+            jj = k - ii * dw;
+            p = (ii + 1) * W2 + jj + 1;
+            keep = nms_keep(map, p, W2, t);
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+            const int idx = base + lanes_below(m);
+            out[idx] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + ii), (uint32_t)(map[p] - 1));
+        }
+        base += __popcll(m);
+    }
+    if (lane == 0) *out_count = base;
+}
+
+void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
+{
+    dim3 grid((g.ncells + 3) / 4, batch);
+    hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, s, b.geom, p, b.cells, b.slots, b.cell_counts);
+}
+
+// ---------------------------------------------------------------------------
+// K3: DistributeOctTree (src/ORBextractor.cc:644-907), one workgroup per
+// (frame, level).  Keypoints stay in registers (KPT per thread, overflow in a
+// global spill array) and carry the list position of their node; nodes live in
+// LDS arrays indexed by list position and are renumbered every round, so the
+// std::list push_front/erase order is reproduced with prefix sums:
+//   after a round the list is [children of the last split node (n4..n1), ...,
+//   children of the first split node, surviving nodes in their old order].
+// The phase-2 size sort breaks ties by creation order (canonical; the
+// reference uses heap addresses).
+// ---------------------------------------------------------------------------
+constexpr int QT_NT = 512;
+constexpr int QT_KPT = 24;
+constexpr int QT_NW = QT_NT / 64;
+constexpr uint16_t kNone = 0xFFFF;
+
+__device__ uint32_t block_scan_excl(uint32_t* a, int n, uint32_t* wsum)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int per = (n + QT_NT - 1) / QT_NT;
+    const int b = tid * per, e = min(n, b + per);
+    uint32_t local = 0;
+    for (int i = b; i < e; ++i) local += a[i];
+    uint32_t inc = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int w = 0; w < QT_NW; ++w) {
+            const uint32_t t = wsum[w];
+            wsum[w] = run;
+            run += t;
+        }
+        wsum[QT_NW] = run;
+    }
+    __syncthreads();
+    uint32_t run = wsum[wid] + inc - local;
+    for (int i = b; i < e; ++i) {
+        const uint32_t t = a[i];
+        a[i] = run;
+        run += t;
+    }
+    const uint32_t total = wsum[QT_NW];
+    __syncthreads();
+    return total;
+}
+
+__device__ void block_bitonic_desc(uint32_t* k, int p2)
+{
+    for (int size = 2; size <= p2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < (p2 >> 1); i += QT_NT) {
+                const int lo = 2 * i - (i & (stride - 1));
+                const int hi = lo + stride;
+                const bool desc = (lo & size) == 0;
+                const uint32_t a = k[lo], b = k[hi];
+                if ((a < b) == desc) {
+                    k[lo] = b;
+                    k[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ int next_pow2(int v)
+{
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+struct QtLayout {
+    size_t scan, rect, cnt, srank, npos, snode, smx, smy, ccnt, cpos, vprev, vnew, skey, best, wsum, sh, total;
+};
+
+__host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap)
+{
+    QtLayout L;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += (bytes + 15) & ~(size_t)15;
+        return r;
+    };
+    int p2 = 1;
+    while (p2 < lcap) p2 <<= 1;
+    const int scan_n = (4 * lcap > cellcap ? 4 * lcap : cellcap) + 1;
+    L.scan = take(sizeof(uint32_t) * scan_n);
+    L.rect = take(sizeof(int16_t) * 4 * 2 * lcap);   // [2 buffers][4 coords][lcap]
+    L.cnt = take(sizeof(uint32_t) * 2 * lcap);
+    L.srank = take(sizeof(uint16_t) * lcap);
+    L.npos = take(sizeof(uint16_t) * lcap);
+    L.snode = take(sizeof(uint16_t) * lcap);
+    L.smx = take(sizeof(int16_t) * lcap);
+    L.smy = take(sizeof(int16_t) * lcap);
+    L.ccnt = take(sizeof(uint32_t) * 4 * lcap);
+    L.cpos = take(sizeof(uint16_t) * 4 * lcap);
+    L.vprev = take(sizeof(uint16_t) * lcap);
+    L.vnew = take(sizeof(uint16_t) * lcap);
+    L.skey = take(sizeof(uint32_t) * p2);
+    L.best = take(sizeof(unsigned long long) * lcap);
+    L.wsum = take(sizeof(uint32_t) * (QT_NW + 1));
+    L.sh = take(sizeof(int) * 16);
+    L.total = o;
+    return L;
+}
+
+size_t quadtree_smem_bytes(const Geometry& g) { return qt_layout(g.lcap, g.max_cells_level).total; }
+
+// shared scalar slots
+enum { SH_N = 0, SH_L, SH_PHASE, SH_M, SH_DONE, SH_KK, SH_ERR, SH_S, SH_C, SH_NEWL };
+
+__global__ __launch_bounds__(QT_NT) void k_quadtree(const Geometry* __restrict__ G,
+                                                   const Cell* __restrict__ cells,
+                                                   const uint32_t* __restrict__ slots,
+                                                   const int* __restrict__ cell_counts,
+                                                   uint32_t* __restrict__ spill,
+                                                   uint32_t* __restrict__ spill_node,
+                                                   uint32_t* __restrict__ qt_out, int* __restrict__ qt_cnt,
+                                                   int* __restrict__ frame_counts, int* __restrict__ status)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int l = blockIdx.x, f = blockIdx.y;
+    const int tid = threadIdx.x;
+    const LevelGeom& LG = G->lv[l];
+    const int lcap = G->lcap;
+    const QtLayout Ly = qt_layout(lcap, G->max_cells_level);
+    uint32_t* scan = (uint32_t*)(smem + Ly.scan);
+    int16_t* rect = (int16_t*)(smem + Ly.rect);
+    uint32_t* cntb = (uint32_t*)(smem + Ly.cnt);
+    uint16_t* srank = (uint16_t*)(smem + Ly.srank);
+    uint16_t* npos = (uint16_t*)(smem + Ly.npos);
+    uint16_t* snode = (uint16_t*)(smem + Ly.snode);
+    int16_t* smx = (int16_t*)(smem + Ly.smx);
+    int16_t* smy = (int16_t*)(smem + Ly.smy);
+    uint32_t* ccnt = (uint32_t*)(smem + Ly.ccnt);
+    uint16_t* cpos = (uint16_t*)(smem + Ly.cpos);
+    uint16_t* vprev = (uint16_t*)(smem + Ly.vprev);
+    uint16_t* vnew = (uint16_t*)(smem + Ly.vnew);
+    uint32_t* skey = (uint32_t*)(smem + Ly.skey);
+    unsigned long long* best = (unsigned long long*)(smem + Ly.best);
+    uint32_t* wsum = (uint32_t*)(smem + Ly.wsum);
+    int* sh = (int*)(smem + Ly.sh);
+    // rect buffers: [buf][coord][lcap], coord 0..3 = x0, x1, y0, y1
+    auto R = [&](int buf, int coord) { return rect + (size_t)(buf * 4 + coord) * lcap; };
+
+    // ---- 1. gather this level's FAST candidates in reference order ----------
+    const int ncl = LG.ncells, cb = LG.cell_begin;
+    for (int c = tid; c < ncl; c += QT_NT) scan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
+    __syncthreads();
+    const int n = (int)block_scan_excl(scan, ncl, wsum);
+    const uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
+    uint32_t* fspill = spill + (size_t)f * G->spill_per_frame + (LG.slot_begin > 0 ? 0 : 0);
+    uint32_t* fspill_node = spill_node + (size_t)f * G->spill_per_frame;
+    // spill region of this level: levels share the frame's spill array in level order
+    {
+        int off = 0;
+        for (int q = 0; q < l; ++q) {
+            const int extra = G->lv[q].slot_cap - QT_NT * QT_KPT;
+            off += extra > 0 ? extra : 0;
+        }
+        fspill += off;
+        fspill_node += off;
+    }
+    auto fetch = [&](int i) -> uint32_t {
+        int lo = 0, hi = ncl - 1;   // last cell with scan[c] <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)scan[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        return fslots[cells[cb + lo].slot_base + (i - (int)scan[lo])];
+    };
+    uint32_t kp[QT_KPT], nd[QT_KPT];
+#pragma unroll
+    for (int r = 0; r < QT_KPT; ++r) {
+        const int i = tid + r * QT_NT;
+        kp[r] = i < n ? fetch(i) : 0u;
+        nd[r] = 0;
+    }
+    for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) fspill[i - QT_NT * QT_KPT] = fetch(i);
+
+    // visit every keypoint (register part unrolled, spill part in a loop)
+    auto visit = [&](auto&& fn) {
+#pragma unroll
+        for (int r = 0; r < QT_KPT; ++r) {
+            const int i = tid + r * QT_NT;
+            if (i < n) fn(kp[r], nd[r], i);
+        }
+        for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) {
+            uint32_t k = fspill[i - QT_NT * QT_KPT];
+            uint32_t d = fspill_node[i - QT_NT * QT_KPT];
+            fn(k, d, i);
+            fspill_node[i - QT_NT * QT_KPT] = d;
+        }
+    };
+
+    // ---- 2. initial nodes, src/ORBextractor.cc:650-699 ------------------------
+    const int nIni = LG.nIni;
+    const float hX = LG.hX;
+    const int N = LG.nfeat;
+    for (int i = tid; i < nIni; i += QT_NT) ccnt[i] = 0;
+    __syncthreads();
+    visit([&](uint32_t& k, uint32_t& d, int) {
+        const int x = (int)(k & 0xFFF);
+        int r = (int)((float)x / hX);
+        if (r >= nIni) r = nIni - 1;
+        d = (uint32_t)r;
+        atomicAdd(&ccnt[r], 1u);
+    });
+    __syncthreads();
+    if (tid == 0) {
+        int L = 0;
+        for (int i = 0; i < nIni; ++i) {
+            npos[i] = kNone;
+            if (ccnt[i] > 0) {
+                if (L < lcap) {
+                    R(0, 0)[L] = (int16_t)(int)(hX * (float)i);
+                    R(0, 1)[L] = (int16_t)(int)(hX * (float)(i + 1));
+                    R(0, 2)[L] = 0;
+                    R(0, 3)[L] = (int16_t)LG.qh;
+                    cntb[L] = ccnt[i];
+                }
+                npos[i] = (uint16_t)L;
+                ++L;
+            }
+        }
+        sh[SH_N] = n;
+        sh[SH_L] = L;
+        sh[SH_PHASE] = 1;
+        sh[SH_DONE] = 0;
+        sh[SH_ERR] = L > lcap ? kStatusListOverflow : 0;
+        if (L > lcap) sh[SH_DONE] = 1;
+    }
+    __syncthreads();
+    visit([&](uint32_t&, uint32_t& d, int) { d = npos[d]; });
+
+    int cur = 0;
+    while (true) {
+        __syncthreads();
+        if (sh[SH_DONE]) break;
+        const int L = sh[SH_L];
+        const int phase = sh[SH_PHASE];
+        uint32_t* cntc = cntb + (size_t)cur * lcap;
+        uint32_t* cntn = cntb + (size_t)(cur ^ 1) * lcap;
+        int16_t *cx0 = R(cur, 0), *cx1 = R(cur, 1), *cy0 = R(cur, 2), *cy1 = R(cur, 3);
+        int16_t *nx0 = R(cur ^ 1, 0), *nx1 = R(cur ^ 1, 1), *ny0 = R(cur ^ 1, 2), *ny1 = R(cur ^ 1, 3);
+
+        int S;           // number of candidate (split) nodes this round
+        int m = 0;       // phase 2: vPrev length
+        if (phase == 1) {
+            // split set = nodes with more than one key, ranked in list order
+            for (int p = tid; p < L; p += QT_NT) scan[p] = cntc[p] > 1 ? 1u : 0u;
+            __syncthreads();
+            S = (int)block_scan_excl(scan, L, wsum);
+            for (int p = tid; p < L; p += QT_NT) {
+                if (cntc[p] > 1) {
+                    const int s = (int)scan[p];
+                    srank[p] = (uint16_t)s;
+                    snode[s] = (uint16_t)p;
+                } else {
+                    srank[p] = kNone;
+                }
+                npos[p] = (uint16_t)(p - (int)scan[p]);   // rank among non-split nodes
+            }
+        } else {
+            // phase 2: sort vPrev by (size, creation) and split from the back
+            m = sh[SH_M];
+            const int p2 = next_pow2(m);
+            for (int k = tid; k < p2; k += QT_NT)
+                skey[k] = k < m ? ((cntc[vprev[k]] << 16) | (uint32_t)k) : 0u;
+            for (int p = tid; p < L; p += QT_NT) srank[p] = kNone;
+            __syncthreads();
+            block_bitonic_desc(skey, p2);
+            for (int j = tid; j < m; j += QT_NT) {
+                const int p = vprev[skey[j] & 0xFFFF];
+                srank[p] = (uint16_t)j;
+                snode[j] = (uint16_t)p;
+            }
+            S = m;
+        }
+        __syncthreads();
+        // midlines of candidate nodes (ExtractorNode::DivideNode, :572-573)
+        for (int s = tid; s < S; s += QT_NT) {
+            const int p = snode[s];
+            const int hx = (int)ceilf((float)(cx1[p] - cx0[p]) / 2);
+            const int hy = (int)ceilf((float)(cy1[p] - cy0[p]) / 2);
+            smx[s] = (int16_t)(cx0[p] + hx);
+            smy[s] = (int16_t)(cy0[p] + hy);
+            ccnt[4 * s] = ccnt[4 * s + 1] = ccnt[4 * s + 2] = ccnt[4 * s + 3] = 0;
+        }
+        __syncthreads();
+        visit([&](uint32_t& k, uint32_t& d, int) {
+            const int s = srank[d];
+            if (s != kNone) {
+                const int x = (int)(k & 0xFFF), y = (int)((k >> 12) & 0xFFF);
+                const int q = (x >= smx[s] ? 1 : 0) + (y >= smy[s] ? 2 : 0);
+                atomicAdd(&ccnt[4 * s + q], 1u);
+            }
+        });
+        __syncthreads();
+
+        // how many candidates are actually split (phase 2 stops once size >= N)
+        int kk = S;
+        if (phase == 2) {
+            for (int j = tid; j < S; j += QT_NT) {
+                int cs = 0;
+                for (int q = 0; q < 4; ++q) cs += ccnt[4 * j + q] > 0;
+                scan[j] = (uint32_t)cs;   // delta + 1
+            }
+            if (tid == 0) sh[SH_KK] = S;
+            __syncthreads();
+            block_scan_excl(scan, S, wsum);
+            for (int j = tid; j < S; j += QT_NT) {
+                int cs = 0;
+                for (int q = 0; q < 4; ++q) cs += ccnt[4 * j + q] > 0;
+                const int run = L + (int)scan[j] + cs - (j + 1);   // size after splitting j
+                if (run >= N) atomicMin(&sh[SH_KK], j + 1);
+            }
+            __syncthreads();
+            kk = sh[SH_KK];
+            // non-split rank of every current node
+            for (int p = tid; p < L; p += QT_NT) scan[p] = (srank[p] != kNone && srank[p] < kk) ? 1u : 0u;
+            __syncthreads();
+            block_scan_excl(scan, L, wsum);
+            for (int p = tid; p < L; p += QT_NT) npos[p] = (uint16_t)(p - (int)scan[p]);
+            __syncthreads();
+        }
+
+        // children: count and exclusive offsets over split ranks 0..kk-1
+        for (int s = tid; s < kk; s += QT_NT) {
+            int cs = 0;
+            for (int q = 0; q < 4; ++q) cs += ccnt[4 * s + q] > 0;
+            scan[s] = (uint32_t)cs;
+        }
+        __syncthreads();
+        const int Ctot = (int)block_scan_excl(scan, kk, wsum);
+        const int newL = Ctot + (L - kk);
+        if (newL > lcap) {
+            if (tid == 0) {
+                sh[SH_ERR] |= kStatusListOverflow;
+                sh[SH_DONE] = 1;
+            }
+            continue;
+        }
+        for (int s = tid; s < kk; s += QT_NT) {
+            const int p = snode[s];
+            int cs = 0;
+            for (int q = 0; q < 4; ++q) cs += ccnt[4 * s + q] > 0;
+            const int pos0 = Ctot - (int)scan[s] - cs;   // later splits are pushed in front
+            const int mx = smx[s], my = smy[s];
+            const int x0 = cx0[p], x1 = cx1[p], y0 = cy0[p], y1 = cy1[p];
+            int j = 0;
+            for (int q = 3; q >= 0; --q) {
+                const uint32_t c = ccnt[4 * s + q];
+                if (c == 0) {
+                    cpos[4 * s + q] = kNone;
+                    continue;
+                }
+                const int np = pos0 + j++;
+                cpos[4 * s + q] = (uint16_t)np;
+                nx0[np] = (int16_t)((q & 1) ? mx : x0);
+                nx1[np] = (int16_t)((q & 1) ? x1 : mx);
+                ny0[np] = (int16_t)((q & 2) ? my : y0);
+                ny1[np] = (int16_t)((q & 2) ? y1 : my);
+                cntn[np] = c;
+            }
+        }
+        for (int p = tid; p < L; p += QT_NT) {
+            const bool split = srank[p] != kNone && srank[p] < kk;
+            if (!split) {
+                const int np = Ctot + npos[p];
+                npos[p] = (uint16_t)np;
+                nx0[np] = cx0[p];
+                nx1[np] = cx1[p];
+                ny0[np] = cy0[p];
+                ny1[np] = cy1[p];
+                cntn[np] = cntc[p];
+            }
+        }
+        __syncthreads();
+        // new expandable children in creation order (split rank, then n1..n4)
+        for (int e = tid; e < 4 * kk; e += QT_NT) scan[e] = ccnt[e] > 1 ? 1u : 0u;
+        __syncthreads();
+        const int nexp = (int)block_scan_excl(scan, 4 * kk, wsum);
+        for (int e = tid; e < 4 * kk; e += QT_NT)
+            if (ccnt[e] > 1) vnew[scan[e]] = cpos[e];
+        // relabel keypoints with their new list position
+        visit([&](uint32_t& k, uint32_t& d, int) {
+            const int s = srank[d];
+            if (s != kNone && s < kk) {
+                const int x = (int)(k & 0xFFF), y = (int)((k >> 12) & 0xFFF);
+                const int q = (x >= smx[s] ? 1 : 0) + (y >= smy[s] ? 2 : 0);
+                d = cpos[4 * s + q];
+            } else {
+                d = npos[d];
+            }
+        });
+        __syncthreads();
+        if (tid == 0) {
+            // src/ORBextractor.cc:793-803 and :871-872
+            sh[SH_L] = newL;
+            if (newL >= N || newL == L) {
+                sh[SH_DONE] = 1;
+            } else if (phase == 1) {
+                if (newL + 3 * nexp > N) {
+                    sh[SH_PHASE] = 2;
+                }
+            }
+            sh[SH_M] = nexp;
+        }
+        // vnew -> vprev for the next round
+        for (int e = tid; e < nexp; e += QT_NT) vprev[e] = vnew[e];
+        cur ^= 1;
+    }
+
+    // ---- 4. retain the best keypoint per node (first max wins), :882-906 -----
+    const int L = sh[SH_L];
+    const bool ok = sh[SH_ERR] == 0;
+    for (int p = tid; p < L && ok; p += QT_NT) best[p] = 0ull;
+    __syncthreads();
+    if (ok) {
+        visit([&](uint32_t& k, uint32_t& d, int i) {
+            const unsigned long long key = ((unsigned long long)(k >> 24) << 56) |
+                                           ((unsigned long long)(0xFFFFFFu - (uint32_t)i) << 32) |
+                                           (unsigned long long)(k & 0xFFFFFFu);
+            atomicMax(&best[d], key);
+        });
+    }
+    __syncthreads();
+    const int outn = ok ? (L < LG.cap ? L : LG.cap) : 0;
+    uint32_t* out = qt_out + (size_t)f * G->out_per_frame + LG.out_off;
+    for (int p = tid; p < outn; p += QT_NT) {
+        const unsigned long long key = best[p];
+        const uint32_t x = (uint32_t)(key & 0xFFF) + kMinBorder;
+        const uint32_t y = (uint32_t)((key >> 12) & 0xFFF) + kMinBorder;
+        out[p] = pack_kp(x, y, (uint32_t)(key >> 56));
+    }
+    if (tid == 0) {
+        qt_cnt[(size_t)f * G->nlevels + l] = outn;
+        atomicAdd(&frame_counts[f], outn);
+        int err = sh[SH_ERR];
+        if (ok && L > LG.cap) err |= kStatusOutOverflow;
+        if (err) atomicOr(status, err);
+    }
+}
+
+void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s)
+{
+    const size_t smem = quadtree_smem_bytes(g);
+    dim3 grid(g.nlevels, batch);
+    hipLaunchKernelGGL(k_quadtree, grid, dim3(QT_NT), smem, s, b.geom, b.cells, b.slots, b.cell_counts,
+                       b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+}
+
+// ---------------------------------------------------------------------------
+// K4: one wave per retained keypoint.  The 43x43 raw neighbourhood (reflect-101
+// at level borders) is staged in LDS; IC_Angle sums the 789-pixel disc with a
+// wave reduction; the 7x7 integer Gaussian (kernel [18 34 49 55 49 34 18]/2^16,
+// SURVEY.md A.3) is evaluated on the 37x37 BRIEF support only; the 256 tests
+// become four __ballot words = the descriptor's little-endian u64 words.
+// ---------------------------------------------------------------------------
+constexpr int kRawN = 43, kRawP = 44, kBlN = 37;
+
+__device__ __forceinline__ int reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+
+__device__ __forceinline__ int wave_sum(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
+                                                  const uint32_t* __restrict__ qt_out,
+                                                  const int* __restrict__ qt_cnt,
+                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                  int cap, int* __restrict__ status)
+{
+    __shared__ uint8_t s_raw[4][kRawN * kRawP];
+    __shared__ uint16_t s_row[4][kRawN * kBlN];
+    __shared__ uint8_t s_blur[4][kBlN * kBlN];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int f = blockIdx.y;
+    const int g = blockIdx.x * 4 + wave;
+    if (g >= G->out_per_frame) return;
+    const int L = G->nlevels;
+    int l = 0;
+    while (l + 1 < L && g >= G->lv[l + 1].out_off) ++l;
+    const LevelGeom& LG = G->lv[l];
+    const int pos = g - LG.out_off;
+    const int* cnts = qt_cnt + (size_t)f * L;
+    if (pos >= cnts[l]) return;
+    int oidx = pos;
+    for (int q = 0; q < l; ++q) oidx += cnts[q];
+    if (oidx >= cap) {
+        if (lane == 0) atomicOr(status, (int)kStatusCapOverflow);
+        return;
+    }
+    const uint32_t pk = qt_out[(size_t)f * G->out_per_frame + g];
+    const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF), score = (int)(pk >> 24);
+    int pitch;
+    const uint8_t* img = level_base(P, G, f, l, pitch);
+    const int w = LG.w, h = LG.h;
+    uint8_t* raw = s_raw[wave];
+    uint16_t* row = s_row[wave];
+    uint8_t* bl = s_blur[wave];
+
+    // raw patch [cy-21, cy+21] x [cx-21, cx+21]
+    const bool inside = cx >= 21 && cy >= 21 && cx + 21 < w && cy + 21 < h;
+    for (int i = lane; i < kRawN * kRawN; i += 64) {
+        const int r = i / kRawN, c = i - r * kRawN;
+        int X = cx - 21 + c, Y = cy - 21 + r;
+        if (!inside) {
+            X = reflect101(X, w);
+            Y = reflect101(Y, h);
+        }
+        raw[r * kRawP + c] = img[(size_t)Y * pitch + X];
+    }
+    wave_lds_sync();
+
+    // IC_Angle (src/ORBextractor.cc:84-128): m10 = sum u*I, m01 = sum v*I on the disc
+    int m10 = 0, m01 = 0;
+    for (int i = lane; i < 31 * 31; i += 64) {
+        const int v = i / 31 - 15, u = i % 31 - 15;
+        const int av = v < 0 ? -v : v, au = u < 0 ? -u : u;
+        if (au <= G->umax[av]) {
+            const int val = raw[(21 + v) * kRawP + 21 + u];
+            m10 += u * val;
+            m01 += v * val;
+        }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+
+    // GaussianBlur 7x7: horizontal pass on 43 rows x 37 cols, then vertical
+    const int k7[7] = {18, 34, 49, 55, 49, 34, 18};
+    for (int i = lane; i < kRawN * kBlN; i += 64) {
+        const int r = i / kBlN, c = i - r * kBlN;
+        const uint8_t* s = raw + r * kRawP + c;
+        int acc = 0;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) acc += k7[t] * s[t];
+        row[r * kBlN + c] = (uint16_t)acc;
+    }
+    wave_lds_sync();
+    for (int i = lane; i < kBlN * kBlN; i += 64) {
+        const int r = i / kBlN, c = i - r * kBlN;
+        int acc = 0;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) acc += k7[t] * (int)row[(r + t) * kBlN + c];
+        const int v = (acc + (1 << 15)) >> 16;
+        bl[r * kBlN + c] = (uint8_t)(v > 255 ? 255 : v);
+    }
+    wave_lds_sync();
+
+    // rBRIEF (src/ORBextractor.cc:141-192) with the reference's contracted FMAs
+    const float ang = angle * kFactorPI;
+    const float a = glibc_sincosf(ang, 1), b = glibc_sincosf(ang, 0);
+    unsigned long long words[4];
+#pragma unroll
+    for (int wd = 0; wd < 4; ++wd) {
+        const int m = wd * 64 + lane;
+        int t2[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float px = (float)c_pattern[4 * m + 2 * e], py = (float)c_pattern[4 * m + 2 * e + 1];
+            const int yy = __float2int_rn(__builtin_fmaf(px, b, py * a));
+            const int xx = __float2int_rn(__builtin_fmaf(px, a, -(py * b)));
+            t2[e] = bl[(18 + yy) * kBlN + 18 + xx];
+        }
+        words[wd] = __ballot(t2[0] < t2[1]);
+    }
+    const size_t o = (size_t)f * cap + oidx;
+    if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
+    if (lane == 0) {
+        float x = (float)cx, y = (float)cy;
+        if (l != 0) {
+            x *= LG.scale;
+            y *= LG.scale;
+        }
+        orbx_keypoint k;
+        k.x = x;
+        k.y = y;
+        k.size = LG.patch_size;
+        k.angle = angle;
+        k.response = (float)score;
+        k.octave = l;
+        k.class_id = -1;
+        kps[o] = k;
+    }
+}
+
+void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, orbx_keypoint* kps,
+                     uint8_t* desc, int cap, int batch, hipStream_t s)
+{
+    dim3 grid((g.out_per_frame + 3) / 4, batch);
+    hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, s, b.geom, p, b.qt_out, b.qt_cnt, kps, desc, cap,
+                       b.status);
+}
+
+}  // namespace orbx

@@ -1,0 +1,64 @@
+// Frame geometry computed once per (params, rows, cols) on the host and read by
+// every kernel.  All of it restates ORB-SLAM2 integer/float geometry:
+//   level sizes          src/ORBextractor.cc:1347-1348
+//   FAST cell grid        src/ORBextractor.cc:932-972
+//   quadtree roots        src/ORBextractor.cc:650-675
+//   per-level budgets     src/ORBextractor.cc:496-510
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "orbx_math.hpp"
+
+namespace orbx {
+
+constexpr int kMaxLevels = 16;
+constexpr int kEdge = 19;                 // EDGE_THRESHOLD, src/ORBextractor.cc:74
+constexpr int kMinBorder = kEdge - 3;     // minBorderX/Y, src/ORBextractor.cc:932
+constexpr int kMaxDim = 4096;             // 12-bit packed keypoint coordinates
+
+// One FAST cell ROI (src/ORBextractor.cc:952-976), level coordinates.
+struct Cell {
+    int16_t level, roi_w, roi_h, pad;
+    int32_t roi_x0, roi_y0;
+    int32_t slot_base;   // first candidate slot of this cell (frame-relative)
+    int32_t slot_cap;    // ceil(dw/2)*ceil(dh/2): max strict-NMS survivors
+};
+
+struct LevelGeom {
+    int w, h, pitch;          // pitch: device row pitch (levels >= 1)
+    long long pyr_off;        // byte offset inside a frame's pyramid block (levels >= 1)
+    int xtab_off, ytab_off;   // offsets of the resize coefficient tables (levels >= 1)
+    int ncells, cell_begin;   // cells of this level in the cell table
+    int slot_begin, slot_cap; // candidate slots of this level (frame-relative)
+    int nfeat;                // N_l
+    int cap;                  // max retained keypoints: max(N_l + 2, 4 * nIni)
+    int out_off;              // first output slot of this level (frame-relative)
+    int nIni;                 // quadtree root count
+    float hX;                 // quadtree root width
+    int qw, qh;               // maxX-minX, maxY-minY (quadtree frame)
+    float scale;              // mvScaleFactor[l]
+    float patch_size;         // (float)(int)(PATCH_SIZE * scale)
+};
+
+struct Geometry {
+    int rows, cols, nlevels;
+    int ini_th, min_th;
+    int ncells;               // cells over all levels (per frame)
+    int slots_per_frame;      // candidate slots per frame
+    int out_per_frame;        // sum of level caps
+    int spill_per_frame;      // quadtree register-overflow keypoints per frame
+    int max_cells_level;      // largest per-level cell count
+    int lcap;                 // quadtree list capacity (max level cap + slack)
+    long long pyr_bytes;      // bytes per frame for levels 1..L-1
+    int umax[16];
+    LevelGeom lv[kMaxLevels];
+};
+
+// Packed candidate / retained keypoint: x (12 bits) | y (12 bits) << 12 | score << 24
+ORBX_HD uint32_t pack_kp(uint32_t x, uint32_t y, uint32_t s)
+{
+    return x | (y << 12) | (s << 24);
+}
+
+}  // namespace orbx

@@ -1,0 +1,56 @@
+// Internal kernel interface of liborbx (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/orbx.h"
+#include "orbx_geom.hpp"
+
+namespace orbx {
+
+// Where the levels of frame f live.  Level 0 is the caller's image (no copy);
+// levels >= 1 are in the handle's pyramid block.
+struct FramePtrs {
+    const uint8_t* in;
+    size_t in_fstride;
+    int in_pitch;
+    uint8_t* pyr;
+    size_t pyr_fstride;
+};
+
+struct ExtractBufs {
+    const Geometry* geom;       // device copy
+    const Cell* cells;          // device cell table
+    const int2* xtab;           // resize tables (levels >= 1)
+    const int2* ytab;
+    uint32_t* slots;            // [B][slots_per_frame] FAST candidates
+    int* cell_counts;           // [B][ncells]
+    uint32_t* spill;            // [B][spill_per_frame] quadtree overflow (packed kp)
+    uint32_t* spill_node;       // [B][spill_per_frame]
+    uint32_t* qt_out;           // [B][out_per_frame] retained keypoints (level coords)
+    int* qt_cnt;                // [B][nlevels]
+    int* status;                // device error word (bit flags)
+};
+
+enum : int {
+    kStatusListOverflow = 1,
+    kStatusOutOverflow = 2,
+    kStatusCapOverflow = 4,
+};
+
+size_t quadtree_smem_bytes(const Geometry& g);
+
+void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
+void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
+void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s);
+void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, orbx_keypoint* kps,
+                     uint8_t* desc, int cap, int batch, hipStream_t s);
+
+void launch_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt, int* bi, int* b1, int* b2,
+                          int* part, int nsplit, hipStream_t s);
+void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, uint16_t* out, hipStream_t s);
+void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int cap,
+                        const int* pa, const int* pb, int npairs, int rows, int cols, int window,
+                        float nnratio, int check_ori, uint32_t* cand, int cand_per_pair, int* m12,
+                        int* nm, hipStream_t s);
+
+}  // namespace orbx

@@ -1,0 +1,175 @@
+"""GPU (gfx950) vs CPU oracle parity through the C ABI (liborbx.so).
+
+Bar: bit-exact for pyramid bytes, FAST candidates, keypoint x/y/size/response/
+octave/class_id, keypoint order and BRIEF bits; |angle difference| <= 1e-4
+degrees (the north-star tolerance; expected to be exact).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ANGLE_TOL = 1e-4
+
+
+def _extractor(nfeat, scale=1.2, nlevels=8, ini=20, mn=7):
+    import orbx
+    return orbx.ORBextractor(nfeat, scale, nlevels, ini, mn)
+
+
+def _run_batch(ex, frames, cuda):
+    import torch
+    import orbx
+    imgs = torch.from_numpy(np.ascontiguousarray(frames)).to(cuda)
+    B, H, W = imgs.shape
+    cap = ex.capacity(H, W)
+    kps = torch.empty((B, cap, 7), dtype=torch.int32, device=cuda)
+    desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=cuda)
+    counts = torch.empty((B,), dtype=torch.int32, device=cuda)
+    ex.extract_batch_device(imgs, kps, desc, counts)
+    ex.sync(torch.cuda.current_stream())
+    klist = orbx.keypoints_from_device(kps, counts)
+    d = desc.cpu().numpy()
+    c = counts.cpu().numpy()
+    return imgs, kps, desc, counts, klist, [d[f, :c[f]] for f in range(B)]
+
+
+def assert_same_keypoints(got, want, got_desc, want_desc, tag=""):
+    assert len(got) == len(want), "%s: %d keypoints vs oracle %d" % (tag, len(got), len(want))
+    for field in ("x", "y", "size", "response", "octave", "class_id"):
+        bad = np.nonzero(got[field] != want[field])[0]
+        assert bad.size == 0, "%s: field %s differs at %s (gpu %s, oracle %s)" % (
+            tag, field, bad[:5], got[field][bad[:5]], want[field][bad[:5]])
+    da = np.abs(got["angle"].astype(np.float64) - want["angle"].astype(np.float64))
+    assert da.max(initial=0.0) <= ANGLE_TOL, "%s: angle max diff %g at %d" % (tag, da.max(), int(da.argmax()))
+    bad = np.nonzero((got_desc != want_desc).any(axis=1))[0]
+    assert bad.size == 0, "%s: %d descriptors differ, first %s" % (tag, bad.size, bad[:5])
+
+
+CONFIGS = [
+    # (name, W, H, nfeatures, frames)
+    ("tum640", 640, 480, 1000, "gen"),
+    ("kitti", 1241, 376, 2000, "kitti"),
+    ("euroc", 752, 480, 1000, "gen"),
+    ("small", 320, 240, 300, "gen"),
+    ("kitti_init2x", 1241, 376, 4000, "kitti"),
+]
+
+
+def _frames(kind, W, H, n, seed0=1):
+    import orbx_synth
+    if kind == "kitti":
+        return orbx_synth.kitti_sequence(n, start=seed0 * 7)
+    return np.stack([orbx_synth.gen_image(seed0 + i, W, H) for i in range(n)])
+
+
+@pytest.mark.parametrize("name,W,H,nfeat,kind", CONFIGS)
+def test_extract_parity(orbref, cuda, name, W, H, nfeat, kind):
+    frames = _frames(kind, W, H, 2)
+    ex = _extractor(nfeat)
+    p = orbref.make_params(nfeat, 1.2, 8, 20, 7)
+    sizes = orbref.level_sizes(p, W, H)
+    _, _, _, _, klist, dlist = _run_batch(ex, frames, cuda)
+    for f in range(len(frames)):
+        ref = orbref.extract(frames[f], p)
+        # stage 1: pyramid bytes
+        pyr = ex.debug_pyramid(f, sizes)
+        for l, (a, b) in enumerate(zip(pyr, ref.pyramid)):
+            bad = np.argwhere(a != b)
+            assert bad.size == 0, "%s f%d pyramid level %d differs at %s" % (name, f, l, bad[:3])
+        # stage 2: FAST candidates per level, reference order
+        for l in range(8):
+            want = orbref.level_candidates(ref.pyramid[l])
+            got = ex.debug_candidates(f, l)
+            assert len(got) == len(want), "%s f%d level %d: %d candidates vs %d" % (name, f, l, len(got), len(want))
+            assert np.array_equal(got, want), "%s f%d level %d candidates differ" % (name, f, l)
+        # stage 3+4: final keypoints and descriptors
+        assert len(ref.keypoints) >= 0.9 * nfeat, "%s: oracle kept only %d keypoints" % (name, len(ref.keypoints))
+        assert_same_keypoints(klist[f], ref.keypoints, dlist[f], ref.descriptors, "%s f%d" % (name, f))
+
+
+def test_host_api_matches_batch(orbref, cuda):
+    import orbx_synth
+    img = orbx_synth.gen_image(11, 640, 480)
+    ex = _extractor(1000)
+    kps, desc = ex(img)
+    p = orbref.make_params(1000, 1.2, 8, 20, 7)
+    ref = orbref.extract(img, p)
+    assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "host api")
+    pyr = ex.mvImagePyramid
+    for l in range(8):
+        assert np.array_equal(pyr[l], ref.pyramid[l])
+    assert np.allclose(ex.GetScaleFactors(), orbref.tables(p).scale[:8])
+
+
+def test_empty_and_flat_images(orbref, cuda):
+    ex = _extractor(500)
+    kps, desc = ex(np.zeros((0, 0), np.uint8))
+    assert len(kps) == 0 and desc is None
+    flat = np.full((240, 320), 77, np.uint8)
+    kps, desc = ex(flat)
+    ref = orbref.extract(flat, orbref.make_params(500, 1.2, 8, 20, 7))
+    assert len(kps) == len(ref.keypoints) == 0
+    # half flat / half textured: some cells fall back to minThFAST, some find nothing
+    import orbx_synth
+    img = orbx_synth.gen_image(5, 320, 240)
+    img[:, :160] = 90
+    img[:120, :160] += (np.arange(160) % 2 * 9).astype(np.uint8)[None, :]
+    kps, desc = ex(img)
+    ref = orbref.extract(img, orbref.make_params(500, 1.2, 8, 20, 7))
+    assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "half flat")
+
+
+def test_other_params(orbref, cuda):
+    import orbx_synth
+    img = orbx_synth.gen_image(21, 752, 480)
+    for nfeat, scale, nl, ini, mn in [(1200, 1.2, 8, 20, 7), (500, 1.3, 6, 25, 10), (150, 1.2, 4, 12, 5)]:
+        ex = _extractor(nfeat, scale, nl, ini, mn)
+        kps, desc = ex(img)
+        ref = orbref.extract(img, orbref.make_params(nfeat, scale, nl, ini, mn))
+        assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "params %s" % ((nfeat, scale, nl),))
+
+
+def test_search_for_initialization(orbref, cuda):
+    import torch
+    import orbx
+    frames = _frames("kitti", 1241, 376, 4)
+    ex = _extractor(2000)
+    imgs, kps, desc, counts, klist, dlist = _run_batch(ex, frames, cuda)
+    pa = torch.tensor([0, 1, 2, 0], dtype=torch.int32, device=cuda)
+    pb = torch.tensor([1, 2, 3, 3], dtype=torch.int32, device=cuda)
+    m = orbx.ORBmatcher(0.9, True)
+    m12, nm = m.search_for_initialization_batch(kps, desc, counts, pa, pb, 376, 1241, 100)
+    torch.cuda.synchronize()
+    m12 = m12.cpu().numpy()
+    nm = nm.cpu().numpy()
+    for p, (a, b) in enumerate(zip(pa.tolist(), pb.tolist())):
+        want_n, want_m, _ = orbref.search_for_initialization(klist[a], dlist[a], klist[b], dlist[b], 1241, 376,
+                                                             window=100, nnratio=0.9, check_ori=True)
+        got = m12[p, :len(klist[a])]
+        assert nm[p] == want_n, "pair %d: %d matches vs oracle %d" % (p, nm[p], want_n)
+        assert np.array_equal(got, want_m), "pair %d: match vectors differ at %s" % (p, np.nonzero(got != want_m)[0][:5])
+    assert nm[0] > 50
+
+
+@pytest.mark.parametrize("nq,nt", [(1000, 777), (257, 5000), (10000, 1024)])
+def test_allpairs(orbref, cuda, nq, nt):
+    import torch
+    import orbx
+    import orbx_synth
+    q = orbx_synth.random_descriptors(nq, 55)
+    t = orbx_synth.random_descriptors(nt, 56)
+    t[:min(nq, nt) // 10] = q[:min(nq, nt) // 10] ^ (np.random.default_rng(1).random((min(nq, nt) // 10, 32)) < 0.03)
+    dq, dt = torch.from_numpy(q).to(cuda), torch.from_numpy(t).to(cuda)
+    bi, b1, b2 = orbx.allpairs(dq, dt, orbx.TOP2)
+    full = orbx.allpairs(dq, dt, orbx.FULL_U16)
+    torch.cuda.synchronize()
+    # reference: popcount of xor
+    x = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(axis=2) if nq * nt <= 4_000_000 else None
+    if x is not None:
+        assert np.array_equal(full.cpu().numpy().astype(np.int64), x)
+    sel = np.arange(0, nq, max(1, nq // 300))
+    wi, w1, w2 = orbref.allpairs_top2(q[sel], t)
+    assert np.array_equal(bi.cpu().numpy()[sel], wi)
+    assert np.array_equal(b1.cpu().numpy()[sel], w1)
+    assert np.array_equal(b2.cpu().numpy()[sel], w2)
