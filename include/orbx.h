@@ -77,18 +77,20 @@ orbx_status orbx_get_level(orbx_handle* h, int level, const uint8_t** data, int*
 /* Batched device-resident replay (config 2/4): `batch` frames of rows x cols u8 at
  * d_imgs + f*frame_stride (row pitch `step`), already in HBM.  Outputs per frame f:
  * d_kps[f*cap + i], d_desc[(f*cap + i)*32], d_counts[f].  Asynchronous on `stream`
- * (a hipStream_t; NULL = the handle's own stream). */
+ * (a hipStream_t taken literally: NULL is the HIP null stream). */
 orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int batch, int rows,
                                       int cols, size_t step, size_t frame_stride,
                                       orbx_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int cap,
                                       void* stream);
 
-/* Wait for the work queued by the last extract on `stream` (NULL = handle stream) and
+/* Wait for the work queued on `stream` (NULL = HIP null stream) and
  * return the device-side status (ORBX_ENOSPC when a frame exceeded `cap`). */
 orbx_status orbx_sync(orbx_handle* h, void* stream);
 
-/* Per-stage device timing of the last extract (ms, HIP events on the launch stream).
- * Stages: 0 pyramid, 1 fast, 2 quadtree, 3 describe.  Enable before extracting. */
+/* Per-stage device timing (ms, HIP events recorded on the launch stream between
+ * the stage kernels).  orbx_set_timing(h, 1) starts a new accumulation window;
+ * orbx_get_stage_times returns the per-stage sums over every extract since then.
+ * Stages: 0 pyramid (all levels), 1 fast, 2 quadtree, 3 describe. */
 orbx_status orbx_set_timing(orbx_handle* h, int enable);
 orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n);
 

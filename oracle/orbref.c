@@ -283,6 +283,23 @@ int orbref_level_candidates(const uint8_t* level, size_t step, int w, int h, int
     return n;
 }
 
+int orbref_level_cells(int w, int h)
+{
+    /* number of FAST cells ComputeKeyPointsOctTree scans on a w x h level (:941-972) */
+    const int minB = EDGE_THRESHOLD - 3, maxBX = w - EDGE_THRESHOLD + 3, maxBY = h - EDGE_THRESHOLD + 3;
+    const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+    const int nCols = (int)(width / 30), nRows = (int)(height / 30);
+    if (nCols <= 0 || nRows <= 0) return 0;
+    const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+    int n = 0;
+    for (int i = 0; i < nRows; i++) {
+        if ((float)(minB + i * hCell) >= maxBY - 3) continue;
+        for (int j = 0; j < nCols; j++)
+            if (!((float)(minB + j * wCell) >= maxBX - 6)) n++;
+    }
+    return n;
+}
+
 /* ---- a6: DistributeOctTree, src/ORBextractor.cc:569-907 ------------------ */
 typedef struct {
     int x0, x1, y0, y1;       /* UL.x, UR.x, UL.y, BL.y */

@@ -87,6 +87,9 @@ int orbref_fast(const uint8_t* roi, size_t step, int rows, int cols, int thresho
 int orbref_level_candidates(const uint8_t* level, size_t step, int w, int h,
                             int ini_th, int min_th, int* out_xys, int cap);
 
+/* Number of FAST cells scanned on a w x h level (src/ORBextractor.cc:941-972). */
+int orbref_level_cells(int w, int h);
+
 /* a6: DistributeOctTree (src/ORBextractor.cc:644-907), canonical tie-break.
  * Input triples are relative to (minX, minY).  Writes the indices of the
  * retained keypoints in output (list) order; returns the count, -1 if > cap. */

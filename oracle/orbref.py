@@ -54,6 +54,7 @@ def lib():
         L.orbref_resize_linear.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_int, C.c_int, C.c_size_t]
         L.orbref_fast.argtypes = [u8p, C.c_size_t, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
         L.orbref_level_candidates.argtypes = [u8p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
+        L.orbref_level_cells.argtypes = [C.c_int, C.c_int]
         L.orbref_distribute.argtypes = [i32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
         L.orbref_fast_atan2.argtypes = [C.c_float, C.c_float]
         L.orbref_fast_atan2.restype = C.c_float
@@ -130,6 +131,10 @@ def level_candidates(level: np.ndarray, ini_th=20, min_th=7) -> np.ndarray:
                                       ini_th, min_th, _i32(out), cap)
     assert n >= 0
     return out[:n].copy()
+
+
+def level_cells(w: int, h: int) -> int:
+    return lib().orbref_level_cells(w, h)
 
 
 def distribute(cands: np.ndarray, w: int, h: int, N: int) -> np.ndarray:

@@ -155,10 +155,10 @@ struct orbx_handle {
     std::vector<std::vector<uint8_t>> h_levels;
     std::vector<bool> level_cached;
 
-    // timing
+    // timing: one set of 5 events per timed extract call (stage boundaries)
     bool timing = false;
-    hipEvent_t ev[5] = {};
-    bool timed = false;
+    std::vector<hipEvent_t> ev;
+    int ev_used = 0;
 };
 
 namespace {
@@ -314,16 +314,25 @@ orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_key
     ExtractBufs b = bufs(h);
     hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
     hipMemsetAsync(h->d_status, 0, sizeof(int), s);
-    if (h->timing) hipEventRecord(h->ev[0], s);
+    hipEvent_t* ev = nullptr;
+    if (h->timing) {
+        if ((size_t)(h->ev_used + 1) * 5 > h->ev.size()) {
+            const size_t old = h->ev.size();
+            h->ev.resize(old + 5 * 64);
+            for (size_t i = old; i < h->ev.size(); ++i) hipEventCreate(&h->ev[i]);
+        }
+        ev = &h->ev[(size_t)h->ev_used * 5];
+        h->ev_used++;
+    }
+    if (ev) hipEventRecord(ev[0], s);
     launch_pyramid(g, b, P, batch, s);
-    if (h->timing) hipEventRecord(h->ev[1], s);
+    if (ev) hipEventRecord(ev[1], s);
     launch_fast(g, b, P, batch, s);
-    if (h->timing) hipEventRecord(h->ev[2], s);
+    if (ev) hipEventRecord(ev[2], s);
     launch_quadtree(g, b, counts, batch, s);
-    if (h->timing) hipEventRecord(h->ev[3], s);
+    if (ev) hipEventRecord(ev[3], s);
     launch_describe(g, b, P, kps, desc, cap, batch, s);
-    if (h->timing) hipEventRecord(h->ev[4], s);
-    h->timed = h->timing;
+    if (ev) hipEventRecord(ev[4], s);
     h->last = P;
     h->last_batch = batch;
     std::fill(h->level_cached.begin(), h->level_cached.end(), false);
@@ -367,7 +376,6 @@ orbx_status orbx_create(const orbx_params* params, int device, orbx_handle** out
         delete h;
         return ORBX_EDEVICE;
     }
-    for (auto& e : h->ev) hipEventCreate(&e);
     h->h_levels.resize(kMaxLevels);
     h->level_cached.assign(kMaxLevels, false);
     *out = h;
@@ -504,7 +512,7 @@ orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int
     orbx_status st = ensure_geometry(h, rows, cols);
     if (st != ORBX_OK) return st;
     if ((st = ensure_batch(h, batch)) != ORBX_OK) return st;
-    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    hipStream_t s = (hipStream_t)stream;   // taken literally: NULL is the HIP null stream
     FramePtrs P{d_imgs, frame_stride, (int)step, h->d_pyr, (size_t)h->geom.pyr_bytes};
     return run_pipeline(h, P, batch, d_kps, d_desc, d_counts, cap, s);
 }
@@ -513,7 +521,7 @@ orbx_status orbx_sync(orbx_handle* h, void* stream)
 {
     if (!h) return ORBX_EINVAL;
     hipSetDevice(h->device);
-    if (stream && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return ORBX_EDEVICE;
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return ORBX_EDEVICE;
     if (!h->d_status) return ORBX_OK;
     return status_from_device(h);
 }
@@ -522,14 +530,23 @@ orbx_status orbx_set_timing(orbx_handle* h, int enable)
 {
     if (!h) return ORBX_EINVAL;
     h->timing = enable != 0;
+    h->ev_used = 0;   // (re)start accumulation
     return ORBX_OK;
 }
 
 orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n)
 {
-    if (!h || !ms || !h->timed) return ORBX_EINVAL;
-    if (hipEventSynchronize(h->ev[4]) != hipSuccess) return ORBX_EDEVICE;
-    for (int i = 0; i < n && i < 4; ++i) hipEventElapsedTime(&ms[i], h->ev[i], h->ev[i + 1]);
+    if (!h || !ms || h->ev_used == 0) return ORBX_EINVAL;
+    if (hipEventSynchronize(h->ev[(size_t)h->ev_used * 5 - 1]) != hipSuccess) return ORBX_EDEVICE;
+    for (int i = 0; i < n && i < 4; ++i) ms[i] = 0.f;
+    for (int c = 0; c < h->ev_used; ++c) {
+        const hipEvent_t* e = &h->ev[(size_t)c * 5];
+        for (int i = 0; i < n && i < 4; ++i) {
+            float t = 0.f;
+            hipEventElapsedTime(&t, e[i], e[i + 1]);
+            ms[i] += t;
+        }
+    }
     return ORBX_OK;
 }
 

@@ -196,7 +196,7 @@ class ORBextractor:
         _check("orbx_extract_batch_device", rc)
 
     def sync(self, stream=None):
-        _check("orbx_sync", lib.orbx_sync(self._h, _stream(stream) if stream is not None else None))
+        _check("orbx_sync", lib.orbx_sync(self._h, _stream(stream)))
 
     def set_timing(self, enable=True):
         _check("orbx_set_timing", lib.orbx_set_timing(self._h, 1 if enable else 0))

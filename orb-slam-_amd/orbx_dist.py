@@ -1,0 +1,71 @@
+"""Frame-sharded multi-GPU replay (BASELINE.json config 4).
+
+Frames are independent (ORBextractor::operator() depends only on the image),
+so frame i goes to rank i mod G ... here: rank r owns a contiguous block of
+frames, which also keeps the SearchForInitialization pairs (t-1, t) local.
+The only collective is the hand-back of every rank's keypoints/descriptors to
+rank 0, where the unchanged Tracking/Optimizer would consume them.
+
+Payload per rank = one flat uint8 buffer holding, for B frames with per-frame
+capacity `cap`:  kps  [B, cap, 7] int32 (cv::KeyPoint, 28 B)
+                 desc [B, cap, 32] uint8
+                 counts [B] int32
+so the extractor writes straight into the buffer that is sent (no pack copy).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_frames: int, rank: int, world: int):
+    """Contiguous block of frames owned by `rank`."""
+    per = (n_frames + world - 1) // world
+    a = min(n_frames, rank * per)
+    return a, min(n_frames, a + per)
+
+
+class Payload:
+    def __init__(self, batch: int, cap: int, device):
+        self.batch, self.cap = batch, cap
+        self.kps_bytes = batch * cap * 28
+        self.desc_bytes = batch * cap * 32
+        self.nbytes = self.kps_bytes + self.desc_bytes + batch * 4
+        self.buf = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+        self.kps = self.buf[:self.kps_bytes].view(torch.int32).view(batch, cap, 7)
+        self.desc = self.buf[self.kps_bytes:self.kps_bytes + self.desc_bytes].view(batch, cap, 32)
+        self.counts = self.buf[self.kps_bytes + self.desc_bytes:].view(torch.int32)
+
+    @staticmethod
+    def unpack(buf: torch.Tensor, batch: int, cap: int):
+        kb, db = batch * cap * 28, batch * cap * 32
+        kps = buf[:kb].view(torch.int32).view(batch, cap, 7)
+        desc = buf[kb:kb + db].view(batch, cap, 32)
+        counts = buf[kb + db:kb + db + batch * 4].view(torch.int32)
+        return kps, desc, counts
+
+
+class Gatherer:
+    """Collects every rank's payload on rank 0 (RCCL over xGMI for backend 'nccl').
+
+    Uses point-to-point sends to rank 0: each peer pushes over its own xGMI
+    link, which is what a rank-0 collection needs on a point-to-point fabric
+    (a ring all-gather would push (G-1)x the bytes through every link)."""
+
+    def __init__(self, payload: Payload, world: int, rank: int):
+        self.world, self.rank = world, rank
+        self.payload = payload
+        self.recv = None
+        if rank == 0 and world > 1:
+            self.recv = [torch.empty_like(payload.buf) for _ in range(world - 1)]
+
+    def gather(self):
+        if self.world == 1:
+            return [self.payload.buf]
+        if self.rank == 0:
+            ops = [dist.P2POp(dist.irecv, self.recv[r - 1], r) for r in range(1, self.world)]
+        else:
+            ops = [dist.P2POp(dist.isend, self.payload.buf, 0)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        return [self.payload.buf] + self.recv if self.rank == 0 else None

@@ -173,3 +173,34 @@ def test_allpairs(orbref, cuda, nq, nt):
     assert np.array_equal(bi.cpu().numpy()[sel], wi)
     assert np.array_equal(b1.cpu().numpy()[sel], w1)
     assert np.array_equal(b2.cpu().numpy()[sel], w2)
+
+
+def test_extract_then_match_same_stream_without_host_sync(orbref, cuda):
+    """Regression: extract and match queued back to back on one stream (the bench
+    pattern) must give the same matches as with a host sync in between."""
+    import torch
+    import orbx
+    frames = _frames("kitti", 1241, 376, 3)
+    ex = _extractor(2000)
+    imgs = torch.from_numpy(frames).to(cuda)
+    cap = ex.capacity(376, 1241)
+    m = orbx.ORBmatcher(0.9, True)
+    pa = torch.tensor([0, 1], dtype=torch.int32, device=cuda)
+    pb = torch.tensor([1, 2], dtype=torch.int32, device=cuda)
+    outs = []
+    for s in (torch.cuda.current_stream(), torch.cuda.Stream()):
+        with torch.cuda.stream(s):
+            kps = torch.empty((3, cap, 7), dtype=torch.int32, device=cuda)
+            desc = torch.empty((3, cap, 32), dtype=torch.uint8, device=cuda)
+            counts = torch.empty((3,), dtype=torch.int32, device=cuda)
+            ex.extract_batch_device(imgs, kps, desc, counts, s)
+            m12, nm = m.search_for_initialization_batch(kps, desc, counts, pa, pb, 376, 1241, 100, stream=s)
+            s.synchronize()
+            outs.append((m12.cpu().numpy(), nm.cpu().numpy()))
+    klist = orbx.keypoints_from_device(kps, counts)
+    d = desc.cpu().numpy()
+    c = counts.cpu().numpy()
+    want_n, want_m, _ = orbref.search_for_initialization(klist[0], d[0, :c[0]], klist[1], d[1, :c[1]], 1241, 376)
+    for m12, nm in outs:
+        assert nm[0] == want_n and want_n > 50
+        assert np.array_equal(m12[0, :len(want_m)], want_m)
