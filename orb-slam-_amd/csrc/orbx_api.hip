@@ -642,7 +642,7 @@ orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint
                                           int cols, int window, float nnratio, int check_ori, int* d_matches12,
                                           int* d_nmatches, void* stream)
 {
-    if (!d_kps || !d_desc || !d_counts || cap <= 0 || cap > 65535 || npairs < 0 || rows <= 0 || cols <= 0)
+    if (!d_kps || !d_desc || !d_counts || cap <= 0 || cap > 32767 || npairs < 0 || rows <= 0 || cols <= 0)
         return ORBX_EINVAL;
     if (npairs == 0) return ORBX_OK;
     hipStream_t s = (hipStream_t)stream;

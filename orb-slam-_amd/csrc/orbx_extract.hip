@@ -689,6 +689,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(const Geometry* __restrict__
 void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s)
 {
     const size_t smem = quadtree_smem_bytes(g);
+    hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     dim3 grid(g.nlevels, batch);
     hipLaunchKernelGGL(k_quadtree, grid, dim3(QT_NT), smem, s, b.geom, b.cells, b.slots, b.cell_counts,
                        b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);

@@ -154,17 +154,21 @@ void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, ui
 }
 
 // ---------------------------------------------------------------------------
-// M1: SearchForInitialization for one frame pair per workgroup.
-//   1. F2's level-0 keypoints are ordered like Frame::GetFeaturesInArea visits
-//      them: grid cell (ix outer, iy inner, Frame::PosInGrid rounding), then
-//      index (AssignFeaturesToGrid insertion order), src/Frame.cc:292-518.
-//   2. All waves build every level-0 query's candidate list (window test and
-//      Hamming distance) in that order: CSR in global scratch.
+// M1: SearchForInitialization for one frame pair per workgroup (512 threads).
+//   1. F2's level-0 keypoints are sorted the way Frame::GetFeaturesInArea
+//      visits them: grid cell (ix outer, iy inner, Frame::PosInGrid rounding),
+//      then index (AssignFeaturesToGrid insertion order), src/Frame.cc:292-518.
+//      Keys and positions stay in LDS.
+//   2. Every wave takes level-0 queries; a query's window columns are one
+//      contiguous key range (binary search), filtered by row and |dx|,|dy| < r.
+//      Candidate lists (i2, Hamming) are written in visit order, CSR, in LDS
+//      (global scratch only if a pair overflows the LDS budget).
 //   3. One wave replays the greedy pass in query order (vMatchedDistance skip,
 //      best/second, ratio test, eviction), then the rotation-histogram filter
 //      (ComputeThreeMaxima, src/ORBmatcher.cc:1679-1723).
 // ---------------------------------------------------------------------------
 constexpr int kGridCols = 64, kGridRows = 48;
+constexpr int SI_NT = 512, SI_NW = SI_NT / 64;
 
 __device__ __forceinline__ void bitonic_asc(uint32_t* k, int p2)
 {
@@ -185,44 +189,63 @@ __device__ __forceinline__ void bitonic_asc(uint32_t* k, int p2)
     }
 }
 
-struct Window {
-    int cx0, cx1, cy0, cy1;
-    bool empty;
-};
-
-// Frame::GetFeaturesInArea cell range, src/Frame.cc:421-440 (float arithmetic as written)
-__device__ __forceinline__ Window window_cells(float x, float y, float r, float invW, float invH)
+__device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t v)
 {
-    Window w;
-    const float minX = 0.0f, minY = 0.0f;
-    w.cx0 = max(0, (int)floorf((x - minX - r) * invW));
-    w.cx1 = min(kGridCols - 1, (int)ceilf((x - minX + r) * invW));
-    w.cy0 = max(0, (int)floorf((y - minY - r) * invH));
-    w.cy1 = min(kGridRows - 1, (int)ceilf((y - minY + r) * invH));
-    w.empty = w.cx0 >= kGridCols || w.cx1 < 0 || w.cy0 >= kGridRows || w.cy1 < 0;
-    return w;
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
 }
 
-__global__ __launch_bounds__(256) void k_search_init(const orbx_keypoint* __restrict__ kps,
-                                                     const uint8_t* __restrict__ desc,
-                                                     const int* __restrict__ counts, int cap,
-                                                     const int* __restrict__ pa, const int* __restrict__ pb,
-                                                     int rows, int cols, int window, float nnratio, int check_ori,
-                                                     uint32_t* __restrict__ cand, int cand_per_pair,
-                                                     int* __restrict__ m12_out, int* __restrict__ nm_out)
+struct SiLayout {
+    size_t keys, gxy, off, mdist, m21, m12, bin, cand, total;
+};
+
+__host__ __device__ inline SiLayout si_layout(int cap, int cand_lds)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    SiLayout L;
     int p2 = 1;
     while (p2 < cap) p2 <<= 1;
-    uint32_t* keys = (uint32_t*)smem;                 // [p2]
-    uint32_t* off = keys + p2;                        // [cap + 1]
-    int* mdist = (int*)(off + cap + 1);               // [cap]
-    int* m21 = mdist + cap;                           // [cap]
-    int* m12 = m21 + cap;                             // [cap]
-    int* bin = m12 + cap;                             // [cap]
+    size_t o = 0;
+    auto take = [&](size_t b) {
+        const size_t r = o;
+        o += (b + 15) & ~(size_t)15;
+        return r;
+    };
+    L.keys = take(4 * (size_t)p2);
+    L.gxy = take(8 * (size_t)cap);
+    L.off = take(4 * ((size_t)cap + 1));
+    L.mdist = take(2 * (size_t)cap);
+    L.m21 = take(2 * (size_t)cap);
+    L.m12 = take(2 * (size_t)cap);
+    L.bin = take((size_t)cap);
+    L.cand = take(4 * (size_t)cand_lds);
+    L.total = o;
+    return L;
+}
+
+__global__ __launch_bounds__(SI_NT) void k_search_init(const orbx_keypoint* __restrict__ kps,
+                                                       const uint8_t* __restrict__ desc,
+                                                       const int* __restrict__ counts, int cap,
+                                                       const int* __restrict__ pa, const int* __restrict__ pb,
+                                                       int rows, int cols, int window, float nnratio, int check_ori,
+                                                       uint32_t* __restrict__ cand_g, int cand_per_pair, int cand_lds,
+                                                       int* __restrict__ m12_out, int* __restrict__ nm_out)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const SiLayout Ly = si_layout(cap, cand_lds);
+    uint32_t* keys = (uint32_t*)(smem + Ly.keys);
+    float2* gxy = (float2*)(smem + Ly.gxy);
+    uint32_t* off = (uint32_t*)(smem + Ly.off);
+    uint16_t* mdist = (uint16_t*)(smem + Ly.mdist);
+    int16_t* m21 = (int16_t*)(smem + Ly.m21);
+    int16_t* m12 = (int16_t*)(smem + Ly.m12);
+    int8_t* bin = (int8_t*)(smem + Ly.bin);
+    uint32_t* cand_l = (uint32_t*)(smem + Ly.cand);
     __shared__ int s_n[4];
     __shared__ int s_hist[32];
-    __shared__ uint32_t s_wsum[5];
 
     const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int fa = pa[pair], fb = pb[pair];
@@ -231,74 +254,92 @@ __global__ __launch_bounds__(256) void k_search_init(const orbx_keypoint* __rest
     const uint8_t* d1 = desc + (size_t)fa * cap * 32;
     const uint8_t* d2 = desc + (size_t)fb * cap * 32;
     const int n1 = min(counts[fa], cap), n2 = min(counts[fb], cap);
-    if (tid == 0) { s_n[0] = 0; s_n[1] = 0; }
+    if (tid < 4) s_n[tid] = 0;
     __syncthreads();
     // level-0 keypoints come first (src/ORBextractor.cc:1290-1333)
     int c1 = 0, c2 = 0;
-    for (int i = tid; i < n1; i += 256) c1 += k1[i].octave == 0;
-    for (int i = tid; i < n2; i += 256) c2 += k2[i].octave == 0;
-    atomicAdd(&s_n[0], c1);
-    atomicAdd(&s_n[1], c2);
+    for (int i = tid; i < n1; i += SI_NT) c1 += k1[i].octave == 0;
+    for (int i = tid; i < n2; i += SI_NT) c2 += k2[i].octave == 0;
+    if (c1) atomicAdd(&s_n[0], c1);
+    if (c2) atomicAdd(&s_n[1], c2);
     __syncthreads();
     const int n10 = s_n[0], n20 = s_n[1];
+    int p2 = 1;
+    while (p2 < n20) p2 <<= 1;
 
     const float invW = (float)kGridCols / ((float)cols - 0.0f);
     const float invH = (float)kGridRows / ((float)rows - 0.0f);
-    for (int i = tid; i < p2; i += 256) {
+    for (int i = tid; i < p2; i += SI_NT) {
         uint32_t key = 0xFFFFFFFFu;
         if (i < n20) {
             const int px = (int)roundf((k2[i].x - 0.0f) * invW);
             const int py = (int)roundf((k2[i].y - 0.0f) * invH);
-            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows)
+            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {
                 key = ((uint32_t)(px * kGridRows + py) << 16) | (uint32_t)i;
+                atomicAdd(&s_n[2], 1);
+            }
         }
         keys[i] = key;
     }
     __syncthreads();
-    bitonic_asc(keys, p2);
-    int ng = 0;
-    for (int i = 0; i < n20; ++i) ng += keys[i] != 0xFFFFFFFFu;   // uniform, cheap (n20 small)
+    bitonic_asc(keys, p2);   // invalid keys (outside the grid, PosInGrid false) sort last
+    const int ng_ = s_n[2];
+    for (int g = tid; g < ng_; g += SI_NT) {
+        const int i2 = (int)(keys[g] & 0xFFFF);
+        gxy[g] = make_float2(k2[i2].x, k2[i2].y);
+    }
+    __syncthreads();
+    const int ng = ng_;
 
     const float r = (float)window;
-    uint32_t* pc = cand + (size_t)pair * cand_per_pair;
-    // pass A1/A2: count then write candidate lists (one wave per query)
+    uint32_t* pc = cand_l;
     for (int pass = 0; pass < 2; ++pass) {
-        for (int i1 = wave; i1 < n10; i1 += 4) {
+        for (int i1 = wave; i1 < n10; i1 += SI_NW) {
             const float x = k1[i1].x, y = k1[i1].y;
-            const Window W = window_cells(x, y, r, invW, invH);
+            // Frame::GetFeaturesInArea(x, y, r, 0, 0) cell range, src/Frame.cc:421-440
+            const int cx0 = max(0, (int)floorf((x - 0.0f - r) * invW));
+            const int cx1 = min(kGridCols - 1, (int)ceilf((x - 0.0f + r) * invW));
+            const int cy0 = max(0, (int)floorf((y - 0.0f - r) * invH));
+            const int cy1 = min(kGridRows - 1, (int)ceilf((y - 0.0f + r) * invH));
             int base = pass ? (int)off[i1] : 0;
-            const int limit = pass ? (int)off[i1 + 1] : 0;
-            const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
-            const ulonglong2 a0 = a[0], a1 = a[1];
-            for (int g0 = 0; g0 < ng; g0 += 64) {
-                const int g = g0 + lane;
-                bool in = false;
-                int i2 = 0;
-                if (!W.empty && g < ng) {
-                    const uint32_t key = keys[g];
-                    const int cell = (int)(key >> 16);
-                    const int ix = cell / kGridRows, iy = cell - ix * kGridRows;
-                    i2 = (int)(key & 0xFFFF);
-                    if (ix >= W.cx0 && ix <= W.cx1 && iy >= W.cy0 && iy <= W.cy1) {
-                        const float dx = k2[i2].x - x, dy = k2[i2].y - y;
-                        in = fabsf(dx) < r && fabsf(dy) < r;
+            if (cx0 < kGridCols && cx1 >= 0 && cy0 < kGridRows && cy1 >= 0) {
+                const int lo = lower_bound_u32(keys, ng, (uint32_t)(cx0 * kGridRows) << 16);
+                const int hi = lower_bound_u32(keys, ng, (uint32_t)((cx1 + 1) * kGridRows) << 16);
+                ulonglong2 a0 = make_ulonglong2(0, 0), a1 = a0;
+                if (pass) {
+                    const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
+                    a0 = a[0];
+                    a1 = a[1];
+                }
+                for (int g0 = lo; g0 < hi; g0 += 64) {
+                    const int g = g0 + lane;
+                    bool in = false;
+                    int i2 = 0;
+                    if (g < hi) {
+                        const uint32_t key = keys[g];
+                        const int iy = (int)(key >> 16) % kGridRows;
+                        if (iy >= cy0 && iy <= cy1) {
+                            const float2 p = gxy[g];
+                            in = fabsf(p.x - x) < r && fabsf(p.y - y) < r;
+                            i2 = (int)(key & 0xFFFF);
+                        }
                     }
+                    const unsigned long long m = __ballot(in);
+                    if (pass && in) {
+                        const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)i2 * 32);
+                        const int d = ham256(a0, a1, b[0], b[1]);
+                        const int idx = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                                   (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        pc[idx] = (uint32_t)i2 | ((uint32_t)d << 16);
+                    }
+                    base += __popcll(m);
                 }
-                const unsigned long long m = __ballot(in);
-                if (pass && in) {
-                    const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)i2 * 32);
-                    const int d = ham256(a0, a1, b[0], b[1]);
-                    const int idx = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    if (idx < limit) pc[idx] = (uint32_t)i2 | ((uint32_t)d << 16);
-                }
-                base += __popcll(m);
             }
             if (!pass && lane == 0) off[i1] = (uint32_t)base;
         }
         __syncthreads();
         if (!pass) {
-            // exclusive scan of off[0..n10) (single wave; n10 is a few hundred)
+            // exclusive scan of off[0..n10) (one wave; n10 is a few hundred)
             if (wave == 0) {
                 uint32_t run = 0;
                 for (int b0 = 0; b0 < n10; b0 += 64) {
@@ -314,22 +355,26 @@ __global__ __launch_bounds__(256) void k_search_init(const orbx_keypoint* __rest
                 }
                 if (lane == 0) {
                     off[n10] = run;
-                    s_n[2] = (int)run > cand_per_pair ? 1 : 0;
+                    s_n[3] = (int)run;
                 }
             }
             __syncthreads();
-            if (s_n[2]) {   // scratch too small: clamp lists (reported through nmatches = -1)
-                for (int i = tid; i <= n10; i += 256) off[i] = min(off[i], (uint32_t)cand_per_pair);
-                __syncthreads();
+            const int total = s_n[3];
+            if (total > cand_lds) {
+                if (total > cand_per_pair) {   // cannot hold the lists: report, do nothing
+                    for (int i = tid; i < cap; i += SI_NT) m12_out[(size_t)pair * cap + i] = -1;
+                    if (tid == 0) nm_out[pair] = -1;
+                    return;
+                }
+                pc = cand_g + (size_t)pair * cand_per_pair;
             }
         }
     }
-    (void)s_wsum;
 
     if (wave != 0) return;
     // pass B: the reference's sequential greedy loop
     for (int i = lane; i < n2; i += 64) {
-        mdist[i] = INT_MAX;
+        mdist[i] = 0xFFFF;   // INT_MAX: larger than any distance
         m21[i] = -1;
     }
     for (int i = lane; i < n1; i += 64) {
@@ -349,7 +394,7 @@ __global__ __launch_bounds__(256) void k_search_init(const orbx_keypoint* __rest
         for (int j = o0 + lane; j < o1; j += 64) {
             const uint32_t e = pc[j];
             const int i2 = (int)(e & 0xFFFF), d = (int)(e >> 16);
-            if (mdist[i2] <= d) continue;
+            if ((int)mdist[i2] <= d) continue;
             if (d < b1) {
                 b2 = b1;
                 b1 = d;
@@ -376,16 +421,16 @@ __global__ __launch_bounds__(256) void k_search_init(const orbx_keypoint* __rest
                     m12[m21[bi]] = -1;
                     --nmatches;
                 }
-                m12[i1] = bi;
-                m21[bi] = i1;
-                mdist[bi] = b1;
+                m12[i1] = (int16_t)bi;
+                m21[bi] = (int16_t)i1;
+                mdist[bi] = (uint16_t)b1;
                 ++nmatches;
                 if (check_ori) {
                     float rot = k1[i1].angle - k2[bi].angle;
                     if (rot < 0.0f) rot += 360.0f;
                     int bb = (int)roundf(rot * factor);
                     if (bb == 30) bb = 0;
-                    bin[i1] = bb;
+                    bin[i1] = (int8_t)bb;
                     s_hist[bb] += 1;
                 }
             }
@@ -421,19 +466,27 @@ __global__ __launch_bounds__(256) void k_search_init(const orbx_keypoint* __rest
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     int* out = m12_out + (size_t)pair * cap;
-    for (int i = lane; i < cap; i += 64) out[i] = i < n1 ? m12[i] : -1;
-    if (lane == 0) nm_out[pair] = s_n[2] ? -1 : nmatches;
+    for (int i = lane; i < cap; i += 64) out[i] = i < n1 ? (int)m12[i] : -1;
+    if (lane == 0) nm_out[pair] = nmatches;
+}
+
+int search_init_cand_lds(int cap)
+{
+    // LDS left for candidate lists after the per-pair arrays (160 KiB per CU, one pair per workgroup)
+    const size_t fixed = si_layout(cap, 0).total + 256;
+    const long left = (long)(160 * 1024) - (long)fixed;
+    return left > 0 ? (int)(left / 4) : 0;
 }
 
 void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int cap, const int* pa,
                         const int* pb, int npairs, int rows, int cols, int window, float nnratio, int check_ori,
                         uint32_t* cand, int cand_per_pair, int* m12, int* nm, hipStream_t s)
 {
-    int p2 = 1;
-    while (p2 < cap) p2 <<= 1;
-    const size_t smem = sizeof(uint32_t) * (p2 + cap + 1) + sizeof(int) * 4 * cap;
-    hipLaunchKernelGGL(k_search_init, dim3(npairs), dim3(256), smem, s, kps, desc, counts, cap, pa, pb, rows, cols,
-                       window, nnratio, check_ori, cand, cand_per_pair, m12, nm);
+    const int cand_lds = search_init_cand_lds(cap);
+    const size_t smem = si_layout(cap, cand_lds).total;
+    hipFuncSetAttribute((const void*)k_search_init, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL(k_search_init, dim3(npairs), dim3(SI_NT), smem, s, kps, desc, counts, cap, pa, pb, rows, cols,
+                       window, nnratio, check_ori, cand, cand_per_pair, cand_lds, m12, nm);
 }
 
 }  // namespace orbx
