@@ -204,3 +204,24 @@ def test_extract_then_match_same_stream_without_host_sync(orbref, cuda):
     for m12, nm in outs:
         assert nm[0] == want_n and want_n > 50
         assert np.array_equal(m12[0, :len(want_m)], want_m)
+
+
+def test_cpp_mirror_example(orbref, cuda, tmp_path):
+    """The C++ ORBextractor mirror (orb-slam-_amd/host/ORBextractor.hpp) end to end."""
+    import os
+    import subprocess
+    import orbx_synth
+    from orbref import KEYPOINT_DTYPE
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "orb-slam-_amd", "build", "extract_example")
+    img = orbx_synth.gen_image(31, 752, 480)
+    src = tmp_path / "in.raw"
+    out = tmp_path / "out.bin"
+    img.tofile(src)
+    subprocess.check_call([exe, str(src), "480", "752", "1000", str(out)], timeout=120)
+    raw = out.read_bytes()
+    n = int(np.frombuffer(raw[:4], np.int32)[0])
+    kps = np.frombuffer(raw[4:4 + 28 * n], KEYPOINT_DTYPE)
+    desc = np.frombuffer(raw[4 + 28 * n:], np.uint8).reshape(n, 32)
+    ref = orbref.extract(img, orbref.make_params(1000, 1.2, 8, 20, 7))
+    assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "c++ mirror")
