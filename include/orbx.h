@@ -115,13 +115,13 @@ orbx_status orbm_allpairs_device(const uint8_t* d_q, int nq, const uint8_t* d_t,
                                  void* stream);
 
 /* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:417-588) for `npairs`
- * frame pairs (F1 = pair_a[p], F2 = pair_b[p]) of a device batch produced by
+ * frame pairs (F1 = pair_a[p], F2 = pair_b[p]) of an `nframes` device batch produced by
  * orbx_extract_batch_device (kps/desc/counts, per-frame capacity `cap`).  Grid
  * and window follow Frame::GetFeaturesInArea (src/Frame.cc:410-495) for
  * undistorted rows x cols frames; vbPrevMatched = F1 keypoint positions.
  * Outputs: d_matches12[p*cap + i1] (-1 = none), d_nmatches[p]. */
 orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint8_t* d_desc,
-                                          const int* d_counts, int cap, const int* d_pair_a,
+                                          const int* d_counts, int nframes, int cap, const int* d_pair_a,
                                           const int* d_pair_b, int npairs, int rows, int cols,
                                           int window, float nnratio, int check_ori,
                                           int* d_matches12, int* d_nmatches, void* stream);

@@ -638,20 +638,22 @@ orbx_status orbm_allpairs_device(const uint8_t* d_q, int nq, const uint8_t* d_t,
 }
 
 orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const int* d_counts,
-                                          int cap, const int* d_pair_a, const int* d_pair_b, int npairs, int rows,
-                                          int cols, int window, float nnratio, int check_ori, int* d_matches12,
-                                          int* d_nmatches, void* stream)
+                                          int nframes, int cap, const int* d_pair_a, const int* d_pair_b, int npairs,
+                                          int rows, int cols, int window, float nnratio, int check_ori,
+                                          int* d_matches12, int* d_nmatches, void* stream)
 {
-    if (!d_kps || !d_desc || !d_counts || cap <= 0 || cap > 32767 || npairs < 0 || rows <= 0 || cols <= 0)
+    if (!d_kps || !d_desc || !d_counts || nframes <= 0 || cap <= 0 || cap > 32767 || npairs < 0 || rows <= 0 ||
+        cols <= 0)
         return ORBX_EINVAL;
     if (npairs == 0) return ORBX_OK;
     hipStream_t s = (hipStream_t)stream;
     const int per = std::max(65536, 48 * cap);
-    uint32_t* cand = nullptr;
-    if (hipMallocAsync((void**)&cand, sizeof(uint32_t) * (size_t)per * npairs, s) != hipSuccess) return ORBX_ENOMEM;
-    launch_search_init(d_kps, d_desc, d_counts, cap, d_pair_a, d_pair_b, npairs, rows, cols, window, nnratio,
-                       check_ori, cand, per, d_matches12, d_nmatches, s);
-    hipFreeAsync(cand, s);
+    void* scratch = nullptr;
+    if (hipMallocAsync(&scratch, search_init_scratch_bytes(nframes, npairs, cap, per), s) != hipSuccess)
+        return ORBX_ENOMEM;
+    launch_search_init(d_kps, d_desc, d_counts, nframes, cap, d_pair_a, d_pair_b, npairs, rows, cols, window, nnratio,
+                       check_ori, scratch, per, d_matches12, d_nmatches, s);
+    hipFreeAsync(scratch, s);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 

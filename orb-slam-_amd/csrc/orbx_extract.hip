@@ -50,8 +50,11 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
                                                        const int2* __restrict__ xtab,
                                                        const int2* __restrict__ ytab)
 {
+    // 4 output pixels per thread, one dword store (level pitch is a multiple of 64)
     const int f = blockIdx.z, dy = blockIdx.y;
     const LevelGeom& D = G->lv[l];
+    const int dx0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (dx0 >= D.w) return;
     int spitch;
     const uint8_t* src = level_base(P, G, f, l - 1, spitch);
     uint8_t* dst = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy * D.pitch;
@@ -59,22 +62,28 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
     const uint8_t* r0 = src + (size_t)(yt.x & 0xFFFF) * spitch;
     const uint8_t* r1 = src + (size_t)((uint32_t)yt.x >> 16) * spitch;
     const int b0 = yt.y & 0xFFFF, b1 = (int)((uint32_t)yt.y >> 16);
-    for (int dx = blockIdx.x * 256 + threadIdx.x; dx < D.w; dx += gridDim.x * 256) {
-        const int2 xt = xtab[D.xtab_off + dx];
-        const int x0 = xt.x & 0xFFFF, x1 = (int)((uint32_t)xt.x >> 16);
-        const int a0 = xt.y & 0xFFFF, a1 = (int)((uint32_t)xt.y >> 16);
-        const int h0 = r0[x0] * a0 + r0[x1] * a1;
-        const int h1 = r1[x0] * a0 + r1[x1] * a1;
-        const int v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-        dst[dx] = (uint8_t)(v > 255 ? 255 : v);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int dx = dx0 + k;
+        if (dx < D.w) {
+            const int2 xt = xtab[D.xtab_off + dx];
+            const int x0 = xt.x & 0xFFFF, x1 = (int)((uint32_t)xt.x >> 16);
+            const int a0 = xt.y & 0xFFFF, a1 = (int)((uint32_t)xt.y >> 16);
+            const int h0 = r0[x0] * a0 + r0[x1] * a1;
+            const int h1 = r1[x0] * a0 + r1[x1] * a1;
+            const int v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+            packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
+        }
     }
+    *reinterpret_cast<uint32_t*>(dst + dx0) = packed;
 }
 
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
     for (int l = 1; l < g.nlevels; ++l) {
         const int w = g.lv[l].w, h = g.lv[l].h;
-        dim3 grid((w + 255) / 256, h, batch);
+        dim3 grid((w + 1023) / 1024, h, batch);
         hipLaunchKernelGGL(k_pyramid_level, grid, dim3(256), 0, s, b.geom, p, l, b.xtab, b.ytab);
     }
 }
@@ -92,47 +101,44 @@ constexpr int kRoiMax = 66;
 constexpr int kTileP = 68;
 constexpr int kMapMax = (kRoiMax - 4) * (kRoiMax - 4);
 
+__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
+__device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
+
+// s = max(A, -B) from the raw ring values: A = v - min over arcs of max(arc),
+// -B = max over arcs of min(arc) - v (arcs = the 16 cyclic runs of 9 ring pixels).
 __device__ __forceinline__ int fast_strength(const uint8_t* c, int st)
 {
     const int v = c[0];
-    int d[16];
-    d[0] = v - c[3 * st];
-    d[1] = v - c[3 * st + 1];
-    d[2] = v - c[2 * st + 2];
-    d[3] = v - c[st + 3];
-    d[4] = v - c[3];
-    d[5] = v - c[-st + 3];
-    d[6] = v - c[-2 * st + 2];
-    d[7] = v - c[-3 * st + 1];
-    d[8] = v - c[-3 * st];
-    d[9] = v - c[-3 * st - 1];
-    d[10] = v - c[-2 * st - 2];
-    d[11] = v - c[-st - 3];
-    d[12] = v - c[-3];
-    d[13] = v - c[st - 3];
-    d[14] = v - c[2 * st - 2];
-    d[15] = v - c[3 * st - 1];
-    int mn[16], mx[16];
+    int x[16];
+    x[0] = c[3 * st];
+    x[1] = c[3 * st + 1];
+    x[2] = c[2 * st + 2];
+    x[3] = c[st + 3];
+    x[4] = c[3];
+    x[5] = c[-st + 3];
+    x[6] = c[-2 * st + 2];
+    x[7] = c[-3 * st + 1];
+    x[8] = c[-3 * st];
+    x[9] = c[-3 * st - 1];
+    x[10] = c[-2 * st - 2];
+    x[11] = c[-st - 3];
+    x[12] = c[-3];
+    x[13] = c[st - 3];
+    x[14] = c[2 * st - 2];
+    x[15] = c[3 * st - 1];
+    int M3[16], m3[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        mn[k] = min(d[k], d[(k + 1) & 15]);
-        mx[k] = max(d[k], d[(k + 1) & 15]);
+        M3[k] = max3i(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
+        m3[k] = min3i(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
     }
-    int mn4[16], mx4[16];
+    int minMax = 255, maxMin = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        mn4[k] = min(mn[k], mn[(k + 2) & 15]);
-        mx4[k] = max(mx[k], mx[(k + 2) & 15]);
+        minMax = min(minMax, max3i(M3[k], M3[(k + 3) & 15], M3[(k + 6) & 15]));
+        maxMin = max(maxMin, min3i(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]));
     }
-    int A = -1000, B = 1000;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int m8 = min(mn4[k], mn4[(k + 4) & 15]);
-        const int M8 = max(mx4[k], mx4[(k + 4) & 15]);
-        A = max(A, min(m8, d[(k + 8) & 15]));
-        B = min(B, max(M8, d[(k + 8) & 15]));
-    }
-    return max(A, -B);
+    return max(v - minMax, maxMin - v);
 }
 
 __device__ __forceinline__ bool nms_keep(const uint8_t* m, int p, int W2, int t)
@@ -155,7 +161,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
                                                     uint32_t* __restrict__ slots,
                                                     int* __restrict__ cell_counts)
 {
-    __shared__ uint8_t s_tile[4][kRoiMax * kTileP];
+    __shared__ __attribute__((aligned(16))) uint8_t s_tile[4][kRoiMax * kTileP];
     __shared__ uint8_t s_map[4][kMapMax];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
@@ -173,54 +179,71 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
         if (lane == 0) *out_count = 0;
         return;
     }
+    // ROI -> LDS as aligned dwords (alignbyte realigns rows of any pitch); the ROI
+    // ends >= 16 px before the level's right edge, so the 8-byte read stays in the row
     const uint8_t* src = img + (size_t)C.roi_y0 * pitch + C.roi_x0;
-    for (int i = lane; i < rw * rh; i += 64) {
-        const int r = i / rw, q = i - r * rw;
-        tile[r * kTileP + q] = src[(size_t)r * pitch + q];
+    const int nd = (rw + 3) >> 2;
+    for (int i = lane; i < rh * nd; i += 64) {
+        const int r = i / nd, k = i - r * nd;
+        const uintptr_t a = (uintptr_t)(src + (size_t)r * pitch + 4 * k);
+        const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
+        const uint32_t lo = ap[0], hi = ap[1];
+        *(uint32_t*)(tile + r * kTileP + 4 * k) = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3));
     }
     const int W2 = dw + 2;
     for (int i = lane; i < W2 * (dh + 2); i += 64) map[i] = 0;
     wave_lds_sync();
 
     const int npx = dw * dh;
+    const float inv_dw = 1.0f / (float)dw;   // exact row/col split for npx < 4096
     for (int k = lane; k < npx; k += 64) {
-        const int ii = k / dw, jj = k - ii * dw;
+        const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
         const int s = fast_strength(tile + (ii + 3) * kTileP + (jj + 3), kTileP);
         map[(ii + 1) * W2 + jj + 1] = (uint8_t)(s > 0 ? s : 0);
     }
     wave_lds_sync();
 
+    // NMS at iniThFAST; survivors remembered per round so the common case needs one pass
     const int rounds = (npx + 63) >> 6;
+    unsigned long long keepmask = 0;   // bit r: this lane's pixel of round r survives (rounds <= 57)
     int t = G->ini_th;
     int kept = 0;
     for (int r = 0; r < rounds; ++r) {
         const int k = lane + (r << 6);
         bool keep = false;
         if (k < npx) {
-            const int ii = k / dw, jj = k - ii * dw;
+            const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
             keep = nms_keep(map, (ii + 1) * W2 + jj + 1, W2, t);
         }
+        keepmask |= (unsigned long long)keep << r;
         kept += __popcll(__ballot(keep));
     }
-    if (kept == 0) t = G->min_th;
+    if (kept == 0) {   // src/ORBextractor.cc:982-987: retry the cell at minThFAST
+        t = G->min_th;
+        keepmask = 0;
+        for (int r = 0; r < rounds; ++r) {
+            const int k = lane + (r << 6);
+            bool keep = false;
+            if (k < npx) {
+                const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
+                keep = nms_keep(map, (ii + 1) * W2 + jj + 1, W2, t);
+            }
+            keepmask |= (unsigned long long)keep << r;
+        }
+    }
 
     uint32_t* out = slots + (size_t)f * G->slots_per_frame + C.slot_base;
     const int xr0 = C.roi_x0 + 3 - kMinBorder, yr0 = C.roi_y0 + 3 - kMinBorder;
     int base = 0;
     for (int r = 0; r < rounds; ++r) {
-        const int k = lane + (r << 6);
-        bool keep = false;
-        int ii = 0, jj = 0, p = 0;
-        if (k < npx) {
-            ii = k / dw;
-            jj = k - ii * dw;
-            p = (ii + 1) * W2 + jj + 1;
-            keep = nms_keep(map, p, W2, t);
-        }
+        const bool keep = (keepmask >> r) & 1ull;
         const unsigned long long m = __ballot(keep);
         if (keep) {
+            const int k = lane + (r << 6);
+            const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
             const int idx = base + lanes_below(m);
-            out[idx] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + ii), (uint32_t)(map[p] - 1));
+            out[idx] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + ii),
+                               (uint32_t)(map[(ii + 1) * W2 + jj + 1] - 1));
         }
         base += __popcll(m);
     }
@@ -696,13 +719,23 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 }
 
 // ---------------------------------------------------------------------------
-// K4: one wave per retained keypoint.  The 43x43 raw neighbourhood (reflect-101
-// at level borders) is staged in LDS; IC_Angle sums the 789-pixel disc with a
-// wave reduction; the 7x7 integer Gaussian (kernel [18 34 49 55 49 34 18]/2^16,
-// SURVEY.md A.3) is evaluated on the 37x37 BRIEF support only; the 256 tests
-// become four __ballot words = the descriptor's little-endian u64 words.
+// K4: one wave per retained keypoint.
+//   raw   43x43 neighbourhood (reflect-101 at level borders) in LDS; interior
+//         keypoints load it as aligned dwords realigned with v_alignbyte.
+//   angle IC_Angle: u*I and v*I over the 749-pixel disc, wave reduction, then
+//         cv::fastAtan2 (src/ORBextractor.cc:84-128).
+//   blur  GaussianBlur 7x7 integer kernel [18 34 49 55 49 34 18], >>16
+//         (SURVEY.md A.3): the horizontal pass is v_dot4_u32_u8 on 4 output
+//         columns x 2 rows per lane, stored transposed as u16 row pairs; the
+//         vertical pass is evaluated only at the 512 BRIEF sample points with
+//         four v_dot2_u32_u16 each.
+//   BRIEF fmaf sample coordinates, 256 tests -> four __ballot
+//         words = the descriptor's little-endian u64 words (:141-192).
 // ---------------------------------------------------------------------------
-constexpr int kRawN = 43, kRawP = 44, kBlN = 37;
+constexpr int kRawRows = 44, kRawP = 48;      // 43 rows used, byte pitch 48 (12 dwords)
+constexpr int kTCols = 40, kTP = 22;           // row-blurred, transposed: [col][row pairs], 22 dwords/col
+
+__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
 __device__ __forceinline__ int reflect101(int p, int len)
 {
@@ -718,15 +751,44 @@ __device__ __forceinline__ int wave_sum(int v)
     return v;
 }
 
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ ushort2_t as_us2(uint32_t v)
+{
+    ushort2_t r;
+    r.x = (unsigned short)(v & 0xFFFF);
+    r.y = (unsigned short)(v >> 16);
+    return r;
+}
+
+// blurred value at patch row y (0..36), column x (0..36): sum_t k[t] * rowblur[y+t][x]
+__device__ __forceinline__ int blur_at(const uint32_t* rowT, int y, int x)
+{
+    const uint32_t* col = rowT + x * kTP;
+    const int base = y >> 1;
+    const uint32_t d0 = col[base], d1 = col[base + 1], d2 = col[base + 2], d3 = col[base + 3];
+    // even y: rows y..y+6 = (d0.lo d0.hi d1.lo d1.hi d2.lo d2.hi d3.lo); odd y: (d0.hi .. d3.hi)
+    const bool odd = y & 1;
+    const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
+    const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
+    const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
+    const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
+    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), w0, 0u, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d1), w1, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
+    const int v = (int)((acc + (1u << 15)) >> 16);
+    return v > 255 ? 255 : v;
+}
+
 __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
                                                   const uint32_t* __restrict__ qt_out,
                                                   const int* __restrict__ qt_cnt,
                                                   orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int cap, int* __restrict__ status)
 {
-    __shared__ uint8_t s_raw[4][kRawN * kRawP];
-    __shared__ uint16_t s_row[4][kRawN * kBlN];
-    __shared__ uint8_t s_blur[4][kBlN * kBlN];
+    __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][kRawRows * kRawP / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rowT[4][kTCols * kTP];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int g = blockIdx.x * 4 + wave;
@@ -749,29 +811,34 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
     int pitch;
     const uint8_t* img = level_base(P, G, f, l, pitch);
     const int w = LG.w, h = LG.h;
-    uint8_t* raw = s_raw[wave];
-    uint16_t* row = s_row[wave];
-    uint8_t* bl = s_blur[wave];
+    uint32_t* raw32 = s_raw[wave];
+    uint8_t* raw = (uint8_t*)raw32;
+    uint32_t* rowT = s_rowT[wave];
 
-    // raw patch [cy-21, cy+21] x [cx-21, cx+21]
-    const bool inside = cx >= 21 && cy >= 21 && cx + 21 < w && cy + 21 < h;
-    for (int i = lane; i < kRawN * kRawN; i += 64) {
-        const int r = i / kRawN, c = i - r * kRawN;
-        int X = cx - 21 + c, Y = cy - 21 + r;
-        if (!inside) {
-            X = reflect101(X, w);
-            Y = reflect101(Y, h);
+    // raw patch rows cy-21..cy+21, columns cx-21..cx+26 (the last 5 only feed unused outputs)
+    if (cx >= 21 && cy >= 21 && cy + 21 < h && cx + 31 <= w) {
+        const uint8_t* src = img + (size_t)(cy - 21) * pitch + (cx - 21);
+        for (int i = lane; i < 43 * 12; i += 64) {
+            const int r = i / 12, k = i - r * 12;
+            const uintptr_t a = (uintptr_t)(src + (size_t)r * pitch + 4 * k);
+            const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
+            raw32[r * 12 + k] = __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)(a & 3));
         }
-        raw[r * kRawP + c] = img[(size_t)Y * pitch + X];
+    } else {
+        for (int i = lane; i < 43 * kRawP; i += 64) {
+            const int r = i / kRawP, c = i - r * kRawP;
+            const int X = reflect101(cx - 21 + c, w), Y = reflect101(cy - 21 + r, h);
+            raw[r * kRawP + c] = img[(size_t)Y * pitch + X];
+        }
     }
     wave_lds_sync();
 
-    // IC_Angle (src/ORBextractor.cc:84-128): m10 = sum u*I, m01 = sum v*I on the disc
+    // IC_Angle: m10 = sum u*I, m01 = sum v*I over the disc |u| <= umax[|v|]
     int m10 = 0, m01 = 0;
     for (int i = lane; i < 31 * 31; i += 64) {
         const int v = i / 31 - 15, u = i % 31 - 15;
         const int av = v < 0 ? -v : v, au = u < 0 ? -u : u;
-        if (au <= G->umax[av]) {
+        if (au <= c_umax[av]) {
             const int val = raw[(21 + v) * kRawP + 21 + u];
             m10 += u * val;
             m01 += v * val;
@@ -781,28 +848,29 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
     m01 = wave_sum(m01);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
 
-    // GaussianBlur 7x7: horizontal pass on 43 rows x 37 cols, then vertical
-    const int k7[7] = {18, 34, 49, 55, 49, 34, 18};
-    for (int i = lane; i < kRawN * kBlN; i += 64) {
-        const int r = i / kBlN, c = i - r * kBlN;
-        const uint8_t* s = raw + r * kRawP + c;
-        int acc = 0;
+    // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns
+    const uint32_t K0 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
+    const uint32_t K1 = 49u | (34u << 8) | (18u << 16);
+    for (int i = lane; i < 22 * 10; i += 64) {
+        const int rp = i / 10, cg = i - rp * 10;
+        uint32_t o[2][4];
 #pragma unroll
-        for (int t = 0; t < 7; ++t) acc += k7[t] * s[t];
-        row[r * kBlN + c] = (uint16_t)acc;
-    }
-    wave_lds_sync();
-    for (int i = lane; i < kBlN * kBlN; i += 64) {
-        const int r = i / kBlN, c = i - r * kBlN;
-        int acc = 0;
+        for (int e = 0; e < 2; ++e) {
+            const uint32_t* rr = raw32 + (2 * rp + e) * 12 + cg;
+            const uint32_t W0 = rr[0], W1 = rr[1], W2 = rr[2];
 #pragma unroll
-        for (int t = 0; t < 7; ++t) acc += k7[t] * (int)row[(r + t) * kBlN + c];
-        const int v = (acc + (1 << 15)) >> 16;
-        bl[r * kBlN + c] = (uint8_t)(v > 255 ? 255 : v);
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t A = __builtin_amdgcn_alignbyte(W1, W0, (uint32_t)j);
+                const uint32_t B = __builtin_amdgcn_alignbyte(W2, W1, (uint32_t)j);
+                o[e][j] = __builtin_amdgcn_udot4(A, K0, __builtin_amdgcn_udot4(B, K1, 0u, false), false);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
     }
     wave_lds_sync();
 
-    // rBRIEF (src/ORBextractor.cc:141-192) with the reference's contracted FMAs
+    // rBRIEF with the reference's contracted FMAs; blur evaluated at each sample point
     const float ang = angle * kFactorPI;
     const float a = glibc_sincosf(ang, 1), b = glibc_sincosf(ang, 0);
     unsigned long long words[4];
@@ -815,7 +883,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
             const float px = (float)c_pattern[4 * m + 2 * e], py = (float)c_pattern[4 * m + 2 * e + 1];
             const int yy = __float2int_rn(__builtin_fmaf(px, b, py * a));
             const int xx = __float2int_rn(__builtin_fmaf(px, a, -(py * b)));
-            t2[e] = bl[(18 + yy) * kBlN + 18 + xx];
+            t2[e] = blur_at(rowT, 18 + yy, 18 + xx);
         }
         words[wd] = __ballot(t2[0] < t2[1]);
     }

@@ -154,39 +154,36 @@ void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, ui
 }
 
 // ---------------------------------------------------------------------------
-// M1: SearchForInitialization for one frame pair per workgroup (512 threads).
-//   1. F2's level-0 keypoints are sorted the way Frame::GetFeaturesInArea
-//      visits them: grid cell (ix outer, iy inner, Frame::PosInGrid rounding),
-//      then index (AssignFeaturesToGrid insertion order), src/Frame.cc:292-518.
-//      Keys and positions stay in LDS.
-//   2. Every wave takes level-0 queries; a query's window columns are one
-//      contiguous key range (binary search), filtered by row and |dx|,|dy| < r.
-//      Candidate lists (i2, Hamming) are written in visit order, CSR, in LDS
-//      (global scratch only if a pair overflows the LDS budget).
-//   3. One wave replays the greedy pass in query order (vMatchedDistance skip,
-//      best/second, ratio test, eviction), then the rotation-histogram filter
-//      (ComputeThreeMaxima, src/ORBmatcher.cc:1679-1723).
+// M1: SearchForInitialization (src/ORBmatcher.cc:417-588) for a batch of
+// frame pairs, in three launches:
+//   k_si_grid   one workgroup per frame: its level-0 keypoints sorted the way
+//               Frame::GetFeaturesInArea visits them — grid cell (ix outer,
+//               iy inner, Frame::PosInGrid rounding), then index
+//               (AssignFeaturesToGrid insertion order), src/Frame.cc:292-518.
+//   k_si_build  (pair, query-slice) workgroups: a query's window columns are
+//               one contiguous key range (binary search in LDS), filtered by
+//               row and |dx|,|dy| < r; its candidate list (i2, Hamming) is
+//               written in visit order to the pair's CSR scratch.
+//   k_si_greedy one workgroup per pair: the CSR is staged in LDS and one wave
+//               replays the order-dependent greedy pass (vMatchedDistance
+//               skip, best/second, ratio test, eviction) and the rotation-
+//               histogram filter (ComputeThreeMaxima, :1679-1723).
 // ---------------------------------------------------------------------------
 constexpr int kGridCols = 64, kGridRows = 48;
-constexpr int SI_NT = 512, SI_NW = SI_NT / 64;
+constexpr int SI_BUILD_NT = 256, SI_QSPLIT = 8;
 
-__device__ __forceinline__ void bitonic_asc(uint32_t* k, int p2)
+// min over the 64 lanes with DPP row permutations + 4 readlanes (all lanes active)
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
-    for (int size = 2; size <= p2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < (p2 >> 1); i += blockDim.x) {
-                const int lo = 2 * i - (i & (stride - 1));
-                const int hi = lo + stride;
-                const bool asc = (lo & size) == 0;
-                const uint32_t a = k[lo], b = k[hi];
-                if ((a > b) == asc) {
-                    k[lo] = b;
-                    k[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));   // row_half_mirror
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));   // row_mirror
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(a, b), min(c, d));
 }
 
 __device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t v)
@@ -199,24 +196,172 @@ __device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_
     return lo;
 }
 
-struct SiLayout {
-    size_t keys, gxy, off, mdist, m21, m12, bin, cand, total;
+__device__ __forceinline__ int level0_count(const orbx_keypoint* k, int n)
+{
+    // keypoints are concatenated level by level (src/ORBextractor.cc:1290-1333): binary search
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (k[mid].octave == 0) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict__ kps, const int* __restrict__ counts,
+                                                 int cap, int rows, int cols, uint32_t* __restrict__ gkeys,
+                                                 float2* __restrict__ gxy, int* __restrict__ gn)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
+    __shared__ int s_ng;
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const orbx_keypoint* k = kps + (size_t)f * cap;
+    const int n = min(counts[f], cap);
+    const int n0 = level0_count(k, n);
+    int p2 = 1;
+    while (p2 < n0) p2 <<= 1;
+    if (tid == 0) s_ng = 0;
+    __syncthreads();
+    const float invW = (float)kGridCols / ((float)cols - 0.0f);
+    const float invH = (float)kGridRows / ((float)rows - 0.0f);
+    for (int i = tid; i < p2; i += 256) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (i < n0) {
+            const int px = (int)roundf((k[i].x - 0.0f) * invW);
+            const int py = (int)roundf((k[i].y - 0.0f) * invH);
+            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {   // PosInGrid
+                key = ((uint32_t)(px * kGridRows + py) << 16) | (uint32_t)i;
+                atomicAdd(&s_ng, 1);
+            }
+        }
+        keys[i] = key;
+    }
+    __syncthreads();
+    for (int size = 2; size <= p2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < (p2 >> 1); i += 256) {
+                const int lo = 2 * i - (i & (stride - 1));
+                const int hi = lo + stride;
+                const bool asc = (lo & size) == 0;
+                const uint32_t a = keys[lo], b = keys[hi];
+                if ((a > b) == asc) {
+                    keys[lo] = b;
+                    keys[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const int ng = s_ng;
+    for (int g = tid; g < ng; g += 256) {
+        const uint32_t key = keys[g];
+        const int i2 = (int)(key & 0xFFFF);
+        gkeys[(size_t)f * cap + g] = key;
+        gxy[(size_t)f * cap + g] = make_float2(k[i2].x, k[i2].y);
+    }
+    if (tid == 0) {
+        gn[2 * f] = n0;
+        gn[2 * f + 1] = ng;
+    }
+}
+
+__global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* __restrict__ kps,
+                                                          const uint8_t* __restrict__ desc, int cap,
+                                                          const int* __restrict__ pa, const int* __restrict__ pb,
+                                                          int rows, int cols, int window,
+                                                          const uint32_t* __restrict__ gkeys,
+                                                          const float2* __restrict__ gxy, const int* __restrict__ gn,
+                                                          uint32_t* __restrict__ cand, int cand_per_pair,
+                                                          int* __restrict__ qoff, int* __restrict__ qcnt,
+                                                          int* __restrict__ ptotal)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int fa = pa[pair], fb = pb[pair];
+    const int n10 = gn[2 * fa], ng = gn[2 * fb + 1];
+    uint32_t* keys = (uint32_t*)smem;
+    float2* xy = (float2*)(smem + (((size_t)cap * 4 + 15) & ~(size_t)15));
+    for (int g = tid; g < ng; g += SI_BUILD_NT) {
+        keys[g] = gkeys[(size_t)fb * cap + g];
+        xy[g] = gxy[(size_t)fb * cap + g];
+    }
+    __syncthreads();
+    const orbx_keypoint* k1 = kps + (size_t)fa * cap;
+    const uint8_t* d1 = desc + (size_t)fa * cap * 32;
+    const uint8_t* d2 = desc + (size_t)fb * cap * 32;
+    const float invW = (float)kGridCols / ((float)cols - 0.0f);
+    const float invH = (float)kGridRows / ((float)rows - 0.0f);
+    const float r = (float)window;
+    uint32_t* pc = cand + (size_t)pair * cand_per_pair;
+    const int nwaves = SI_QSPLIT * (SI_BUILD_NT / 64);
+    for (int i1 = blockIdx.y * (SI_BUILD_NT / 64) + wave; i1 < n10; i1 += nwaves) {
+        const float x = k1[i1].x, y = k1[i1].y;
+        // Frame::GetFeaturesInArea(x, y, r, 0, 0) cell range, src/Frame.cc:421-440
+        const int cx0 = max(0, (int)floorf((x - 0.0f - r) * invW));
+        const int cx1 = min(kGridCols - 1, (int)ceilf((x - 0.0f + r) * invW));
+        const int cy0 = max(0, (int)floorf((y - 0.0f - r) * invH));
+        const int cy1 = min(kGridRows - 1, (int)ceilf((y - 0.0f + r) * invH));
+        int lo = 0, hi = 0;
+        if (cx0 < kGridCols && cx1 >= 0 && cy0 < kGridRows && cy1 >= 0) {
+            lo = lower_bound_u32(keys, ng, (uint32_t)(cx0 * kGridRows) << 16);
+            hi = lower_bound_u32(keys, ng, (uint32_t)((cx1 + 1) * kGridRows) << 16);
+        }
+        auto in_window = [&](int g, int& i2) {
+            if (g >= hi) return false;
+            const uint32_t key = keys[g];
+            const int iy = (int)(key >> 16) % kGridRows;
+            if (iy < cy0 || iy > cy1) return false;
+            const float2 p = xy[g];
+            i2 = (int)(key & 0xFFFF);
+            return fabsf(p.x - x) < r && fabsf(p.y - y) < r;
+        };
+        int count = 0;
+        for (int g0 = lo; g0 < hi; g0 += 64) {
+            int i2;
+            count += __popcll(__ballot(in_window(g0 + lane, i2)));
+        }
+        int base = 0;
+        if (lane == 0 && count) base = atomicAdd(&ptotal[pair], count);
+        base = __shfl(base, 0);
+        if (lane == 0) {
+            qoff[(size_t)pair * cap + i1] = base;
+            qcnt[(size_t)pair * cap + i1] = count;
+        }
+        if (!count || base + count > cand_per_pair) continue;   // overflow is detected by k_si_greedy
+        const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
+        const ulonglong2 a0 = a[0], a1 = a[1];
+        for (int g0 = lo; g0 < hi; g0 += 64) {
+            int i2 = 0;
+            const bool in = in_window(g0 + lane, i2);
+            const unsigned long long m = __ballot(in);
+            if (in) {
+                const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)i2 * 32);
+                const int d = ham256(a0, a1, b[0], b[1]);
+                const int idx = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                pc[idx] = (uint32_t)i2 | ((uint32_t)d << 16);
+            }
+            base += __popcll(m);
+        }
+    }
+}
+
+struct SgLayout {
+    size_t off, cnt, ang1, ang2, mdist, m21, m12, bin, cand, total;
 };
 
-__host__ __device__ inline SiLayout si_layout(int cap, int cand_lds)
+__host__ __device__ inline SgLayout sg_layout(int cap, int cand_lds)
 {
-    SiLayout L;
-    int p2 = 1;
-    while (p2 < cap) p2 <<= 1;
+    SgLayout L;
     size_t o = 0;
     auto take = [&](size_t b) {
         const size_t r = o;
         o += (b + 15) & ~(size_t)15;
         return r;
     };
-    L.keys = take(4 * (size_t)p2);
-    L.gxy = take(8 * (size_t)cap);
-    L.off = take(4 * ((size_t)cap + 1));
+    L.off = take(4 * (size_t)cap);
+    L.cnt = take(4 * (size_t)cap);
+    L.ang1 = take(4 * (size_t)cap);
+    L.ang2 = take(4 * (size_t)cap);
     L.mdist = take(2 * (size_t)cap);
     L.m21 = take(2 * (size_t)cap);
     L.m12 = take(2 * (size_t)cap);
@@ -226,196 +371,91 @@ __host__ __device__ inline SiLayout si_layout(int cap, int cand_lds)
     return L;
 }
 
-__global__ __launch_bounds__(SI_NT) void k_search_init(const orbx_keypoint* __restrict__ kps,
-                                                       const uint8_t* __restrict__ desc,
-                                                       const int* __restrict__ counts, int cap,
-                                                       const int* __restrict__ pa, const int* __restrict__ pb,
-                                                       int rows, int cols, int window, float nnratio, int check_ori,
-                                                       uint32_t* __restrict__ cand_g, int cand_per_pair, int cand_lds,
-                                                       int* __restrict__ m12_out, int* __restrict__ nm_out)
+__global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restrict__ kps, const int* __restrict__ counts,
+                                                   int cap, const int* __restrict__ pa, const int* __restrict__ pb,
+                                                   float nnratio, int check_ori, const int* __restrict__ gn,
+                                                   const uint32_t* __restrict__ cand, int cand_per_pair, int cand_lds,
+                                                   const int* __restrict__ qoff, const int* __restrict__ qcnt,
+                                                   const int* __restrict__ ptotal, int* __restrict__ m12_out,
+                                                   int* __restrict__ nm_out)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const SiLayout Ly = si_layout(cap, cand_lds);
-    uint32_t* keys = (uint32_t*)(smem + Ly.keys);
-    float2* gxy = (float2*)(smem + Ly.gxy);
-    uint32_t* off = (uint32_t*)(smem + Ly.off);
+    const SgLayout Ly = sg_layout(cap, cand_lds);
+    int* off = (int*)(smem + Ly.off);
+    int* cnt = (int*)(smem + Ly.cnt);
+    float* ang1 = (float*)(smem + Ly.ang1);
+    float* ang2 = (float*)(smem + Ly.ang2);
     uint16_t* mdist = (uint16_t*)(smem + Ly.mdist);
     int16_t* m21 = (int16_t*)(smem + Ly.m21);
     int16_t* m12 = (int16_t*)(smem + Ly.m12);
     int8_t* bin = (int8_t*)(smem + Ly.bin);
-    uint32_t* cand_l = (uint32_t*)(smem + Ly.cand);
-    __shared__ int s_n[4];
+    uint32_t* cl = (uint32_t*)(smem + Ly.cand);
     __shared__ int s_hist[32];
-
-    const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int fa = pa[pair], fb = pb[pair];
+    const int n1 = min(counts[fa], cap), n2 = min(counts[fb], cap);
+    const int n10 = gn[2 * fa];
+    const int total = ptotal[pair];
+    int* out = m12_out + (size_t)pair * cap;
+    if (total > cand_per_pair) {   // scratch too small for this pair: report, leave no matches
+        for (int i = tid; i < cap; i += 256) out[i] = -1;
+        if (tid == 0) nm_out[pair] = -1;
+        return;
+    }
+    const uint32_t* gc = cand + (size_t)pair * cand_per_pair;
+    const bool in_lds = total <= cand_lds;
+    if (in_lds)
+        for (int j = tid; j < total; j += 256) cl[j] = gc[j];
+    const uint32_t* pc = in_lds ? cl : gc;
     const orbx_keypoint* k1 = kps + (size_t)fa * cap;
     const orbx_keypoint* k2 = kps + (size_t)fb * cap;
-    const uint8_t* d1 = desc + (size_t)fa * cap * 32;
-    const uint8_t* d2 = desc + (size_t)fb * cap * 32;
-    const int n1 = min(counts[fa], cap), n2 = min(counts[fb], cap);
-    if (tid < 4) s_n[tid] = 0;
-    __syncthreads();
-    // level-0 keypoints come first (src/ORBextractor.cc:1290-1333)
-    int c1 = 0, c2 = 0;
-    for (int i = tid; i < n1; i += SI_NT) c1 += k1[i].octave == 0;
-    for (int i = tid; i < n2; i += SI_NT) c2 += k2[i].octave == 0;
-    if (c1) atomicAdd(&s_n[0], c1);
-    if (c2) atomicAdd(&s_n[1], c2);
-    __syncthreads();
-    const int n10 = s_n[0], n20 = s_n[1];
-    int p2 = 1;
-    while (p2 < n20) p2 <<= 1;
-
-    const float invW = (float)kGridCols / ((float)cols - 0.0f);
-    const float invH = (float)kGridRows / ((float)rows - 0.0f);
-    for (int i = tid; i < p2; i += SI_NT) {
-        uint32_t key = 0xFFFFFFFFu;
-        if (i < n20) {
-            const int px = (int)roundf((k2[i].x - 0.0f) * invW);
-            const int py = (int)roundf((k2[i].y - 0.0f) * invH);
-            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {
-                key = ((uint32_t)(px * kGridRows + py) << 16) | (uint32_t)i;
-                atomicAdd(&s_n[2], 1);
-            }
-        }
-        keys[i] = key;
+    for (int i = tid; i < n10; i += 256) {
+        off[i] = qoff[(size_t)pair * cap + i];
+        cnt[i] = qcnt[(size_t)pair * cap + i];
+        ang1[i] = k1[i].angle;
     }
-    __syncthreads();
-    bitonic_asc(keys, p2);   // invalid keys (outside the grid, PosInGrid false) sort last
-    const int ng_ = s_n[2];
-    for (int g = tid; g < ng_; g += SI_NT) {
-        const int i2 = (int)(keys[g] & 0xFFFF);
-        gxy[g] = make_float2(k2[i2].x, k2[i2].y);
-    }
-    __syncthreads();
-    const int ng = ng_;
-
-    const float r = (float)window;
-    uint32_t* pc = cand_l;
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int i1 = wave; i1 < n10; i1 += SI_NW) {
-            const float x = k1[i1].x, y = k1[i1].y;
-            // Frame::GetFeaturesInArea(x, y, r, 0, 0) cell range, src/Frame.cc:421-440
-            const int cx0 = max(0, (int)floorf((x - 0.0f - r) * invW));
-            const int cx1 = min(kGridCols - 1, (int)ceilf((x - 0.0f + r) * invW));
-            const int cy0 = max(0, (int)floorf((y - 0.0f - r) * invH));
-            const int cy1 = min(kGridRows - 1, (int)ceilf((y - 0.0f + r) * invH));
-            int base = pass ? (int)off[i1] : 0;
-            if (cx0 < kGridCols && cx1 >= 0 && cy0 < kGridRows && cy1 >= 0) {
-                const int lo = lower_bound_u32(keys, ng, (uint32_t)(cx0 * kGridRows) << 16);
-                const int hi = lower_bound_u32(keys, ng, (uint32_t)((cx1 + 1) * kGridRows) << 16);
-                ulonglong2 a0 = make_ulonglong2(0, 0), a1 = a0;
-                if (pass) {
-                    const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
-                    a0 = a[0];
-                    a1 = a[1];
-                }
-                for (int g0 = lo; g0 < hi; g0 += 64) {
-                    const int g = g0 + lane;
-                    bool in = false;
-                    int i2 = 0;
-                    if (g < hi) {
-                        const uint32_t key = keys[g];
-                        const int iy = (int)(key >> 16) % kGridRows;
-                        if (iy >= cy0 && iy <= cy1) {
-                            const float2 p = gxy[g];
-                            in = fabsf(p.x - x) < r && fabsf(p.y - y) < r;
-                            i2 = (int)(key & 0xFFFF);
-                        }
-                    }
-                    const unsigned long long m = __ballot(in);
-                    if (pass && in) {
-                        const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)i2 * 32);
-                        const int d = ham256(a0, a1, b[0], b[1]);
-                        const int idx = base + (int)__builtin_amdgcn_mbcnt_hi(
-                                                   (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        pc[idx] = (uint32_t)i2 | ((uint32_t)d << 16);
-                    }
-                    base += __popcll(m);
-                }
-            }
-            if (!pass && lane == 0) off[i1] = (uint32_t)base;
-        }
-        __syncthreads();
-        if (!pass) {
-            // exclusive scan of off[0..n10) (one wave; n10 is a few hundred)
-            if (wave == 0) {
-                uint32_t run = 0;
-                for (int b0 = 0; b0 < n10; b0 += 64) {
-                    const int i = b0 + lane;
-                    const uint32_t v = i < n10 ? off[i] : 0u;
-                    uint32_t inc = v;
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const uint32_t y = __shfl_up(inc, o);
-                        if (lane >= o) inc += y;
-                    }
-                    if (i < n10) off[i] = run + inc - v;
-                    run += __shfl(inc, 63);
-                }
-                if (lane == 0) {
-                    off[n10] = run;
-                    s_n[3] = (int)run;
-                }
-            }
-            __syncthreads();
-            const int total = s_n[3];
-            if (total > cand_lds) {
-                if (total > cand_per_pair) {   // cannot hold the lists: report, do nothing
-                    for (int i = tid; i < cap; i += SI_NT) m12_out[(size_t)pair * cap + i] = -1;
-                    if (tid == 0) nm_out[pair] = -1;
-                    return;
-                }
-                pc = cand_g + (size_t)pair * cand_per_pair;
-            }
-        }
-    }
-
-    if (wave != 0) return;
-    // pass B: the reference's sequential greedy loop
-    for (int i = lane; i < n2; i += 64) {
+    for (int i = tid; i < n2; i += 256) {
         mdist[i] = 0xFFFF;   // INT_MAX: larger than any distance
         m21[i] = -1;
+        ang2[i] = k2[i].angle;
     }
-    for (int i = lane; i < n1; i += 64) {
+    for (int i = tid; i < n1; i += 256) {
         m12[i] = -1;
         bin[i] = -1;
     }
-    if (lane < 32) s_hist[lane] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (tid < 32) s_hist[tid] = 0;
+    __syncthreads();
+    if (tid >= 64) return;
+
     int nmatches = 0;
     const float factor = 1.0f / 30;
     for (int i1 = 0; i1 < n10; ++i1) {
-        const int o0 = (int)off[i1], o1 = (int)off[i1 + 1];
-        if (o1 == o0) continue;   // vIndices2.empty()
-        int b1 = INT_MAX, b2 = INT_MAX, bp = INT_MAX;
-        for (int j = o0 + lane; j < o1; j += 64) {
-            const uint32_t e = pc[j];
-            const int i2 = (int)(e & 0xFFFF), d = (int)(e >> 16);
-            if ((int)mdist[i2] <= d) continue;
+        const int c = cnt[i1];
+        if (c == 0) continue;   // vIndices2.empty()
+        const int o0 = off[i1];
+        // lane-local best (first min) and second (2nd order statistic) over this lane's candidates
+        uint32_t b1 = 0x1FF, b2 = 0x1FF, bp = 0xFFFF;
+        for (int j = lane; j < c; j += 64) {
+            const uint32_t e = pc[o0 + j];
+            const uint32_t i2 = e & 0xFFFF, d = e >> 16;
+            if ((uint32_t)mdist[i2] <= d) continue;
             if (d < b1) {
                 b2 = b1;
                 b1 = d;
-                bp = j;
+                bp = (uint32_t)j;
             } else if (d < b2) {
                 b2 = d;
             }
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const int y1 = __shfl_xor(b1, o), yp = __shfl_xor(bp, o), y2 = __shfl_xor(b2, o);
-            if (y1 < b1 || (y1 == b1 && yp < bp)) {
-                b2 = min(b1, y2);
-                b1 = y1;
-                bp = yp;
-            } else {
-                b2 = min(b2, y1);
-            }
-        }
-        if (b1 <= 50 && (float)b1 < (float)b2 * nnratio) {
-            const int bi = (int)(pc[bp] & 0xFFFF);
+        // wave: best = min (dist, position); second = min over lanes of (winner ? its b2 : b1)
+        const uint32_t key = (b1 << 16) | bp;
+        const uint32_t kmin = wave_min_u32(key);
+        const uint32_t sec = wave_min_u32(key == kmin ? b2 : b1);
+        const int bd = (int)(kmin >> 16);
+        const int bd2 = sec >= 0x1FF ? INT_MAX : (int)sec;
+        const int bpos = (int)(kmin & 0xFFFF);
+        if (bd <= 50 && (float)bd < (float)bd2 * nnratio) {
+            const int bi = (int)(pc[o0 + bpos] & 0xFFFF);
             if (lane == 0) {
                 if (m21[bi] >= 0) {
                     m12[m21[bi]] = -1;
@@ -423,10 +463,10 @@ __global__ __launch_bounds__(SI_NT) void k_search_init(const orbx_keypoint* __re
                 }
                 m12[i1] = (int16_t)bi;
                 m21[bi] = (int16_t)i1;
-                mdist[bi] = (uint16_t)b1;
+                mdist[bi] = (uint16_t)bd;
                 ++nmatches;
                 if (check_ori) {
-                    float rot = k1[i1].angle - k2[bi].angle;
+                    float rot = ang1[i1] - ang2[bi];
                     if (rot < 0.0f) rot += 360.0f;
                     int bb = (int)roundf(rot * factor);
                     if (bb == 30) bb = 0;
@@ -465,28 +505,48 @@ __global__ __launch_bounds__(SI_NT) void k_search_init(const orbx_keypoint* __re
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    int* out = m12_out + (size_t)pair * cap;
     for (int i = lane; i < cap; i += 64) out[i] = i < n1 ? (int)m12[i] : -1;
     if (lane == 0) nm_out[pair] = nmatches;
 }
 
-int search_init_cand_lds(int cap)
+size_t search_init_scratch_bytes(int nframes, int npairs, int cap, int cand_per_pair)
 {
-    // LDS left for candidate lists after the per-pair arrays (160 KiB per CU, one pair per workgroup)
-    const size_t fixed = si_layout(cap, 0).total + 256;
-    const long left = (long)(160 * 1024) - (long)fixed;
-    return left > 0 ? (int)(left / 4) : 0;
+    return (size_t)nframes * cap * (4 + 8) + (size_t)nframes * 2 * 4 + (size_t)npairs * cap * 8 + (size_t)npairs * 4 +
+           (size_t)npairs * cand_per_pair * 4 + 64 * 5;
 }
 
-void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int cap, const int* pa,
-                        const int* pb, int npairs, int rows, int cols, int window, float nnratio, int check_ori,
-                        uint32_t* cand, int cand_per_pair, int* m12, int* nm, hipStream_t s)
+void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int nframes, int cap,
+                        const int* pa, const int* pb, int npairs, int rows, int cols, int window, float nnratio,
+                        int check_ori, void* scratch, int cand_per_pair, int* m12, int* nm, hipStream_t s)
 {
-    const int cand_lds = search_init_cand_lds(cap);
-    const size_t smem = si_layout(cap, cand_lds).total;
-    hipFuncSetAttribute((const void*)k_search_init, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(k_search_init, dim3(npairs), dim3(SI_NT), smem, s, kps, desc, counts, cap, pa, pb, rows, cols,
-                       window, nnratio, check_ori, cand, cand_per_pair, cand_lds, m12, nm);
+    uint8_t* p = (uint8_t*)scratch;
+    auto carve = [&](size_t bytes) {
+        uint8_t* r = p;
+        p += (bytes + 63) & ~(size_t)63;
+        return r;
+    };
+    uint32_t* gkeys = (uint32_t*)carve((size_t)nframes * cap * 4);
+    float2* gxy = (float2*)carve((size_t)nframes * cap * 8);
+    int* gn = (int*)carve((size_t)nframes * 2 * 4);
+    int* qoff = (int*)carve((size_t)npairs * cap * 4);
+    int* qcnt = (int*)carve((size_t)npairs * cap * 4);
+    int* ptotal = (int*)carve((size_t)npairs * 4);
+    uint32_t* cand = (uint32_t*)carve((size_t)npairs * cand_per_pair * 4);
+    int p2 = 1;
+    while (p2 < cap) p2 <<= 1;
+    hipMemsetAsync(ptotal, 0, (size_t)npairs * 4, s);
+    hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)p2 * 4, s, kps, counts, cap, rows, cols, gkeys,
+                       gxy, gn);
+    const size_t bsmem = (((size_t)cap * 4 + 15) & ~(size_t)15) + (size_t)cap * 8;
+    hipLaunchKernelGGL(k_si_build, dim3(npairs, SI_QSPLIT), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, rows,
+                       cols, window, gkeys, gxy, gn, cand, cand_per_pair, qoff, qcnt, ptotal);
+    const size_t fixed = sg_layout(cap, 0).total + 512;
+    const long left = (long)(160 * 1024) - (long)fixed;
+    const int cand_lds = left > 0 ? (int)(left / 4) : 0;
+    const size_t gsmem = sg_layout(cap, cand_lds).total;
+    hipFuncSetAttribute((const void*)k_si_greedy, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gsmem);
+    hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), gsmem, s, kps, counts, cap, pa, pb, nnratio, check_ori, gn,
+                       cand, cand_per_pair, cand_lds, qoff, qcnt, ptotal, m12, nm);
 }
 
 }  // namespace orbx

@@ -71,8 +71,8 @@ def _load():
     L.orbx_debug_candidates.argtypes = [vp, C.c_int, C.c_int, i32p, C.c_int, i32p]
     L.orbm_descriptor_distance.argtypes = [u8p, u8p]
     L.orbm_allpairs_device.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]
-    L.orbm_search_init_batch_device.argtypes = [vp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int,
-                                                C.c_float, C.c_int, vp, vp, vp]
+    L.orbm_search_init_batch_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int,
+                                                C.c_int, C.c_float, C.c_int, vp, vp, vp]
     return L
 
 
@@ -257,7 +257,8 @@ class ORBmatcher:
             matches12 = torch.empty((npairs, cap), dtype=torch.int32, device=kps.device)
         if nmatches is None:
             nmatches = torch.empty((npairs,), dtype=torch.int32, device=kps.device)
-        rc = lib.orbm_search_init_batch_device(_ptr(kps), _ptr(desc), _ptr(counts), cap, _ptr(pair_a), _ptr(pair_b),
+        rc = lib.orbm_search_init_batch_device(_ptr(kps), _ptr(desc), _ptr(counts), kps.shape[0], cap, _ptr(pair_a),
+                                               _ptr(pair_b),
                                                npairs, rows, cols, window, self.mfNNratio,
                                                1 if self.mbCheckOrientation else 0, _ptr(matches12), _ptr(nmatches),
                                                _stream(stream))
