@@ -221,6 +221,8 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
                 c.roi_w = (int16_t)((int)maxX - (int)iniX);
                 c.roi_h = (int16_t)((int)maxY - (int)iniY);
                 if (c.roi_w > 66 || c.roi_h > 66) return ORBX_EINVAL;
+                g.max_roi_w = std::max(g.max_roi_w, (int)c.roi_w);
+                g.max_roi_h = std::max(g.max_roi_h, (int)c.roi_h);
                 const int dw = c.roi_w - 6, dh = c.roi_h - 6;
                 c.slot_base = slot;
                 c.slot_cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;

@@ -46,45 +46,77 @@ __device__ __forceinline__ const uint8_t* level_base(const FramePtrs& P, const G
 // (11-bit coefficients, 22-bit vertical rounding) — SURVEY.md A.2.
 // Coefficient tables are built on the host exactly like OpenCV builds them.
 // ---------------------------------------------------------------------------
+constexpr int kPyrRows = 4;
+
 __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
                                                        const int2* __restrict__ xtab,
                                                        const int2* __restrict__ ytab)
 {
-    // 4 output pixels per thread, one dword store (level pitch is a multiple of 64)
-    const int f = blockIdx.z, dy = blockIdx.y;
+    // A block makes kPyrRows output rows of one frame: the source rows they need are
+    // staged in LDS with coalesced dword loads (realigned with v_alignbyte, so any
+    // source pitch works), then each thread makes 4 output pixels per dword store.
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
+    const int f = blockIdx.z, dy0 = blockIdx.y * kPyrRows;
     const LevelGeom& D = G->lv[l];
-    const int dx0 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    if (dx0 >= D.w) return;
+    const int sw = G->lv[l - 1].w;
+    const int dyn = min(kPyrRows, D.h - dy0);
     int spitch;
     const uint8_t* src = level_base(P, G, f, l - 1, spitch);
-    uint8_t* dst = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy * D.pitch;
-    const int2 yt = ytab[D.ytab_off + dy];
-    const uint8_t* r0 = src + (size_t)(yt.x & 0xFFFF) * spitch;
-    const uint8_t* r1 = src + (size_t)((uint32_t)yt.x >> 16) * spitch;
-    const int b0 = yt.y & 0xFFFF, b1 = (int)((uint32_t)yt.y >> 16);
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int dx = dx0 + k;
-        if (dx < D.w) {
-            const int2 xt = xtab[D.xtab_off + dx];
-            const int x0 = xt.x & 0xFFFF, x1 = (int)((uint32_t)xt.x >> 16);
-            const int a0 = xt.y & 0xFFFF, a1 = (int)((uint32_t)xt.y >> 16);
-            const int h0 = r0[x0] * a0 + r0[x1] * a1;
-            const int h1 = r1[x0] * a0 + r1[x1] * a1;
-            const int v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-            packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
-        }
+    const int sy0 = ytab[D.ytab_off + dy0].x & 0xFFFF;
+    const int sy1 = (int)((uint32_t)ytab[D.ytab_off + dy0 + dyn - 1].x >> 16);
+    const int nrows = sy1 - sy0 + 1;
+    const int nd = (sw + 3) >> 2;                 // dwords per staged row
+    for (int i = threadIdx.x; i < nrows * nd; i += 256) {
+        const int r = i / nd, k = i - r * nd;
+        const uint8_t* p = src + (size_t)(sy0 + r) * spitch + 4 * k;
+        const uintptr_t a = (uintptr_t)p;
+        const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
+        // the second dword is needed only if some of its bytes belong to the row; an aligned
+        // dword that starts inside the row cannot run past the (4-byte aligned) buffer end
+        const int sh = (int)(a & 3);
+        const bool tail = sh == 0 || 4 * k + 4 - sh >= sw;
+        const uint32_t lo = ap[0], hi = tail ? 0u : ap[1];
+        s_src[r * nd + k] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3));
     }
-    *reinterpret_cast<uint32_t*>(dst + dx0) = packed;
+    __syncthreads();
+    const uint8_t* S = (const uint8_t*)s_src;
+    const int srow = nd * 4;
+    for (int j = threadIdx.x; j < dyn * ((D.w + 3) >> 2); j += 256) {
+        const int q = (D.w + 3) >> 2;
+        const int rr = j / q, dx0 = (j - rr * q) * 4;
+        const int dy = dy0 + rr;
+        const int2 yt = ytab[D.ytab_off + dy];
+        const uint8_t* r0 = S + ((yt.x & 0xFFFF) - sy0) * srow;
+        const uint8_t* r1 = S + ((int)((uint32_t)yt.x >> 16) - sy0) * srow;
+        const int b0 = yt.y & 0xFFFF, b1 = (int)((uint32_t)yt.y >> 16);
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int dx = dx0 + k;
+            if (dx < D.w) {
+                const int2 xt = xtab[D.xtab_off + dx];
+                const int x0 = xt.x & 0xFFFF, x1 = (int)((uint32_t)xt.x >> 16);
+                const int a0 = xt.y & 0xFFFF, a1 = (int)((uint32_t)xt.y >> 16);
+                const int h0 = r0[x0] * a0 + r0[x1] * a1;
+                const int h1 = r1[x0] * a0 + r1[x1] * a1;
+                const int v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+                packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
+            }
+        }
+        *reinterpret_cast<uint32_t*>(P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy * D.pitch + dx0) =
+            packed;
+    }
 }
 
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
     for (int l = 1; l < g.nlevels; ++l) {
-        const int w = g.lv[l].w, h = g.lv[l].h;
-        dim3 grid((w + 1023) / 1024, h, batch);
-        hipLaunchKernelGGL(k_pyramid_level, grid, dim3(256), 0, s, b.geom, p, l, b.xtab, b.ytab);
+        const int h = g.lv[l].h;
+        // source rows per block: kPyrRows * (src/dst scale) + 2, bounded by the level ratio
+        const int srows = (kPyrRows * g.lv[l - 1].h + g.lv[l].h - 1) / g.lv[l].h + 2;
+        const size_t smem = (size_t)srows * (((g.lv[l - 1].w + 3) >> 2) * 4);
+        dim3 grid(1, (h + kPyrRows - 1) / kPyrRows, batch);
+        hipLaunchKernelGGL(k_pyramid_level, grid, dim3(256), smem, s, b.geom, p, l, b.xtab, b.ytab);
     }
 }
 
@@ -97,9 +129,15 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
 // (src/ORBextractor.cc:982-987).  Survivors are emitted row-major, i.e. in
 // OpenCV's emission order.
 // ---------------------------------------------------------------------------
-constexpr int kRoiMax = 66;
-constexpr int kTileP = 68;
-constexpr int kMapMax = (kRoiMax - 4) * (kRoiMax - 4);
+// ROI tile row pitch (dword aligned, +1 dword of slack for the 8-byte realigning read)
+__host__ __device__ inline int fast_tile_pitch(int max_roi_w) { return ((max_roi_w + 3) & ~3) + 4; }
+// per-wave LDS: ROI tile + zero-bordered strength map of the detection window
+__host__ __device__ inline size_t fast_wave_bytes(int max_roi_w, int max_roi_h)
+{
+    const size_t tile = (size_t)max_roi_h * fast_tile_pitch(max_roi_w);
+    const size_t map = (size_t)(max_roi_h - 4) * (max_roi_w - 4);
+    return (tile + map + 15) & ~(size_t)15;
+}
 
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 __device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
@@ -161,8 +199,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
                                                     uint32_t* __restrict__ slots,
                                                     int* __restrict__ cell_counts)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_tile[4][kRoiMax * kTileP];
-    __shared__ uint8_t s_map[4][kMapMax];
+    // per-wave LDS sized from the geometry's largest cell ROI (more resident waves per CU)
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
+    const int kTileP = fast_tile_pitch(G->max_roi_w);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
     const int c = blockIdx.x * 4 + wave;
@@ -170,8 +209,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     const Cell C = cells[c];
     int pitch;
     const uint8_t* img = level_base(P, G, f, C.level, pitch);
-    uint8_t* tile = s_tile[wave];
-    uint8_t* map = s_map[wave];
+    uint8_t* tile = s_fast + (size_t)wave * fast_wave_bytes(G->max_roi_w, G->max_roi_h);
+    uint8_t* map = tile + (size_t)G->max_roi_h * kTileP;
     const int rw = C.roi_w, rh = C.roi_h;
     const int dw = rw - 6, dh = rh - 6;
     int* out_count = cell_counts + (size_t)f * G->ncells + c;
@@ -196,6 +235,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
 
     const int npx = dw * dh;
     const float inv_dw = 1.0f / (float)dw;   // exact row/col split for npx < 4096
+#pragma unroll 2
     for (int k = lane; k < npx; k += 64) {
         const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
         const int s = fast_strength(tile + (ii + 3) * kTileP + (jj + 3), kTileP);
@@ -253,7 +293,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
     dim3 grid((g.ncells + 3) / 4, batch);
-    hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), 0, s, b.geom, p, b.cells, b.slots, b.cell_counts);
+    const size_t smem = 4 * fast_wave_bytes(g.max_roi_w, g.max_roi_h);
+    hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts);
 }
 
 // ---------------------------------------------------------------------------
@@ -719,11 +760,16 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 }
 
 // ---------------------------------------------------------------------------
-// K4: one wave per retained keypoint.
-//   raw   43x43 neighbourhood (reflect-101 at level borders) in LDS; interior
-//         keypoints load it as aligned dwords realigned with v_alignbyte.
-//   angle IC_Angle: u*I and v*I over the 749-pixel disc, wave reduction, then
-//         cv::fastAtan2 (src/ORBextractor.cc:84-128).
+// K4: a wave describes kDescPerWave consecutive retained keypoints.
+//   raw   the 43-row neighbourhood of the keypoint in LDS, 64 B per row.
+//         Interior keypoints arrive by LDS-DMA (global_load_lds_dword of 13
+//         aligned dwords per row, so row r starts at byte sh_r = (src +
+//         r*pitch) & 3 of its LDS row); border keypoints are filled with reflect-101 bytes
+//         at shift 0.  The next keypoint's DMA is issued as soon as the
+//         current one's raw reads are done, so it lands under the BRIEF work.
+//   angle IC_Angle: u*I and v*I over the 749-pixel disc as per-lane column
+//         sums (lane = disc column, half-wave = upper/lower rows), wave
+//         reduction, then cv::fastAtan2 (src/ORBextractor.cc:84-128).
 //   blur  GaussianBlur 7x7 integer kernel [18 34 49 55 49 34 18], >>16
 //         (SURVEY.md A.3): the horizontal pass is v_dot4_u32_u8 on 4 output
 //         columns x 2 rows per lane, stored transposed as u16 row pairs; the
@@ -732,8 +778,12 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 //   BRIEF fmaf sample coordinates, 256 tests -> four __ballot
 //         words = the descriptor's little-endian u64 words (:141-192).
 // ---------------------------------------------------------------------------
-constexpr int kRawRows = 44, kRawP = 48;      // 43 rows used, byte pitch 48 (12 dwords)
-constexpr int kTCols = 40, kTP = 22;           // row-blurred, transposed: [col][row pairs], 22 dwords/col
+constexpr int kRawD = 13;                             // dwords loaded per raw row: 48 B + shift slack
+constexpr int kRawP = 64;                             // LDS row pitch (bytes): 4 rows per 64-lane DMA
+constexpr int kRawRows = 44;                          // 43 rows used
+constexpr int kRawSlots = kRawRows * kRawP / 4;
+constexpr int kTCols = 40, kTP = 22;                  // row-blurred, transposed: [col][row pairs], 22 dwords/col
+constexpr int kDescPerWave = 4;                       // keypoints per wave (lane state set up once per wave)
 
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
@@ -782,135 +832,198 @@ __device__ __forceinline__ int blur_at(const uint32_t* rowT, int y, int x)
 }
 
 __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
-                                                  const uint32_t* __restrict__ qt_out,
-                                                  const int* __restrict__ qt_cnt,
-                                                  orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                  int cap, int* __restrict__ status)
+                                               const uint32_t* __restrict__ qt_out,
+                                               const int* __restrict__ qt_cnt,
+                                               orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                               int cap, int* __restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][kRawRows * kRawP / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][kRawSlots];
     __shared__ __attribute__((aligned(16))) uint32_t s_rowT[4][kTCols * kTP];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int f = blockIdx.y;
-    const int g = blockIdx.x * 4 + wave;
-    if (g >= G->out_per_frame) return;
     const int L = G->nlevels;
-    int l = 0;
-    while (l + 1 < L && g >= G->lv[l + 1].out_off) ++l;
-    const LevelGeom& LG = G->lv[l];
-    const int pos = g - LG.out_off;
     const int* cnts = qt_cnt + (size_t)f * L;
-    if (pos >= cnts[l]) return;
-    int oidx = pos;
-    for (int q = 0; q < l; ++q) oidx += cnts[q];
-    if (oidx >= cap) {
-        if (lane == 0) atomicOr(status, (int)kStatusCapOverflow);
-        return;
-    }
-    const uint32_t pk = qt_out[(size_t)f * G->out_per_frame + g];
-    const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF), score = (int)(pk >> 24);
-    int pitch;
-    const uint8_t* img = level_base(P, G, f, l, pitch);
-    const int w = LG.w, h = LG.h;
     uint32_t* raw32 = s_raw[wave];
     uint8_t* raw = (uint8_t*)raw32;
     uint32_t* rowT = s_rowT[wave];
+    const int g0 = (blockIdx.x * 4 + wave) * kDescPerWave;
 
-    // raw patch rows cy-21..cy+21, columns cx-21..cx+26 (the last 5 only feed unused outputs)
-    if (cx >= 21 && cy >= 21 && cy + 21 < h && cx + 31 <= w) {
-        const uint8_t* src = img + (size_t)(cy - 21) * pitch + (cx - 21);
-        for (int i = lane; i < 43 * 12; i += 64) {
-            const int r = i / 12, k = i - r * 12;
-            const uintptr_t a = (uintptr_t)(src + (size_t)r * pitch + 4 * k);
-            const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
-            raw32[r * 12 + k] = __builtin_amdgcn_alignbyte(ap[1], ap[0], (uint32_t)(a & 3));
-        }
-    } else {
-        for (int i = lane; i < 43 * kRawP; i += 64) {
-            const int r = i / kRawP, c = i - r * kRawP;
-            const int X = reflect101(cx - 21 + c, w), Y = reflect101(cy - 21 + r, h);
-            raw[r * kRawP + c] = img[(size_t)Y * pitch + X];
-        }
-    }
-    wave_lds_sync();
-
-    // IC_Angle: m10 = sum u*I, m01 = sum v*I over the disc |u| <= umax[|v|]
-    int m10 = 0, m01 = 0;
-    for (int i = lane; i < 31 * 31; i += 64) {
-        const int v = i / 31 - 15, u = i % 31 - 15;
-        const int av = v < 0 ? -v : v, au = u < 0 ? -u : u;
-        if (au <= c_umax[av]) {
-            const int val = raw[(21 + v) * kRawP + 21 + u];
-            m10 += u * val;
-            m01 += v * val;
-        }
-    }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
-    const float angle = fast_atan2_deg((float)m01, (float)m10);
-
-    // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns
-    const uint32_t K0 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
-    const uint32_t K1 = 49u | (34u << 8) | (18u << 16);
-    for (int i = lane; i < 22 * 10; i += 64) {
-        const int rp = i / 10, cg = i - rp * 10;
-        uint32_t o[2][4];
+    // ---- keypoint-independent lane state, set up once for the wave's keypoints ----
+    // IC_Angle: the lane owns disc column u = (lane & 31) - 15 (lanes 31, 63 idle) and the
+    // rows v = -15..0 (lanes 0..31) or v = 1..15 (lanes 32..63), 16 row steps k.  The
+    // disc |u| <= umax[|v|] is |v| <= vmax(|u|) (umax is non-increasing), i.e. a k range.
+    const int hu = lane & 31, half = lane >> 5;
+    const int u = hu - 15, au = u < 0 ? -u : u;
+    int vmax = -1;
+    if (hu < 31)
+        for (int v = 0; v < 16; ++v)
+            if (au <= c_umax[v]) vmax = v;
+    const int klo = half ? 0 : 15 - vmax, khi = half ? vmax - 1 : 15;   // empty when vmax < 0
+    const uint32_t kmask = klo > khi ? 0u : ((2u << khi) - 1u) & ~((1u << klo) - 1u);
+    const int voff = half ? 1 : -15;   // v = k + voff; raw row = 21 + v
+    const uint8_t* icb = raw + (half ? 22 : 6) * kRawP + 21 + u;
+    // rBRIEF: this lane's 8 tests (word wd = lane + 64 wd), pattern points as floats
+    float ppx[8], ppy[8];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const uint32_t* rr = raw32 + (2 * rp + e) * 12 + cg;
-            const uint32_t W0 = rr[0], W1 = rr[1], W2 = rr[2];
+    for (int q = 0; q < 8; ++q) {
+        const int m = (q >> 1) * 64 + lane, e = q & 1;
+        ppx[q] = (float)c_pattern[4 * m + 2 * e];
+        ppy[q] = (float)c_pattern[4 * m + 2 * e + 1];
+    }
+
+    // output index g (level-major, as the reference concatenates levels) -> level, keypoint.
+    // The wave's indices are consecutive, so past the frame's total the rest are too.
+    auto lookup = [&](int g, int& l, uint32_t& pk) -> bool {
+        int base = 0;
+        for (l = 0; l < L; ++l) {
+            if (g < base + cnts[l]) break;
+            base += cnts[l];
+        }
+        if (l == L) return false;
+        if (g >= cap) {
+            if (lane == 0) atomicOr(status, (int)kStatusCapOverflow);
+            return false;
+        }
+        pk = qt_out[(size_t)f * G->out_per_frame + G->lv[l].out_off + (g - base)];
+        return true;
+    };
+    // raw patch rows cy-21..cy+21 from column cx-21 (48 bytes used per row); sets the
+    // wave-uniform row-shift state: row r starts at byte (sb + r*sp) & 3 of its LDS row
+    auto fill = [&](int l, uint32_t pk, int& sb, int& sp) {
+        const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF);
+        const int w = G->lv[l].w, h = G->lv[l].h;
+        int pitch;
+        const uint8_t* img = level_base(P, G, f, l, pitch);
+        if (cx >= 21 && cy >= 21 && cy + 21 < h && cx + 31 <= w) {
+            // DMA instruction t moves rows 4t..4t+3 (lane = 16 * row + dword; dwords 13..15
+            // repeat dword 12, row 43 repeats row 42).  Each row's aligned dwords end at or
+            // before column cx+30 < w and start at or after the 4-byte aligned allocation.
+            const uintptr_t s0 = (uintptr_t)(img + (size_t)(cy - 21) * pitch + (cx - 21));
+            const uint8_t* ub = (const uint8_t*)(s0 & ~(uintptr_t)3);   // wave-uniform, aligned
+            sb = (int)(s0 & 3);
+            sp = pitch & 3;
+            const int rr = lane >> 4, kk = min(lane & 15, kRawD - 1);
+            const uint32_t off = (uint32_t)((sb + rr * pitch) & ~3) + 4u * kk;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t A = __builtin_amdgcn_alignbyte(W1, W0, (uint32_t)j);
-                const uint32_t B = __builtin_amdgcn_alignbyte(W2, W1, (uint32_t)j);
-                o[e][j] = __builtin_amdgcn_udot4(A, K0, __builtin_amdgcn_udot4(B, K1, 0u, false), false);
+            for (int t = 0; t < kRawRows / 4; ++t) {
+                const uint32_t o = (t == kRawRows / 4 - 1 && rr == 3) ? off - (uint32_t)pitch : off;
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(ub + (size_t)(4 * t) * pitch + o),
+                    (__attribute__((address_space(3))) void*)(raw32 + 64 * t), 4, 0, 0);
+            }
+        } else {
+            sb = 0;
+            sp = 0;
+            for (int i = lane; i < 43 * kRawP; i += 64) {
+                const int r = i / kRawP, c = i - r * kRawP;
+                const int X = reflect101(cx - 21 + c, w), Y = reflect101(cy - 21 + r, h);
+                raw[i] = img[(size_t)Y * pitch + X];
             }
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
-    }
-    wave_lds_sync();
+    };
 
-    // rBRIEF with the reference's contracted FMAs; blur evaluated at each sample point
-    const float ang = angle * kFactorPI;
-    const float a = glibc_sincosf(ang, 1), b = glibc_sincosf(ang, 0);
-    unsigned long long words[4];
+    int nl = 0, sb = 0, sp = 0;
+    uint32_t npk = 0;
+    bool nvalid = lookup(g0, nl, npk);
+    if (nvalid) fill(nl, npk, sb, sp);
+#pragma unroll 1
+    for (int jj = 0; jj < kDescPerWave && nvalid; ++jj) {
+        const int oidx = g0 + jj, l = nl;
+        const uint32_t pk = npk;
+        const int csb = sb, csp = sp;
+        const LevelGeom& LG = G->lv[l];
+        const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF), score = (int)(pk >> 24);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this keypoint's DMA has landed
+        wave_lds_sync();
+
+        // IC_Angle: m10 = sum u*I = u * (column sum), m01 = sum v*I = t + voff * (column sum).
+        // Rows 6+k and 22+k have the same shift (16*pitch = 0 mod 4), period 4 in k.
+        const uint8_t* icr[4];
 #pragma unroll
-    for (int wd = 0; wd < 4; ++wd) {
-        const int m = wd * 64 + lane;
-        int t2[2];
+        for (int m = 0; m < 4; ++m) icr[m] = icb + ((csb + (6 + m) * csp) & 3);
+        int csum = 0, t = 0;
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const float px = (float)c_pattern[4 * m + 2 * e], py = (float)c_pattern[4 * m + 2 * e + 1];
-            const int yy = __float2int_rn(__builtin_fmaf(px, b, py * a));
-            const int xx = __float2int_rn(__builtin_fmaf(px, a, -(py * b)));
-            t2[e] = blur_at(rowT, 18 + yy, 18 + xx);
+        for (int k = 0; k < 16; ++k) {
+            const int val = icr[k & 3][k * kRawP] & ((int)(kmask << (31 - k)) >> 31);
+            csum += val;
+            t += k * val;
         }
-        words[wd] = __ballot(t2[0] < t2[1]);
-    }
-    const size_t o = (size_t)f * cap + oidx;
-    if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
-    if (lane == 0) {
-        float x = (float)cx, y = (float)cy;
-        if (l != 0) {
-            x *= LG.scale;
-            y *= LG.scale;
+        const int m10 = wave_sum(u * csum);
+        const int m01 = wave_sum(t + voff * csum);
+
+        // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns
+        const uint32_t K0 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
+        const uint32_t K1 = 49u | (34u << 8) | (18u << 16);
+        for (int i = lane; i < 22 * 10; i += 64) {
+            const int rp = i / 10, cg = i - rp * 10;
+            uint32_t o[2][4];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int r = 2 * rp + e;
+                const uint32_t sh = (uint32_t)((csb + r * csp) & 3);
+                const uint32_t* rr = raw32 + r * (kRawP / 4) + cg;
+                const uint32_t W0 = rr[0], W1 = rr[1], W2 = rr[2], W3 = rr[3];
+                const uint32_t R0 = __builtin_amdgcn_alignbyte(W1, W0, sh);
+                const uint32_t R1 = __builtin_amdgcn_alignbyte(W2, W1, sh);
+                const uint32_t R2 = __builtin_amdgcn_alignbyte(W3, W2, sh);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t A = __builtin_amdgcn_alignbyte(R1, R0, (uint32_t)j);
+                    const uint32_t B = __builtin_amdgcn_alignbyte(R2, R1, (uint32_t)j);
+                    o[e][j] = __builtin_amdgcn_udot4(A, K0, __builtin_amdgcn_udot4(B, K1, 0u, false), false);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
         }
-        orbx_keypoint k;
-        k.x = x;
-        k.y = y;
-        k.size = LG.patch_size;
-        k.angle = angle;
-        k.response = (float)score;
-        k.octave = l;
-        k.class_id = -1;
-        kps[o] = k;
+        wave_lds_sync();   // raw is free: start the next keypoint's patch, it lands under BRIEF
+        nvalid = jj + 1 < kDescPerWave && lookup(oidx + 1, nl, npk);
+        if (nvalid) fill(nl, npk, sb, sp);
+
+        // rBRIEF with the reference's contracted FMAs; blur evaluated at each sample point
+        const float angle = fast_atan2_deg((float)m01, (float)m10);
+        const float ang = angle * kFactorPI;
+        float a, b;
+        glibc_sincosf_pair(ang, &b, &a);   // a = cosf, b = sinf (src/ORBextractor.cc:148)
+        unsigned long long words[4];
+#pragma unroll
+        for (int wd = 0; wd < 4; ++wd) {
+            int t2[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float px = ppx[2 * wd + e], py = ppy[2 * wd + e];
+                const int yy = __float2int_rn(__builtin_fmaf(px, b, py * a));
+                const int xx = __float2int_rn(__builtin_fmaf(px, a, -(py * b)));
+                t2[e] = blur_at(rowT, 18 + yy, 18 + xx);
+            }
+            words[wd] = __ballot(t2[0] < t2[1]);
+        }
+        const size_t o = (size_t)f * cap + oidx;
+        if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
+        if (lane == 0) {
+            float x = (float)cx, y = (float)cy;
+            if (l != 0) {
+                x *= LG.scale;
+                y *= LG.scale;
+            }
+            orbx_keypoint k;
+            k.x = x;
+            k.y = y;
+            k.size = LG.patch_size;
+            k.angle = angle;
+            k.response = (float)score;
+            k.octave = l;
+            k.class_id = -1;
+            kps[o] = k;
+        }
+        wave_lds_sync();   // rowT is rewritten by the next keypoint
     }
 }
 
 void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, orbx_keypoint* kps,
                      uint8_t* desc, int cap, int batch, hipStream_t s)
 {
-    dim3 grid((g.out_per_frame + 3) / 4, batch);
+    dim3 grid((g.out_per_frame + 4 * kDescPerWave - 1) / (4 * kDescPerWave), batch);
     hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, s, b.geom, p, b.qt_out, b.qt_cnt, kps, desc, cap,
                        b.status);
 }

@@ -49,6 +49,7 @@ struct Geometry {
     int out_per_frame;        // sum of level caps
     int spill_per_frame;      // quadtree register-overflow keypoints per frame
     int max_cells_level;      // largest per-level cell count
+    int max_roi_w, max_roi_h; // largest FAST cell ROI (sizes the per-wave LDS tiles)
     int lcap;                 // quadtree list capacity (max level cap + slack)
     long long pyr_bytes;      // bytes per frame for levels 1..L-1
     int umax[16];

@@ -19,59 +19,77 @@
 
 namespace orbx {
 
-struct SinCosTable {
-    double sign[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4;
-};
-
-// __sincosf_table[2] (glibc sincosf_data.c, x86-64 build without TOINT intrinsics)
-#define ORBX_SINCOS_T0 {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, 0x1p0, \
-    -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,        \
-    -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16}
-#define ORBX_SINCOS_T1 {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0, -0x1p0, \
-    0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5, 0x1.1107605230bc4p-7,        \
-    0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16}
+// __sincosf_table[0] (glibc sincosf_data.c, x86-64 build without TOINT intrinsics).
+// __sincosf_table[1] is the same table with the cosine coefficients c0..c4 negated, so a
+// cosine polynomial evaluated through it is exactly the negation of the one below
+// (negating every fma operand negates the correctly rounded result).
+constexpr double kSC_hpi_inv = 0x1.45f306dc9c883p+23, kSC_hpi = 0x1.921fb54442d18p+0;
+constexpr double kSC_c0 = 0x1p0, kSC_c1 = -0x1.ffffffd0c621cp-2, kSC_c2 = 0x1.55553e1068f19p-5,
+                 kSC_c3 = -0x1.6c087e89a359dp-10, kSC_c4 = 0x1.99343027bf8c3p-16;
+constexpr double kSC_s1 = -0x1.555545995a603p-3, kSC_s2 = 0x1.1107605230bc4p-7, kSC_s3 = -0x1.994eb3774cf24p-13;
 
 ORBX_HD uint32_t f32_bits(float f) { union { float f; uint32_t u; } c; c.f = f; return c.u; }
 ORBX_HD uint32_t abstop12(float x) { return (f32_bits(x) >> 20) & 0x7ff; }
 
 ORBX_HD double fma_d(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
-// sinf_poly: n even -> sine polynomial, odd -> cosine polynomial
-ORBX_HD float sincos_poly(double x, double x2, const SinCosTable& p, int n)
+// sinf_poly (table 0): sine polynomial
+ORBX_HD float sin_poly(double x, double x2)
 {
-    if ((n & 1) == 0) {
-        const double x3 = x * x2;
-        const double s1 = fma_d(x2, p.s3, p.s2);
-        const double x7 = x3 * x2;
-        const double s = fma_d(x3, p.s1, x);
-        return (float)fma_d(x7, s1, s);
-    }
+    const double x3 = x * x2;
+    const double s1 = fma_d(x2, kSC_s3, kSC_s2);
+    const double x7 = x3 * x2;
+    const double s = fma_d(x3, kSC_s1, x);
+    return (float)fma_d(x7, s1, s);
+}
+
+// sinf_poly (table 0): cosine polynomial
+ORBX_HD float cos_poly(double x2)
+{
     const double x4 = x2 * x2;
-    const double c2 = fma_d(x2, p.c4, p.c3);
-    const double c1 = fma_d(x2, p.c1, p.c0);
+    const double c2 = fma_d(x2, kSC_c4, kSC_c3);
+    const double c1 = fma_d(x2, kSC_c1, kSC_c0);
     const double x6 = x4 * x2;
-    const double c = fma_d(x4, p.c2, c1);
+    const double c = fma_d(x4, kSC_c2, c1);
     return (float)fma_d(x6, c2, c);
 }
 
-// glibc cosf/sinf for |y| < 120 (every BRIEF angle is in [0, 2*pi)).
-// which = 0 -> sinf(y), 1 -> cosf(y)
-ORBX_HD float glibc_sincosf(float y, int which)
+// glibc sinf and cosf of one argument, |y| < 120 (every BRIEF angle is in [0, 2*pi)).
+// glibc's sinf(y) = sinf_poly(x*s, x*x, p, n) and cosf(y) = sinf_poly(x*s, x*x, p, n^1)
+// with p = table (n & 2); the reduction is shared.
+ORBX_HD void glibc_sincosf_pair(float y, float* sinv, float* cosv)
 {
-    const SinCosTable t0 = ORBX_SINCOS_T0;
-    const SinCosTable t1 = ORBX_SINCOS_T1;
     const float pio4f = 0x1.921FB6p-1f;
     double x = y;
     if (abstop12(y) < abstop12(pio4f)) {
         const double x2 = x * x;
-        if (abstop12(y) < abstop12(0x1p-12f)) return which ? 1.0f : y;
-        return sincos_poly(x, x2, t0, which);
+        if (abstop12(y) < abstop12(0x1p-12f)) {
+            *sinv = y;
+            *cosv = 1.0f;
+            return;
+        }
+        *sinv = sin_poly(x, x2);
+        *cosv = cos_poly(x2);
+        return;
     }
-    const double r = x * t0.hpi_inv;
+    const double r = x * kSC_hpi_inv;
     const int n = ((int32_t)r + 0x800000) >> 24;
-    x = fma_d(-(double)n, t0.hpi, x);
-    const double s = t0.sign[n & 3];
-    return sincos_poly(x * s, x * x, (n & 2) ? t1 : t0, which ? (n ^ 1) : n);
+    x = fma_d(-(double)n, kSC_hpi, x);
+    const double xs = ((n + 1) & 2) ? -x : x;   // sign[n & 3] = {1, -1, -1, 1}
+    const double x2 = x * x;
+    const float sp = sin_poly(xs, x2);
+    const float cp = (n & 2) ? -cos_poly(x2) : cos_poly(x2);
+    // n even: sinf = sine poly, cosf = cosine poly; n odd: swapped
+    *sinv = (n & 1) ? cp : sp;
+    *cosv = (n & 1) ? sp : cp;
+}
+
+// which = 0 -> sinf(y), 1 -> cosf(y)
+ORBX_HD float glibc_sincosf(float y, int which)
+{
+    float s, c;
+    glibc_sincosf_pair(y, &s, &c);
+    return which ? c : s;
 }
 
 // cv::fastAtan2 (OpenCV 3.x), degrees in [0, 360)
