@@ -649,12 +649,11 @@ orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint
         return ORBX_EINVAL;
     if (npairs == 0) return ORBX_OK;
     hipStream_t s = (hipStream_t)stream;
-    const int per = std::max(65536, 48 * cap);
     void* scratch = nullptr;
-    if (hipMallocAsync(&scratch, search_init_scratch_bytes(nframes, npairs, cap, per), s) != hipSuccess)
+    if (hipMallocAsync(&scratch, search_init_scratch_bytes(nframes, npairs, cap), s) != hipSuccess)
         return ORBX_ENOMEM;
     launch_search_init(d_kps, d_desc, d_counts, nframes, cap, d_pair_a, d_pair_b, npairs, rows, cols, window, nnratio,
-                       check_ori, scratch, per, d_matches12, d_nmatches, s);
+                       check_ori, scratch, d_matches12, d_nmatches, s);
     hipFreeAsync(scratch, s);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }

@@ -48,9 +48,9 @@ void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p
 void launch_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt, int* bi, int* b1, int* b2,
                           int* part, int nsplit, hipStream_t s);
 void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, uint16_t* out, hipStream_t s);
-size_t search_init_scratch_bytes(int nframes, int npairs, int cap, int cand_per_pair);
+size_t search_init_scratch_bytes(int nframes, int npairs, int cap);
 void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int nframes, int cap,
                         const int* pa, const int* pb, int npairs, int rows, int cols, int window, float nnratio,
-                        int check_ori, void* scratch, int cand_per_pair, int* m12, int* nm, hipStream_t s);
+                        int check_ori, void* scratch, int* m12, int* nm, hipStream_t s);
 
 }  // namespace orbx

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
+#include <algorithm>
+
 #include "orbx_kernels.hpp"
 
 namespace orbx {
@@ -160,17 +162,23 @@ void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, ui
 //               Frame::GetFeaturesInArea visits them — grid cell (ix outer,
 //               iy inner, Frame::PosInGrid rounding), then index
 //               (AssignFeaturesToGrid insertion order), src/Frame.cc:292-518.
-//   k_si_build  (pair, query-slice) workgroups: a query's window columns are
-//               one contiguous key range (binary search in LDS), filtered by
-//               row and |dx|,|dy| < r; its candidate list (i2, Hamming) is
-//               written in visit order to the pair's CSR scratch.
-//   k_si_greedy one workgroup per pair: the CSR is staged in LDS and one wave
-//               replays the order-dependent greedy pass (vMatchedDistance
-//               skip, best/second, ratio test, eviction) and the rotation-
-//               histogram filter (ComputeThreeMaxima, :1679-1723).
+//   k_si_build  (pair, query-slice) workgroups, one wave per query: the
+//               window's columns are one contiguous key range (binary search
+//               in LDS), filtered by row and |dx|,|dy| < r.  The wave keeps the
+//               4 smallest (Hamming, visit position) candidates and the count.
+//   k_si_greedy one workgroup per pair: one wave replays the order-dependent
+//               greedy pass (vMatchedDistance skip, best/second, ratio test,
+//               eviction) and the rotation-histogram filter
+//               (ComputeThreeMaxima, :1679-1723).  best/second are the first
+//               two candidates in (Hamming, position) order that the skip
+//               does not drop, so a step needs only the query's top-4; a
+//               candidate outside it has Hamming >= the 4th, which settles
+//               the step unless the best is within the ratio of it — then the
+//               wave re-enumerates the window (k_si_build's walk) and scans.
 // ---------------------------------------------------------------------------
 constexpr int kGridCols = 64, kGridRows = 48;
-constexpr int SI_BUILD_NT = 256, SI_QSPLIT = 8;
+constexpr int SI_BUILD_NT = 256;
+constexpr int SI_TOPK = 4;
 
 // min over the 64 lanes with DPP row permutations + 4 readlanes (all lanes active)
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
@@ -184,6 +192,19 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
     const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
     return min(min(a, b), min(c, d));
+}
+
+// orders this wave's LDS accesses (a wave-level barrier for data exchanged through LDS)
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lanes_below_u64(unsigned long long m)
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 __device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_t v)
@@ -264,15 +285,51 @@ __global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict
     }
 }
 
+// query window of GetFeaturesInArea(x, y, r, 0, 0) (src/Frame.cc:410-440) over the sorted
+// grid keys: the cells' columns are one key range [lo, hi), rows are filtered per key
+struct SiWindow {
+    int lo, hi, cy0, cy1;
+    float x, y, r;
+};
+
+__device__ __forceinline__ SiWindow si_window(const uint32_t* keys, int ng, float x, float y, float r, float invW,
+                                              float invH)
+{
+    SiWindow w;
+    w.x = x;
+    w.y = y;
+    w.r = r;
+    const int cx0 = max(0, (int)floorf((x - 0.0f - r) * invW));
+    const int cx1 = min(kGridCols - 1, (int)ceilf((x - 0.0f + r) * invW));
+    w.cy0 = max(0, (int)floorf((y - 0.0f - r) * invH));
+    w.cy1 = min(kGridRows - 1, (int)ceilf((y - 0.0f + r) * invH));
+    w.lo = w.hi = 0;
+    if (cx0 < kGridCols && cx1 >= 0 && w.cy0 < kGridRows && w.cy1 >= 0) {
+        w.lo = lower_bound_u32(keys, ng, (uint32_t)(cx0 * kGridRows) << 16);
+        w.hi = lower_bound_u32(keys, ng, (uint32_t)((cx1 + 1) * kGridRows) << 16);
+    }
+    return w;
+}
+
+__device__ __forceinline__ bool si_in_window(const uint32_t* keys, const float2* xy, const SiWindow& w, int g,
+                                             int& i2)
+{
+    if (g >= w.hi) return false;
+    const uint32_t key = keys[g];
+    const int iy = (int)(key >> 16) % kGridRows;
+    if (iy < w.cy0 || iy > w.cy1) return false;
+    const float2 p = xy[g];
+    i2 = (int)(key & 0xFFFF);
+    return fabsf(p.x - w.x) < w.r && fabsf(p.y - w.y) < w.r;
+}
+
 __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* __restrict__ kps,
                                                           const uint8_t* __restrict__ desc, int cap,
                                                           const int* __restrict__ pa, const int* __restrict__ pb,
                                                           int rows, int cols, int window,
                                                           const uint32_t* __restrict__ gkeys,
                                                           const float2* __restrict__ gxy, const int* __restrict__ gn,
-                                                          uint32_t* __restrict__ cand, int cand_per_pair,
-                                                          int* __restrict__ qoff, int* __restrict__ qcnt,
-                                                          int* __restrict__ ptotal)
+                                                          int* __restrict__ qcnt, uint4* __restrict__ qtop)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -290,66 +347,68 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
     const uint8_t* d2 = desc + (size_t)fb * cap * 32;
     const float invW = (float)kGridCols / ((float)cols - 0.0f);
     const float invH = (float)kGridRows / ((float)rows - 0.0f);
-    const float r = (float)window;
-    uint32_t* pc = cand + (size_t)pair * cand_per_pair;
-    const int nwaves = SI_QSPLIT * (SI_BUILD_NT / 64);
+    const int nwaves = gridDim.y * (SI_BUILD_NT / 64);
     for (int i1 = blockIdx.y * (SI_BUILD_NT / 64) + wave; i1 < n10; i1 += nwaves) {
-        const float x = k1[i1].x, y = k1[i1].y;
-        // Frame::GetFeaturesInArea(x, y, r, 0, 0) cell range, src/Frame.cc:421-440
-        const int cx0 = max(0, (int)floorf((x - 0.0f - r) * invW));
-        const int cx1 = min(kGridCols - 1, (int)ceilf((x - 0.0f + r) * invW));
-        const int cy0 = max(0, (int)floorf((y - 0.0f - r) * invH));
-        const int cy1 = min(kGridRows - 1, (int)ceilf((y - 0.0f + r) * invH));
-        int lo = 0, hi = 0;
-        if (cx0 < kGridCols && cx1 >= 0 && cy0 < kGridRows && cy1 >= 0) {
-            lo = lower_bound_u32(keys, ng, (uint32_t)(cx0 * kGridRows) << 16);
-            hi = lower_bound_u32(keys, ng, (uint32_t)((cx1 + 1) * kGridRows) << 16);
-        }
-        auto in_window = [&](int g, int& i2) {
-            if (g >= hi) return false;
-            const uint32_t key = keys[g];
-            const int iy = (int)(key >> 16) % kGridRows;
-            if (iy < cy0 || iy > cy1) return false;
-            const float2 p = xy[g];
-            i2 = (int)(key & 0xFFFF);
-            return fabsf(p.x - x) < r && fabsf(p.y - y) < r;
-        };
-        int count = 0;
-        for (int g0 = lo; g0 < hi; g0 += 64) {
-            int i2;
-            count += __popcll(__ballot(in_window(g0 + lane, i2)));
-        }
-        int base = 0;
-        if (lane == 0 && count) base = atomicAdd(&ptotal[pair], count);
-        base = __shfl(base, 0);
-        if (lane == 0) {
-            qoff[(size_t)pair * cap + i1] = base;
-            qcnt[(size_t)pair * cap + i1] = count;
-        }
-        if (!count || base + count > cand_per_pair) continue;   // overflow is detected by k_si_greedy
         const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
         const ulonglong2 a0 = a[0], a1 = a[1];
-        for (int g0 = lo; g0 < hi; g0 += 64) {
+        const SiWindow w = si_window(keys, ng, k1[i1].x, k1[i1].y, (float)window, invW, invH);
+        // lane-local 4 smallest (Hamming << 16 | visit position), with their i2
+        uint32_t hk[SI_TOPK], hi2[SI_TOPK];
+#pragma unroll
+        for (int q = 0; q < SI_TOPK; ++q) hk[q] = hi2[q] = 0xFFFFFFFFu;
+        int count = 0;
+        for (int g0 = w.lo; g0 < w.hi; g0 += 64) {
             int i2 = 0;
-            const bool in = in_window(g0 + lane, i2);
+            const bool in = si_in_window(keys, xy, w, g0 + lane, i2);
             const unsigned long long m = __ballot(in);
             if (in) {
                 const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)i2 * 32);
                 const int d = ham256(a0, a1, b[0], b[1]);
-                const int idx = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                pc[idx] = (uint32_t)i2 | ((uint32_t)d << 16);
+                const int pos = count + lanes_below_u64(m);
+                uint32_t k = ((uint32_t)d << 16) | (uint32_t)pos, v = (uint32_t)i2;
+#pragma unroll
+                for (int q = 0; q < SI_TOPK; ++q) {   // sorted insert
+                    if (k < hk[q]) {
+                        const uint32_t tk = hk[q], tv = hi2[q];
+                        hk[q] = k;
+                        hi2[q] = v;
+                        k = tk;
+                        v = tv;
+                    }
+                }
             }
-            base += __popcll(m);
+            count += __popcll(m);
+        }
+        // wave merge: keys are unique (visit positions), so one lane pops per round
+        uint32_t top[SI_TOPK];
+#pragma unroll
+        for (int q = 0; q < SI_TOPK; ++q) {
+            const uint32_t kmin = wave_min_u32(hk[0]);
+            const unsigned long long wm = __ballot(hk[0] == kmin);
+            const int wl = wm ? (int)__builtin_ctzll(wm) : 0;
+            const uint32_t i2 = (uint32_t)__builtin_amdgcn_readlane((int)hi2[0], wl);
+            top[q] = kmin == 0xFFFFFFFFu ? 0xFFFFFFFFu : ((kmin & 0xFFFF0000u) | i2);
+            if (kmin != 0xFFFFFFFFu && hk[0] == kmin) {
+#pragma unroll
+                for (int r = 0; r + 1 < SI_TOPK; ++r) {
+                    hk[r] = hk[r + 1];
+                    hi2[r] = hi2[r + 1];
+                }
+                hk[SI_TOPK - 1] = hi2[SI_TOPK - 1] = 0xFFFFFFFFu;
+            }
+        }
+        if (lane == 0) {
+            qtop[(size_t)pair * cap + i1] = make_uint4(top[0], top[1], top[2], top[3]);
+            qcnt[(size_t)pair * cap + i1] = count;
         }
     }
 }
 
 struct SgLayout {
-    size_t off, cnt, ang1, ang2, mdist, m21, m12, bin, cand, total;
+    size_t top, cnt, ang1, ang2, mdist, m21, m12, bin, wmax, wmin, total;
 };
 
-__host__ __device__ inline SgLayout sg_layout(int cap, int cand_lds)
+__host__ __device__ inline SgLayout sg_layout(int cap)
 {
     SgLayout L;
     size_t o = 0;
@@ -358,30 +417,35 @@ __host__ __device__ inline SgLayout sg_layout(int cap, int cand_lds)
         o += (b + 15) & ~(size_t)15;
         return r;
     };
-    L.off = take(4 * (size_t)cap);
-    L.cnt = take(4 * (size_t)cap);
+    L.top = take(16 * ((size_t)cap + 2));   // padded with 2 empty entries past n10
+    L.cnt = take(4 * ((size_t)cap + 2));
     L.ang1 = take(4 * (size_t)cap);
     L.ang2 = take(4 * (size_t)cap);
     L.mdist = take(2 * (size_t)cap);
     L.m21 = take(2 * (size_t)cap);
     L.m12 = take(2 * (size_t)cap);
     L.bin = take((size_t)cap);
-    L.cand = take(4 * (size_t)cand_lds);
+    L.wmax = take(4 * (size_t)cap);
+    L.wmin = take(4 * (size_t)cap);
     L.total = o;
     return L;
 }
 
-__global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restrict__ kps, const int* __restrict__ counts,
+__global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restrict__ kps,
+                                                   const uint8_t* __restrict__ desc, const int* __restrict__ counts,
                                                    int cap, const int* __restrict__ pa, const int* __restrict__ pb,
-                                                   float nnratio, int check_ori, const int* __restrict__ gn,
-                                                   const uint32_t* __restrict__ cand, int cand_per_pair, int cand_lds,
-                                                   const int* __restrict__ qoff, const int* __restrict__ qcnt,
-                                                   const int* __restrict__ ptotal, int* __restrict__ m12_out,
-                                                   int* __restrict__ nm_out)
+                                                   int rows, int cols, int window, float nnratio, int check_ori,
+                                                   const uint32_t* __restrict__ gkeys,
+                                                   const float2* __restrict__ gxy, const int* __restrict__ gn,
+                                                   const int* __restrict__ qcnt, const uint4* __restrict__ qtop,
+                                                   int* __restrict__ m12_out, int* __restrict__ nm_out)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const SgLayout Ly = sg_layout(cap, cand_lds);
-    int* off = (int*)(smem + Ly.off);
+#ifdef ORBX_SI_PROF
+    const long long pt0 = clock64();
+#endif
+    const SgLayout Ly = sg_layout(cap);
+    uint4* top = (uint4*)(smem + Ly.top);
     int* cnt = (int*)(smem + Ly.cnt);
     float* ang1 = (float*)(smem + Ly.ang1);
     float* ang2 = (float*)(smem + Ly.ang2);
@@ -389,34 +453,29 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
     int16_t* m21 = (int16_t*)(smem + Ly.m21);
     int16_t* m12 = (int16_t*)(smem + Ly.m12);
     int8_t* bin = (int8_t*)(smem + Ly.bin);
-    uint32_t* cl = (uint32_t*)(smem + Ly.cand);
+    uint32_t* wmax = (uint32_t*)(smem + Ly.wmax);
+    uint32_t* wmin = (uint32_t*)(smem + Ly.wmin);
     __shared__ int s_hist[32];
     const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int fa = pa[pair], fb = pb[pair];
     const int n1 = min(counts[fa], cap), n2 = min(counts[fb], cap);
-    const int n10 = gn[2 * fa];
-    const int total = ptotal[pair];
+    const int n10 = gn[2 * fa], ng = gn[2 * fb + 1];
     int* out = m12_out + (size_t)pair * cap;
-    if (total > cand_per_pair) {   // scratch too small for this pair: report, leave no matches
-        for (int i = tid; i < cap; i += 256) out[i] = -1;
-        if (tid == 0) nm_out[pair] = -1;
-        return;
-    }
-    const uint32_t* gc = cand + (size_t)pair * cand_per_pair;
-    const bool in_lds = total <= cand_lds;
-    if (in_lds)
-        for (int j = tid; j < total; j += 256) cl[j] = gc[j];
-    const uint32_t* pc = in_lds ? cl : gc;
     const orbx_keypoint* k1 = kps + (size_t)fa * cap;
     const orbx_keypoint* k2 = kps + (size_t)fb * cap;
     for (int i = tid; i < n10; i += 256) {
-        off[i] = qoff[(size_t)pair * cap + i];
         cnt[i] = qcnt[(size_t)pair * cap + i];
+        top[i] = qtop[(size_t)pair * cap + i];
         ang1[i] = k1[i].angle;
+    }
+    if (tid < 2) {
+        cnt[n10 + tid] = 0;
+        top[n10 + tid] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     }
     for (int i = tid; i < n2; i += 256) {
         mdist[i] = 0xFFFF;   // INT_MAX: larger than any distance
         m21[i] = -1;
+        wmax[i] = wmin[i] = 0;
         ang2[i] = k2[i].angle;
     }
     for (int i = tid; i < n1; i += 256) {
@@ -426,61 +485,221 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
     if (tid < 32) s_hist[tid] = 0;
     __syncthreads();
     if (tid >= 64) return;
+#ifdef ORBX_SI_PROF
+    const long long pt1 = clock64();
+#endif
 
-    int nmatches = 0;
-    const float factor = 1.0f / 30;
-    for (int i1 = 0; i1 < n10; ++i1) {
-        const int c = cnt[i1];
-        if (c == 0) continue;   // vIndices2.empty()
-        const int o0 = off[i1];
-        // lane-local best (first min) and second (2nd order statistic) over this lane's candidates
-        uint32_t b1 = 0x1FF, b2 = 0x1FF, bp = 0xFFFF;
-        for (int j = lane; j < c; j += 64) {
-            const uint32_t e = pc[o0 + j];
-            const uint32_t i2 = e & 0xFFFF, d = e >> 16;
-            if ((uint32_t)mdist[i2] <= d) continue;
-            if (d < b1) {
-                b2 = b1;
-                b1 = d;
-                bp = (uint32_t)j;
-            } else if (d < b2) {
-                b2 = d;
+    // Greedy pass, 64 steps at a time (lane = step).  m12 holds each query's tentative
+    // match (kept even if a later query evicts it: the reference's rotHist keeps evicted
+    // entries too, :506-536); the final vnMatches12 is m12[i1] where m21 still points back.
+    //
+    // A step's outcome is a function of mdist over its top-4 targets, which earlier steps
+    // change only by their own matches.  Each lane decides from the mdist of the chunk's
+    // start patched with the previous round's decisions of the lanes before it; a round
+    // publishes every lane's match (target, lane, distance) in LDS tables stamped with the
+    // round, so a lane finds the last earlier writer of each of its targets with two reads.
+    // The rounds reach the fixed point where every lane's decision follows from the ones
+    // before it, which is the sequential result.  A step that needs a full scan ends the
+    // chunk's exact prefix: it is replayed on its own with the wave.
+    const int n2c = max(n2 - 1, 0);
+    const float invW = (float)kGridCols / ((float)cols - 0.0f);
+    const float invH = (float)kGridRows / ((float)rows - 0.0f);
+    auto decide = [&](const uint32_t (&e)[SI_TOPK], const uint32_t (&md)[SI_TOPK], int c, int& bi, int& bd,
+                      bool& scan) -> bool {
+        bool ok[SI_TOPK];
+        int d[SI_TOPK];
+#pragma unroll
+        for (int q = 0; q < SI_TOPK; ++q) {
+            d[q] = (int)(e[q] >> 16);
+            ok[q] = e[q] != 0xFFFFFFFFu && md[q] > (uint32_t)d[q];   // vMatchedDistance[i2] <= dist: skip
+        }
+        const int nf = (int)ok[0] + (int)ok[1] + (int)ok[2] + (int)ok[3];
+        // best = first survivor, second = the next one (entries are in (dist, position) order)
+        int bd2 = INT_MAX;
+        bd = INT_MAX;
+        bi = -1;
+        if (ok[0]) {
+            bd = d[0];
+            bi = (int)(e[0] & 0xFFFF);
+            bd2 = ok[1] ? d[1] : ok[2] ? d[2] : ok[3] ? d[3] : INT_MAX;
+        } else if (ok[1]) {
+            bd = d[1];
+            bi = (int)(e[1] & 0xFFFF);
+            bd2 = ok[2] ? d[2] : ok[3] ? d[3] : INT_MAX;
+        } else if (ok[2]) {
+            bd = d[2];
+            bi = (int)(e[2] & 0xFFFF);
+            bd2 = ok[3] ? d[3] : INT_MAX;
+        } else if (ok[3]) {
+            bd = d[3];
+            bi = (int)(e[3] & 0xFFFF);
+        }
+        // Candidates past the top-4 have Hamming >= d[3], so when fewer than two of the
+        // top-4 survive, d[3] usually settles the step without the rest:
+        //   none survive  -> best >= d[3]: no match if d[3] > TH_LOW;
+        //   one survives  -> second >= d[3]: the ratio test holds if best < d[3] * r.
+        scan = false;
+        if (c > SI_TOPK && nf < 2) {
+            if (nf == 0)
+                scan = d[3] <= 50;
+            else if (bd <= 50 && (float)bd < (float)d[3] * nnratio)
+                bd2 = d[3];   // stands in for the exact second: both pass the test
+            else
+                scan = bd <= 50;
+        }
+        return !scan && bd <= 50 && (float)bd < (float)bd2 * nnratio;   // TH_LOW, mfNNratio
+    };
+    uint32_t stamp = 0;   // round stamp of the writer tables (tables start at 0)
+    int base = 0;
+    while (base < n10) {
+        const int i1 = base + lane;
+        const bool act = i1 < n10;
+        const int ii = min(i1, n10);   // top[n10] is an empty entry
+        const uint4 tv = top[ii];
+        const int c = act ? cnt[ii] : 0;
+        const uint32_t e[SI_TOPK] = {tv.x, tv.y, tv.z, tv.w};
+        uint32_t md0[SI_TOPK], md[SI_TOPK];
+#pragma unroll
+        for (int q = 0; q < SI_TOPK; ++q) {
+            const uint32_t v = mdist[min((int)(e[q] & 0xFFFF), n2c)];
+            md0[q] = md[q] = e[q] == 0xFFFFFFFFu ? 0u : v;
+        }
+        int bi, bd;
+        bool scan;
+        bool mt = decide(e, md, c, bi, bd, scan);
+        for (;;) {
+            ++stamp;
+            if (mt) {
+                atomicMax(&wmax[bi], (stamp << 12) | ((uint32_t)lane << 6) | (uint32_t)bd);
+                atomicMax(&wmin[bi], (stamp << 12) | ((uint32_t)(63 - lane) << 6) | (uint32_t)bd);
+            }
+            wave_lds_sync();
+            bool amb = false;
+#pragma unroll
+            for (int q = 0; q < SI_TOPK; ++q) {
+                const int i2 = min((int)(e[q] & 0xFFFF), n2c);
+                const uint32_t a = wmax[i2], b = wmin[i2];
+                md[q] = md0[q];
+                if (e[q] != 0xFFFFFFFFu && (a >> 12) == stamp) {
+                    const int hi = (int)((a >> 6) & 63), lo = 63 - (int)((b >> 6) & 63);
+                    if (hi < lane)
+                        md[q] = a & 63;   // the last writer before this lane
+                    else if (lo < lane)
+                        amb = true;       // writers on both sides: resolved below
+                }
+            }
+            if (__ballot(amb)) {
+                // exact last-earlier-writer by broadcasting every lane's decision
+#pragma unroll
+                for (int q = 0; q < SI_TOPK; ++q) md[q] = md0[q];
+                for (int j = 0; j < 64; ++j) {
+                    if (!__builtin_amdgcn_readlane((int)mt, j)) continue;
+                    const int bij = __builtin_amdgcn_readlane(bi, j), bdj = __builtin_amdgcn_readlane(bd, j);
+#pragma unroll
+                    for (int q = 0; q < SI_TOPK; ++q)
+                        if (j < lane && e[q] != 0xFFFFFFFFu && (int)(e[q] & 0xFFFF) == bij) md[q] = (uint32_t)bdj;
+                }
+            }
+            int nbi, nbd;
+            bool nscan;
+            const bool nmt = decide(e, md, c, nbi, nbd, nscan);
+            const bool ch = nmt != mt || nbi != bi || nbd != bd || nscan != scan;
+            mt = nmt;
+            bi = nbi;
+            bd = nbd;
+            scan = nscan;
+            if (!__ballot(ch)) break;
+        }
+        // the first step that needs a scan bounds the exact prefix
+        const unsigned long long sm = __ballot(act && scan);
+        const int lim = sm ? (int)__builtin_ctzll(sm) : min(64, n10 - base);
+        // commit: tentative m12 for every match; the last writer of a target owns m21/mdist
+        ++stamp;
+        const bool cm = mt && lane < lim;
+        if (cm) atomicMax(&wmax[bi], (stamp << 12) | ((uint32_t)lane << 6) | (uint32_t)bd);
+        wave_lds_sync();
+        if (cm) {
+            m12[i1] = (int16_t)bi;
+            if ((int)((wmax[bi] >> 6) & 63) == lane) {
+                m21[bi] = (int16_t)i1;   // evicts the previous owner (:513-517)
+                mdist[bi] = (uint16_t)bd;
             }
         }
-        // wave: best = min (dist, position); second = min over lanes of (winner ? its b2 : b1)
-        const uint32_t key = (b1 << 16) | bp;
-        const uint32_t kmin = wave_min_u32(key);
-        const uint32_t sec = wave_min_u32(key == kmin ? b2 : b1);
-        const int bd = (int)(kmin >> 16);
-        const int bd2 = sec >= 0x1FF ? INT_MAX : (int)sec;
-        const int bpos = (int)(kmin & 0xFFFF);
-        if (bd <= 50 && (float)bd < (float)bd2 * nnratio) {
-            const int bi = (int)(pc[o0 + bpos] & 0xFFFF);
-            if (lane == 0) {
-                if (m21[bi] >= 0) {
-                    m12[m21[bi]] = -1;
-                    --nmatches;
+        wave_lds_sync();
+        base += lim;
+        if (sm) {
+            // step `base`: re-enumerate its window (global grid of frame fb) and scan it with
+            // the current mdist: lane-local best (first min) and second, best = min (dist,
+            // position) over lanes, second = min over lanes of (winner ? its b2 : b1)
+            const int q1 = base;
+            const uint32_t* keys = gkeys + (size_t)fb * cap;
+            const float2* xy = gxy + (size_t)fb * cap;
+            const ulonglong2* a = (const ulonglong2*)(desc + ((size_t)fa * cap + q1) * 32);
+            const ulonglong2 a0 = a[0], a1 = a[1];
+            const SiWindow w = si_window(keys, ng, k1[q1].x, k1[q1].y, (float)window, invW, invH);
+            uint32_t b1 = 0x1FF, b2 = 0x1FF, bp = 0xFFFF, bx = 0;
+            int count = 0;
+            for (int g0 = w.lo; g0 < w.hi; g0 += 64) {
+                int i2 = 0;
+                const bool in = si_in_window(keys, xy, w, g0 + lane, i2);
+                const unsigned long long m = __ballot(in);
+                if (in) {
+                    const ulonglong2* b = (const ulonglong2*)(desc + ((size_t)fb * cap + i2) * 32);
+                    const uint32_t d = (uint32_t)ham256(a0, a1, b[0], b[1]);
+                    if ((uint32_t)mdist[i2] > d) {
+                        if (d < b1) {
+                            b2 = b1;
+                            b1 = d;
+                            bp = (uint32_t)(count + lanes_below_u64(m));
+                            bx = (uint32_t)i2;
+                        } else if (d < b2) {
+                            b2 = d;
+                        }
+                    }
                 }
-                m12[i1] = (int16_t)bi;
-                m21[bi] = (int16_t)i1;
-                mdist[bi] = (uint16_t)bd;
-                ++nmatches;
-                if (check_ori) {
-                    float rot = ang1[i1] - ang2[bi];
-                    if (rot < 0.0f) rot += 360.0f;
-                    int bb = (int)roundf(rot * factor);
-                    if (bb == 30) bb = 0;
-                    bin[i1] = (int8_t)bb;
-                    s_hist[bb] += 1;
+                count += __popcll(m);
+            }
+            const uint32_t key = (b1 << 16) | bp;
+            const uint32_t kmin = wave_min_u32(key);
+            const uint32_t sec = wave_min_u32(key == kmin ? b2 : b1);
+            const unsigned long long wm = __ballot(key == kmin);
+            const int wl = wm ? (int)__builtin_ctzll(wm) : 0;
+            const int sbd = kmin >> 16 >= 0x1FF ? INT_MAX : (int)(kmin >> 16);
+            const int sbd2 = sec >= 0x1FF ? INT_MAX : (int)sec;
+            if (sbd <= 50 && (float)sbd < (float)sbd2 * nnratio) {
+                const int sbi = __builtin_amdgcn_readlane((int)bx, wl);
+                if (lane == 0) {
+                    m12[q1] = (int16_t)sbi;
+                    m21[sbi] = (int16_t)q1;
+                    mdist[sbi] = (uint16_t)sbd;
                 }
             }
-            nmatches = __shfl(nmatches, 0);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_lds_sync();
+            base += 1;
         }
     }
-    if (check_ori) {
+#ifdef ORBX_SI_PROF
+    const long long pt2 = clock64();
+#endif
+    // rotation bins of every match made (evicted ones included), final vnMatches12
+    const float factor = 1.0f / 30;
+    for (int i = lane; i < n10; i += 64) {
+        const int b = m12[i];
+        if (b < 0) continue;
+        if (check_ori) {
+            float rot = ang1[i] - ang2[b];
+            if (rot < 0.0f) rot += 360.0f;
+            int bb = (int)roundf(rot * factor);
+            if (bb == 30) bb = 0;
+            bin[i] = (int8_t)bb;
+            atomicAdd(&s_hist[bb], 1);
+        }
+        if (m21[b] != i) m12[i] = -1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (check_ori) {   // ComputeThreeMaxima + removal, src/ORBmatcher.cc:562-580
         int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;
         for (int i = 0; i < 30; ++i) {
             const int s = s_hist[i];
@@ -490,34 +709,42 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
         }
         if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
-        int removed = 0;
         for (int i = lane; i < n10; i += 64) {
             const int bb = bin[i];
             if (bb < 0 || bb == ind1 || bb == ind2 || bb == ind3) continue;
-            if (m12[i] >= 0) {
-                m12[i] = -1;
-                ++removed;
-            }
+            m12[i] = -1;
         }
-        for (int o = 32; o > 0; o >>= 1) removed += __shfl_xor(removed, o);
-        nmatches -= removed;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    for (int i = lane; i < cap; i += 64) out[i] = i < n1 ? (int)m12[i] : -1;
+    int nmatches = 0;
+    for (int i = lane; i < cap; i += 64) {
+        const int v = i < n1 ? (int)m12[i] : -1;
+        out[i] = v;
+        nmatches += v >= 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) nmatches += __shfl_xor(nmatches, o);
     if (lane == 0) nm_out[pair] = nmatches;
+#ifdef ORBX_SI_PROF
+    const long long pt3 = clock64();
+    if (lane == 0) {   // phase cycles (staging, greedy loop, bins+filter+output) over the unused tail
+        out[cap - 4] = (int)(pt1 - pt0);
+        out[cap - 3] = (int)(pt2 - pt1);
+        out[cap - 2] = (int)(pt3 - pt2);
+        out[cap - 1] = n10;
+    }
+#endif
 }
 
-size_t search_init_scratch_bytes(int nframes, int npairs, int cap, int cand_per_pair)
+size_t search_init_scratch_bytes(int nframes, int npairs, int cap)
 {
-    return (size_t)nframes * cap * (4 + 8) + (size_t)nframes * 2 * 4 + (size_t)npairs * cap * 8 + (size_t)npairs * 4 +
-           (size_t)npairs * cand_per_pair * 4 + 64 * 5;
+    return (size_t)nframes * cap * (4 + 8) + (size_t)nframes * 2 * 4 + (size_t)npairs * cap * (4 + 16) + 64 * 6;
 }
 
 void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int nframes, int cap,
                         const int* pa, const int* pb, int npairs, int rows, int cols, int window, float nnratio,
-                        int check_ori, void* scratch, int cand_per_pair, int* m12, int* nm, hipStream_t s)
+                        int check_ori, void* scratch, int* m12, int* nm, hipStream_t s)
 {
     uint8_t* p = (uint8_t*)scratch;
     auto carve = [&](size_t bytes) {
@@ -528,25 +755,21 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     uint32_t* gkeys = (uint32_t*)carve((size_t)nframes * cap * 4);
     float2* gxy = (float2*)carve((size_t)nframes * cap * 8);
     int* gn = (int*)carve((size_t)nframes * 2 * 4);
-    int* qoff = (int*)carve((size_t)npairs * cap * 4);
     int* qcnt = (int*)carve((size_t)npairs * cap * 4);
-    int* ptotal = (int*)carve((size_t)npairs * 4);
-    uint32_t* cand = (uint32_t*)carve((size_t)npairs * cand_per_pair * 4);
+    uint4* qtop = (uint4*)carve((size_t)npairs * cap * 16);
     int p2 = 1;
     while (p2 < cap) p2 <<= 1;
-    hipMemsetAsync(ptotal, 0, (size_t)npairs * 4, s);
     hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)p2 * 4, s, kps, counts, cap, rows, cols, gkeys,
                        gxy, gn);
     const size_t bsmem = (((size_t)cap * 4 + 15) & ~(size_t)15) + (size_t)cap * 8;
-    hipLaunchKernelGGL(k_si_build, dim3(npairs, SI_QSPLIT), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, rows,
-                       cols, window, gkeys, gxy, gn, cand, cand_per_pair, qoff, qcnt, ptotal);
-    const size_t fixed = sg_layout(cap, 0).total + 512;
-    const long left = (long)(160 * 1024) - (long)fixed;
-    const int cand_lds = left > 0 ? (int)(left / 4) : 0;
-    const size_t gsmem = sg_layout(cap, cand_lds).total;
+    // query slices per pair: about 8 waves per SIMD over the chip, at least 4 queries per wave
+    const int qsplit = std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
+    hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, rows,
+                       cols, window, gkeys, gxy, gn, qcnt, qtop);
+    const size_t gsmem = sg_layout(cap).total;
     hipFuncSetAttribute((const void*)k_si_greedy, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gsmem);
-    hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), gsmem, s, kps, counts, cap, pa, pb, nnratio, check_ori, gn,
-                       cand, cand_per_pair, cand_lds, qoff, qcnt, ptotal, m12, nm);
+    hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), gsmem, s, kps, desc, counts, cap, pa, pb, rows, cols,
+                       window, nnratio, check_ori, gkeys, gxy, gn, qcnt, qtop, m12, nm);
 }
 
 }  // namespace orbx

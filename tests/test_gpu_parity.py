@@ -152,6 +152,54 @@ def test_search_for_initialization(orbref, cuda):
     assert nm[0] > 50
 
 
+@pytest.mark.parametrize("seed,noise,nproto", [(1, 0.02, 40), (2, 0.06, 25), (3, 0.10, 12), (4, 0.04, 4)])
+def test_search_for_initialization_contended(orbref, cuda, seed, noise, nproto):
+    """Adversarial SearchForInitialization: descriptors are noisy copies of a few
+    prototypes, so windows hold many candidates within TH_LOW of each other.  This
+    drives evictions, ratio-test near-ties, targets re-matched inside one 64-step
+    chunk, and steps whose top-4 cannot settle them (the full-window scan)."""
+    import torch
+    import orbx
+    rng = np.random.default_rng(seed)
+    W, H, n = 1241, 376, 600
+    cap = 640
+    proto = rng.integers(0, 256, (nproto, 32), dtype=np.uint8)
+    kl, dl = [], []
+    for f in range(2):
+        k = np.zeros(n, orbref.KEYPOINT_DTYPE)
+        k["x"] = rng.uniform(20, W - 20, n).astype(np.float32)
+        k["y"] = rng.uniform(20, H - 20, n).astype(np.float32)
+        k["size"] = 31
+        k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+        k["response"] = rng.integers(1, 80, n).astype(np.float32)
+        k["class_id"] = -1
+        bits = (rng.random((n, 256)) < noise).astype(np.uint8)
+        d = proto[rng.integers(0, nproto, n)] ^ np.packbits(bits, axis=1, bitorder="little")
+        kl.append(k)
+        dl.append(d)
+    kps = np.zeros((2, cap, 7), np.int32)
+    desc = np.zeros((2, cap, 32), np.uint8)
+    for f in range(2):
+        kps[f, :n] = kl[f].view(np.int32).reshape(n, 7)
+        desc[f, :n] = dl[f]
+    tk, td = torch.from_numpy(kps).to(cuda), torch.from_numpy(desc).to(cuda)
+    tc = torch.tensor([n, n], dtype=torch.int32, device=cuda)
+    pa = torch.tensor([0, 1], dtype=torch.int32, device=cuda)
+    pb = torch.tensor([1, 0], dtype=torch.int32, device=cuda)
+    for check_ori in (True, False):
+        m = orbx.ORBmatcher(0.9, check_ori)
+        m12, nm = m.search_for_initialization_batch(tk, td, tc, pa, pb, H, W, 100)
+        torch.cuda.synchronize()
+        m12, nm = m12.cpu().numpy(), nm.cpu().numpy()
+        for p, (a, b) in enumerate([(0, 1), (1, 0)]):
+            want_n, want_m, _ = orbref.search_for_initialization(kl[a], dl[a], kl[b], dl[b], W, H, window=100,
+                                                                 nnratio=0.9, check_ori=check_ori)
+            assert nm[p] == want_n, "pair %d ori %d: %d matches vs oracle %d" % (p, check_ori, nm[p], want_n)
+            assert np.array_equal(m12[p, :n], want_m), "pair %d ori %d differ at %s" % (
+                p, check_ori, np.nonzero(m12[p, :n] != want_m)[0][:5])
+            assert want_n > 0
+
+
 @pytest.mark.parametrize("nq,nt", [(1000, 777), (257, 5000), (10000, 1024)])
 def test_allpairs(orbref, cuda, nq, nt):
     import torch
