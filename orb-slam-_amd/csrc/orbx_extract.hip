@@ -131,12 +131,14 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
 // ---------------------------------------------------------------------------
 // ROI tile row pitch (dword aligned, +1 dword of slack for the 8-byte realigning read)
 __host__ __device__ inline int fast_tile_pitch(int max_roi_w) { return ((max_roi_w + 3) & ~3) + 4; }
-// per-wave LDS: ROI tile + zero-bordered strength map of the detection window
+// per-wave LDS: ROI tile + zero-bordered strength map of the detection window + the
+// candidate list (u16 pixel indices)
 __host__ __device__ inline size_t fast_wave_bytes(int max_roi_w, int max_roi_h)
 {
     const size_t tile = (size_t)max_roi_h * fast_tile_pitch(max_roi_w);
     const size_t map = (size_t)(max_roi_h - 4) * (max_roi_w - 4);
-    return (tile + map + 15) & ~(size_t)15;
+    const size_t list = 2 * (size_t)(max_roi_h - 6) * (max_roi_w - 6);
+    return (((tile + map + 15) & ~(size_t)15) + list + 15) & ~(size_t)15;
 }
 
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
@@ -179,6 +181,18 @@ __device__ __forceinline__ int fast_strength(const uint8_t* c, int st)
     return max(v - minMax, maxMin - v);
 }
 
+// Necessary condition for s > t: a 9-arc holds two consecutive compass points
+// (ring positions 0, 4, 8, 12), so some consecutive pair is brighter than v+t or
+// some pair is darker than v-t.
+__device__ __forceinline__ bool fast_compass(const uint8_t* c, int st, int t)
+{
+    const int v = c[0];
+    const int a = c[3 * st], b = c[3], d = c[-3 * st], e = c[-3];
+    const int br = max(max(min(a, b), min(b, d)), max(min(d, e), min(e, a)));
+    const int dk = min(min(max(a, b), max(b, d)), min(max(d, e), max(e, a)));
+    return br > v + t || dk < v - t;
+}
+
 __device__ __forceinline__ bool nms_keep(const uint8_t* m, int p, int W2, int t)
 {
     const int s = m[p];
@@ -211,6 +225,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     const uint8_t* img = level_base(P, G, f, C.level, pitch);
     uint8_t* tile = s_fast + (size_t)wave * fast_wave_bytes(G->max_roi_w, G->max_roi_h);
     uint8_t* map = tile + (size_t)G->max_roi_h * kTileP;
+    uint16_t* list = (uint16_t*)(tile + (((size_t)G->max_roi_h * kTileP +
+                                          (size_t)(G->max_roi_h - 4) * (G->max_roi_w - 4) + 15) & ~(size_t)15));
     const int rw = C.roi_w, rh = C.roi_h;
     const int dw = rw - 6, dh = rh - 6;
     int* out_count = cell_counts + (size_t)f * G->ncells + c;
@@ -233,25 +249,54 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     for (int i = lane; i < W2 * (dh + 2); i += 64) map[i] = 0;
     wave_lds_sync();
 
+    // Pass 1: compass filter at the lower of the two thresholds; survivors listed in
+    // row-major order.  Pass 2: exact strength of the listed pixels into the map; the
+    // list keeps those above the lower threshold (in place: a round writes at or
+    // before the entries it has read).  Only listed pixels can pass either NMS test.
+    const int tq = min(G->ini_th, G->min_th);
     const int npx = dw * dh;
     const float inv_dw = 1.0f / (float)dw;   // exact row/col split for npx < 4096
-#pragma unroll 2
-    for (int k = lane; k < npx; k += 64) {
-        const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
-        const int s = fast_strength(tile + (ii + 3) * kTileP + (jj + 3), kTileP);
-        map[(ii + 1) * W2 + jj + 1] = (uint8_t)(s > 0 ? s : 0);
+    int n1 = 0;
+    for (int k0 = 0; k0 < npx; k0 += 64) {
+        const int k = k0 + lane;
+        bool in = false;
+        if (k < npx) {
+            const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
+            in = fast_compass(tile + (ii + 3) * kTileP + (jj + 3), kTileP, tq);
+        }
+        const unsigned long long m = __ballot(in);
+        if (in) list[n1 + lanes_below(m)] = (uint16_t)k;
+        n1 += __popcll(m);
+    }
+    wave_lds_sync();
+    int n2 = 0;
+    for (int j0 = 0; j0 < n1; j0 += 64) {
+        const int j = j0 + lane;
+        bool in = false;
+        int k = 0;
+        if (j < n1) {
+            k = list[j];
+            const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
+            const int s = fast_strength(tile + (ii + 3) * kTileP + (jj + 3), kTileP);
+            in = s > tq;
+            if (in) map[(ii + 1) * W2 + jj + 1] = (uint8_t)s;
+        }
+        const unsigned long long m = __ballot(in);
+        if (in) list[n2 + lanes_below(m)] = (uint16_t)k;
+        n2 += __popcll(m);
     }
     wave_lds_sync();
 
-    // NMS at iniThFAST; survivors remembered per round so the common case needs one pass
-    const int rounds = (npx + 63) >> 6;
-    unsigned long long keepmask = 0;   // bit r: this lane's pixel of round r survives (rounds <= 57)
+    // NMS at iniThFAST over the list; survivors remembered per round (rounds <= 57)
+    const int rounds = (n2 + 63) >> 6;
+    unsigned long long keepmask = 0;
     int t = G->ini_th;
     int kept = 0;
     for (int r = 0; r < rounds; ++r) {
-        const int k = lane + (r << 6);
+        const int j = lane + (r << 6);
         bool keep = false;
-        if (k < npx) {
+        if (j < n2) {
+            const int k = list[j];
             const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
             keep = nms_keep(map, (ii + 1) * W2 + jj + 1, W2, t);
         }
@@ -262,9 +307,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
         t = G->min_th;
         keepmask = 0;
         for (int r = 0; r < rounds; ++r) {
-            const int k = lane + (r << 6);
+            const int j = lane + (r << 6);
             bool keep = false;
-            if (k < npx) {
+            if (j < n2) {
+                const int k = list[j];
                 const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
                 keep = nms_keep(map, (ii + 1) * W2 + jj + 1, W2, t);
             }
@@ -279,7 +325,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
         const bool keep = (keepmask >> r) & 1ull;
         const unsigned long long m = __ballot(keep);
         if (keep) {
-            const int k = lane + (r << 6);
+            const int k = list[lane + (r << 6)];
             const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
             const int idx = base + lanes_below(m);
             out[idx] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + ii),
