@@ -187,20 +187,27 @@ def main():
         "pyramid": B * sum(A[l - 1] + A[l] for l in range(1, NLEVELS)),
         "fast": B * (sum(A) + 4 * cand),
         "quadtree": B * (4 * cand + 4 * kept),
-        "describe": B * kept * (43 * 43 + 4 + 60),
+        # compulsory bytes: every level pixel once (patches overlap), the packed keypoint in,
+        # the 28 B keypoint + 32 B descriptor out
+        "describe": B * (sum(A) + kept * (4 + 60)),
         "match": (B - 1) * 2 * kept * 60,
     }
     dom = max(stages, key=lambda k: stages[k])
     launches = {"pyramid": NLEVELS - 1}.get(dom, 1)
     t_launch = stages[dom] / launches * 1e-3
     achieved = alg[dom] / launches / t_launch / 1e9
+    kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree",
+             "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
+    # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
+    # same command (tools/collect_pmc.sh -> tools/pmc_summary.py); null when absent
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
             d = json.load(open(pmc))
-            if d.get("kernel_stage") == dom and d.get("batch") == B:
-                traffic = d.get("bytes_per_launch")
+            if d.get("batch") == B:
+                parts = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"]}.get(dom, [kname])
+                traffic = int(sum(d["kernels"][k]["bytes_per_launch"] for k in parts))
         except Exception:
             traffic = None
     out = {
@@ -222,9 +229,7 @@ def main():
         "stage_ms_per_step": {k: round(v, 4) for k, v in stages.items()},
         "keypoints_per_frame": round(kept, 1),
         "matches_per_pair": round(float(nmatch.mean()), 1),
-        "roofline": {"bound": "hbm", "kernel": {"pyramid": "k_pyramid_level", "fast": "k_fast_cells",
-                                                 "quadtree": "k_quadtree", "describe": "k_describe",
-                                                 "match": "k_search_init"}[dom],
+        "roofline": {"bound": "hbm", "kernel": kname,
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "alg_bytes_per_launch": int(alg[dom] / launches)},

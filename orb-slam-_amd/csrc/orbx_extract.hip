@@ -56,7 +56,8 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
     // staged in LDS with coalesced dword loads (realigned with v_alignbyte, so any
     // source pitch works), then each thread makes 4 output pixels per dword store.
     extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
-    const int f = blockIdx.z, dy0 = blockIdx.y * kPyrRows;
+    const int lb = xcd_block(blockIdx.y + blockIdx.z * gridDim.y, gridDim.y * gridDim.z);
+    const int f = lb / gridDim.y, dy0 = (lb - f * gridDim.y) * kPyrRows;
     const LevelGeom& D = G->lv[l];
     const int sw = G->lv[l - 1].w;
     const int dyn = min(kPyrRows, D.h - dy0);
@@ -217,8 +218,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
     const int kTileP = fast_tile_pitch(G->max_roi_w);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int f = blockIdx.y;
-    const int c = blockIdx.x * 4 + wave;
+    const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    const int f = lb / gridDim.x;
+    const int c = (lb - f * gridDim.x) * 4 + wave;
     if (c >= G->ncells) return;   // wave-uniform; no block barriers below
     const Cell C = cells[c];
     int pitch;
@@ -886,13 +888,14 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
     __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][kRawSlots];
     __shared__ __attribute__((aligned(16))) uint32_t s_rowT[4][kTCols * kTP];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int f = blockIdx.y;
+    const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    const int f = lb / gridDim.x, bx = lb - f * gridDim.x;
     const int L = G->nlevels;
     const int* cnts = qt_cnt + (size_t)f * L;
     uint32_t* raw32 = s_raw[wave];
     uint8_t* raw = (uint8_t*)raw32;
     uint32_t* rowT = s_rowT[wave];
-    const int g0 = (blockIdx.x * 4 + wave) * kDescPerWave;
+    const int g0 = (bx * 4 + wave) * kDescPerWave;
 
     // ---- keypoint-independent lane state, set up once for the wave's keypoints ----
     // IC_Angle: the lane owns disc column u = (lane & 31) - 15 (lanes 31, 63 idle) and the

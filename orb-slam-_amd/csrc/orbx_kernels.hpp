@@ -31,6 +31,18 @@ struct ExtractBufs {
     int* status;                // device error word (bit flags)
 };
 
+// XCD-aware workgroup order.  The dispatcher hands flat workgroup id b to XCD b % 8;
+// each XCD has its own 4 MiB L2.  xcd_block maps b to a logical id so that every
+// XCD owns one contiguous range of logical ids (whole frames, in order), so the
+// overlapping reads of neighbouring cells / keypoint patches hit that XCD's L2.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_block(int b, int nblocks)
+{
+    const int q = nblocks / kXcds, r = nblocks - q * kXcds;
+    const int x = b % kXcds, k = b / kXcds;
+    return x * q + min(x, r) + k;
+}
+
 enum : int {
     kStatusListOverflow = 1,
     kStatusOutOverflow = 2,

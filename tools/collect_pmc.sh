@@ -5,9 +5,10 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=${1:-r01}
 cd /tmp && export TMPDIR=/tmp
+mkdir -p $R/gpurun_out/pmc_$TAG
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d $R/gpurun_out/pmc_$TAG/$C -o run -- \
+  timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d $R/gpurun_out/pmc_$TAG/$C -o run -- \
     python3 $R/bench.py --steps 5 --warmup 1 --no-cpu > $R/gpurun_out/pmc_$TAG/bench_$C.json 2> $R/gpurun_out/pmc_$TAG/bench_$C.err \
     || { echo PMC_FAIL $C; tail -20 $R/gpurun_out/pmc_$TAG/bench_$C.err; exit 1; }
 done
-python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_$TAG
+python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_$TAG --profiles $R/gpurun_out/pmc_$TAG/pmc_traffic.json
