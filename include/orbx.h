@@ -100,6 +100,31 @@ orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n);
 orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t out_size);
 orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys, int cap, int* n);
 
+/* ---- Stereo (Frame::ComputeStereoMatches, src/Frame.cc:630-872) ----
+ * bf = Camera.bf (mbf), fx = K(0,0).  The search limits follow :676-681 with
+ * mb = bf / fx (the value src/Frame.cc:140 assigns; the reference reads mb one
+ * statement before that assignment).  Outputs mvuRight / mvDepth per left
+ * keypoint (-1 = no stereo match) and the number of matches kept after the
+ * median cut. */
+
+/* Host path: `left` / `right` are the extractor handles (mpORBextractorLeft/Right)
+ * right after their orbx_extract on the two images; kps/desc are what those calls
+ * returned.  The SAD stage reads both handles' device pyramids (no pyramid D2H). */
+orbx_status orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orbx_keypoint* kps_l,
+                                        const uint8_t* desc_l, int n_l, const orbx_keypoint* kps_r,
+                                        const uint8_t* desc_r, int n_r, float bf, float fx, float* u_right,
+                                        float* depth, int* n_good);
+
+/* Batched device path (config 3): `npairs` stereo pairs of the handle's last
+ * orbx_extract_batch_device batch, left frame d_left[p], right frame d_right[p]
+ * (kps/desc/counts/cap as produced by that call; its level-0 images must still be
+ * resident).  Outputs d_u_right[p*cap + i], d_depth[p*cap + i], d_n_good[p].
+ * Asynchronous on `stream`. */
+orbx_status orbx_stereo_batch_device(orbx_handle* h, const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                                     const int* d_counts, int cap, const int* d_left, const int* d_right,
+                                     int npairs, float bf, float fx, float* d_u_right, float* d_depth,
+                                     int* d_n_good, void* stream);
+
 /* ---- Matcher (ORBmatcher Hamming inner loops, include/ORBmatcher.h:37-102) ---- */
 
 /* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1728-1744), host helper. */

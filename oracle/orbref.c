@@ -867,3 +867,168 @@ void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,
         best_idx[i] = bi; best_d[i] = b1; second_d[i] = b2;
     }
 }
+
+/* ---- a15: Frame::ComputeStereoMatches, src/Frame.cc:630-872 -------------- */
+/* Level l of a concatenated pyramid dump (orbref_extract's `pyramid` layout). */
+static const uint8_t* pyr_level(const uint8_t* pyr, const orbref_tables* t, int l, int cols, int rows, int* w, int* h)
+{
+    size_t o = 0;
+    for (int q = 0; q < l; q++) {
+        int qw, qh;
+        orbref_level_size(t, q, cols, rows, &qw, &qh);
+        o += (size_t)qw * qh;
+    }
+    orbref_level_size(t, l, cols, rows, w, h);
+    return pyr + o;
+}
+
+static int cmp_dist_idx(const void* a, const void* b)
+{
+    const int* x = (const int*)a;
+    const int* y = (const int*)b;
+    if (x[0] != y[0]) return x[0] < y[0] ? -1 : 1;   /* std::pair<int,int> ordering */
+    return x[1] < y[1] ? -1 : (x[1] > y[1]);
+}
+
+int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, const uint8_t* pyrL,
+                                  const uint8_t* pyrR, const orbref_keypoint* kL, const uint8_t* dL, int nL,
+                                  const orbref_keypoint* kR, const uint8_t* dR, int nR, float bf, float fx,
+                                  float* uRight, float* depth, int* sad_out)
+{
+    orbref_tables t;
+    if (orbref_make_tables(p, &t) != 0) return -22;
+    for (int i = 0; i < nL; i++) { uRight[i] = -1.0f; depth[i] = -1.0f; if (sad_out) sad_out[i] = -1; }  /* :633-634 */
+    const int thOrbDist = (100 + TH_LOW) / 2;                                                             /* :638 */
+    const int nRows = rows;                                                                               /* :641 */
+
+    /* row table :645-673: vRowIndices[yi] lists iR in increasing order.  Rows outside
+     * [0, nRows) are UB in the reference (never reached for kps >= 19 px from the edge);
+     * they are dropped here. */
+    int* rcnt = (int*)calloc((size_t)nRows + 1, sizeof(int));
+    for (int iR = 0; iR < nR; iR++) {
+        const float kpY = kR[iR].y;
+        const float r = 2.0f * t.scale[kR[iR].octave];
+        const int maxr = (int)ceilf(kpY + r);
+        const int minr = (int)floorf(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) rcnt[yi + 1]++;
+    }
+    for (int y = 0; y < nRows; y++) rcnt[y + 1] += rcnt[y];
+    int* ridx = (int*)malloc(sizeof(int) * ((size_t)rcnt[nRows] + 1));
+    int* rfill = (int*)calloc((size_t)nRows + 1, sizeof(int));
+    for (int iR = 0; iR < nR; iR++) {
+        const float kpY = kR[iR].y;
+        const float r = 2.0f * t.scale[kR[iR].octave];
+        const int maxr = (int)ceilf(kpY + r);
+        const int minr = (int)floorf(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) ridx[rcnt[yi] + rfill[yi]++] = iR;
+    }
+
+    /* :676-681.  The reference reads the member mb before Frame's constructor assigns
+     * it (src/Frame.cc:108 vs :140); the intended value mb = mbf/fx is used. */
+    const float mb = bf / fx;
+    const float minZ = mb;
+    const float minD = 0;
+    const float maxD = bf / minZ;
+
+    int* vDistIdx = (int*)malloc(sizeof(int) * 2 * ((size_t)nL + 1));
+    int nd = 0;
+    for (int iL = 0; iL < nL; iL++) {
+        const orbref_keypoint* kpL = &kL[iL];
+        const int levelL = kpL->octave;
+        const float vL = kpL->y, uL = kpL->x;
+        const size_t row = (size_t)vL;                       /* vRowIndices[vL], :699 */
+        if (row >= (size_t)nRows) continue;
+        const int c0 = rcnt[row], c1 = rcnt[row + 1];
+        if (c0 == c1) continue;                              /* :702-703 */
+        const float minU = uL - maxD, maxU = uL - minD;      /* :707-708 */
+        if (maxU < 0) continue;
+        int bestDist = 100;                                  /* ORBmatcher::TH_HIGH */
+        int bestIdxR = 0;
+        for (int c = c0; c < c1; c++) {                      /* :723-757 */
+            const int iR = ridx[c];
+            const orbref_keypoint* kpR = &kR[iR];
+            if (kpR->octave < levelL - 1 || kpR->octave > levelL + 1) continue;
+            const float uR = kpR->x;
+            if (uR >= minU && uR <= maxU) {
+                const int dist = orbref_descriptor_distance(dL + 32 * (size_t)iL, dR + 32 * (size_t)iR);
+                if (dist < bestDist) { bestDist = dist; bestIdxR = iR; }
+            }
+        }
+        if (bestDist >= thOrbDist) continue;                 /* :762 */
+
+        /* sub-pixel match by correlation, :764-853 */
+        const float uR0 = kR[bestIdxR].x;
+        const float scaleFactor = t.inv_scale[levelL];
+        const float scaleduL = roundf(kpL->x * scaleFactor);
+        const float scaledvL = roundf(kpL->y * scaleFactor);
+        const float scaleduR0 = roundf(uR0 * scaleFactor);
+        const int w = 5, L = 5;
+        int lw, lh, rw, rh;
+        const uint8_t* IL0 = pyr_level(pyrL, &t, levelL, cols, rows, &lw, &lh);
+        const uint8_t* IR0 = pyr_level(pyrR, &t, levelL, cols, rows, &rw, &rh);
+        const float iniu = scaleduR0 + L - w;                /* quirk kept: +L, :795 */
+        const float endu = scaleduR0 + L + w + 1;
+        if (iniu < 0 || endu >= rw) continue;
+        const int vy = (int)scaledvL, ux = (int)scaleduL, ur = (int)scaleduR0;
+        /* windows read the level's 19-px BORDER_REFLECT_101 padding when they cross an
+         * edge (ComputePyramid :1350-1373); beyond the padding the reference is UB */
+        if (vy - w < -EDGE_THRESHOLD || vy + w >= lh + EDGE_THRESHOLD || ux - w < -EDGE_THRESHOLD ||
+            ux + w >= lw + EDGE_THRESHOLD || ur - L - w < -EDGE_THRESHOLD)
+            continue;
+#define PADPX(img, W, H, X, Y) ((float)(img)[(size_t)reflect101((Y), (H)) * (W) + reflect101((X), (W))])
+        const float cL = PADPX(IL0, lw, lh, ux, vy);
+        float vDists[11];
+        int bestDistS = INT_MAX, bestincR = 0;
+        for (int incR = -L; incR <= L; incR++) {
+            const float cR = PADPX(IR0, rw, rh, ur + incR, vy);
+            double acc = 0.0;                                /* cv::norm(IL, IR, NORM_L1) */
+            for (int y = -w; y <= w; y++)
+                for (int x = -w; x <= w; x++) {
+                    const float a = PADPX(IL0, lw, lh, ux + x, vy + y) - cL;
+                    const float b = PADPX(IR0, rw, rh, ur + incR + x, vy + y) - cR;
+                    acc += fabs((double)a - (double)b);
+                }
+            const float dist = (float)acc;
+            if (dist < (float)bestDistS) { bestDistS = (int)dist; bestincR = incR; }
+            vDists[L + incR] = dist;
+        }
+        if (bestincR == -L || bestincR == L) continue;       /* :816-817 */
+        const float dist1 = vDists[L + bestincR - 1];
+        const float dist2 = vDists[L + bestincR];
+        const float dist3 = vDists[L + bestincR + 1];
+        const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+        if (deltaR < -1 || deltaR > 1) continue;
+        float bestuR = t.scale[levelL] * ((float)scaleduR0 + (float)bestincR + deltaR);
+        float disparity = (uL - bestuR);
+        if (disparity >= minD && disparity < maxD) {
+            if (disparity <= 0) {
+                disparity = (float)0.01;
+                bestuR = (float)((double)uL - 0.01);
+            }
+            depth[iL] = bf / disparity;
+            uRight[iL] = bestuR;
+            if (sad_out) sad_out[iL] = bestDistS;
+            vDistIdx[2 * nd] = bestDistS;
+            vDistIdx[2 * nd + 1] = iL;
+            nd++;
+        }
+    }
+    /* median cut :857-871 (an empty vDistIdx is UB in the reference: nothing to cut) */
+    int good = nd;
+    if (nd > 0) {
+        qsort(vDistIdx, (size_t)nd, 2 * sizeof(int), cmp_dist_idx);
+        const float median = (float)vDistIdx[2 * (nd / 2)];
+        const float thDist = 1.5f * 1.4f * median;
+        for (int i = nd - 1; i >= 0; i--) {
+            if ((float)vDistIdx[2 * i] < thDist) break;
+            uRight[vDistIdx[2 * i + 1]] = -1;
+            depth[vDistIdx[2 * i + 1]] = -1;
+            good--;
+        }
+    }
+#undef PADPX
+    free(rcnt); free(ridx); free(rfill); free(vDistIdx);
+    return good;
+}

@@ -11,7 +11,7 @@
  *   /root/reference/src/ORBmatcher.cc     (DescriptorDistance, SearchForInitialization,
  *                                          ComputeThreeMaxima)
  *   /root/reference/src/Frame.cc          (AssignFeaturesToGrid / PosInGrid /
- *                                          GetFeaturesInArea)
+ *                                          GetFeaturesInArea, ComputeStereoMatches)
  * with the OpenCV 3.x primitives the reference calls (FAST, resize INTER_LINEAR,
  * GaussianBlur, fastAtan2, cvRound) restated from their published generic
  * scalar code paths, and glibc 2.35 cosf/sinf taken
@@ -130,6 +130,17 @@ int orbref_search_for_initialization(const orbref_keypoint* k1, const uint8_t* d
                                      const orbref_keypoint* k2, const uint8_t* d2, int n2,
                                      int cols, int rows, float* prev_xy, int* matches12,
                                      int window, float nnratio, int check_ori);
+
+/* a15: Frame::ComputeStereoMatches (src/Frame.cc:630-872) for one rectified stereo
+ * pair.  pyrL / pyrR: concatenated level images of the left / right extractor
+ * (orbref_extract's `pyramid` dump, both rows x cols at level 0).  bf = Camera.bf,
+ * fx = K(0,0).  Outputs mvuRight / mvDepth (nL floats, -1 = no match) and, if
+ * sad_out != NULL, the best SAD of each pair accepted before the median cut (-1
+ * otherwise).  Returns the number of stereo matches kept. */
+int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, const uint8_t* pyrL,
+                                  const uint8_t* pyrR, const orbref_keypoint* kL, const uint8_t* dL, int nL,
+                                  const orbref_keypoint* kR, const uint8_t* dR, int nR, float bf, float fx,
+                                  float* uRight, float* depth, int* sad_out);
 
 /* Config-5 brute force: per query best index (first min), best and second distance. */
 void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,

@@ -67,6 +67,9 @@ def lib():
         L.orbref_descriptor_distance.argtypes = [u8p, u8p]
         L.orbref_search_for_initialization.argtypes = [C.c_void_p, u8p, C.c_int, C.c_void_p, u8p, C.c_int,
                                                        C.c_int, C.c_int, f32p, i32p, C.c_int, C.c_float, C.c_int]
+        L.orbref_compute_stereo_matches.argtypes = [P(Params), C.c_int, C.c_int, u8p, u8p, C.c_void_p, u8p,
+                                                     C.c_int, C.c_void_p, u8p, C.c_int, C.c_float, C.c_float,
+                                                     f32p, f32p, i32p]
         L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
         _lib = L
     return _lib
@@ -225,6 +228,27 @@ def search_for_initialization(kps1, desc1, kps2, desc2, cols, rows, window=100, 
                                                 n2, cols, rows, _f32(prev_xy), _i32(m12), window, nnratio,
                                                 1 if check_ori else 0)
     return nm, m12[:n1].copy(), prev_xy
+
+
+def compute_stereo_matches(p: Params, left: ExtractResult, right: ExtractResult, rows: int, cols: int,
+                           bf: float, fx: float):
+    """Frame::ComputeStereoMatches on two oracle extractions (want_pyramid=True).
+    Returns (uRight, depth, sad, ngood)."""
+    pl = np.ascontiguousarray(np.concatenate([l.ravel() for l in left.pyramid]))
+    pr = np.ascontiguousarray(np.concatenate([l.ravel() for l in right.pyramid]))
+    kl = np.ascontiguousarray(left.keypoints, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(right.keypoints, KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(left.descriptors, np.uint8)
+    dr = np.ascontiguousarray(right.descriptors, np.uint8)
+    n = len(kl)
+    ur = np.empty(max(n, 1), np.float32)
+    dp = np.empty(max(n, 1), np.float32)
+    sd = np.empty(max(n, 1), np.int32)
+    good = lib().orbref_compute_stereo_matches(C.byref(p), rows, cols, _u8(pl), _u8(pr), kl.ctypes.data, _u8(dl), n,
+                                               kr.ctypes.data, _u8(dr), len(kr), bf, fx, _f32(ur), _f32(dp), _i32(sd))
+    if good < 0:
+        raise RuntimeError("orbref_compute_stereo_matches failed: %d" % good)
+    return ur[:n].copy(), dp[:n].copy(), sd[:n].copy(), good
 
 
 def allpairs_top2(q: np.ndarray, t: np.ndarray):

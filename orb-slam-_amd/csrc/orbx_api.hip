@@ -245,6 +245,7 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         out += L.cap;
         lcap = std::max(lcap, L.cap + 4);
         L.scale = t.scale[l];
+        L.inv_scale = t.inv_scale[l];
         L.patch_size = (float)(int)(31 * t.scale[l]);   // :1013
     }
     g.ncells = (int)cells.size();
@@ -602,6 +603,111 @@ orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys
     }
     *n = k;
     return k > cap ? ORBX_ENOSPC : ORBX_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// search limits of ComputeStereoMatches (src/Frame.cc:676-681, mb from :140) and the
+// row-band half width that bounds every right keypoint's [floor(y-r), ceil(y+r)]
+void stereo_limits(const orbx_handle* h, float bf, float fx, float* maxD, int* rband)
+{
+    const float mb = bf / fx;
+    const float minZ = mb;
+    *maxD = bf / minZ;
+    float rmax = 0.f;
+    for (int l = 0; l < h->tab.nlevels; ++l) rmax = std::max(rmax, 2.0f * h->tab.scale[l]);
+    *rband = (int)std::ceil(rmax);
+}
+
+bool same_geometry(const orbx_handle* a, const orbx_handle* b)
+{
+    if (!a->geom_ok || !b->geom_ok || a->grows != b->grows || a->gcols != b->gcols) return false;
+    if (a->tab.nlevels != b->tab.nlevels) return false;
+    for (int l = 0; l < a->tab.nlevels; ++l)
+        if (a->tab.scale[l] != b->tab.scale[l]) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+orbx_status orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orbx_keypoint* kps_l,
+                                        const uint8_t* desc_l, int n_l, const orbx_keypoint* kps_r,
+                                        const uint8_t* desc_r, int n_r, float bf, float fx, float* u_right,
+                                        float* depth, int* n_good)
+{
+    if (!left || !right || !n_good || n_l < 0 || n_r < 0) return ORBX_EINVAL;
+    *n_good = 0;
+    if (n_l == 0) return ORBX_OK;   // Frame ctor returns before ComputeStereoMatches (src/Frame.cc:106-107)
+    if (!kps_l || !desc_l || !u_right || !depth || (n_r > 0 && (!kps_r || !desc_r))) return ORBX_EINVAL;
+    if (left->device != right->device || !same_geometry(left, right) || left->last_batch <= 0 ||
+        right->last_batch <= 0 || !(fx != 0.f) || !(bf != 0.f))
+        return ORBX_EINVAL;
+    const int cap = std::max(n_l, n_r);
+    if (cap > 32767) return ORBX_EINVAL;
+    hipSetDevice(left->device);
+    hipStream_t s = left->stream;
+    const size_t kb = sizeof(orbx_keypoint) * 2 * (size_t)cap, db = (size_t)64 * cap;
+    const size_t ob = sizeof(float) * (size_t)cap;
+    uint8_t* buf = nullptr;
+    const size_t total = kb + db + 3 * ob + 64;
+    if (hipMallocAsync((void**)&buf, total, s) != hipSuccess) return ORBX_ENOMEM;
+    orbx_keypoint* dk = (orbx_keypoint*)buf;
+    uint8_t* dd = buf + kb;
+    float* du = (float*)(dd + db);
+    float* dz = du + cap;
+    int* dsad = (int*)(dz + cap);
+    int* meta = (int*)(buf + kb + db + 3 * ob);   // counts[2], fl, fr, ngood
+    const int hmeta[5] = {n_l, n_r, 0, 1, 0};
+    hipMemcpyAsync(dk, kps_l, sizeof(orbx_keypoint) * n_l, hipMemcpyHostToDevice, s);
+    if (n_r > 0) hipMemcpyAsync(dk + cap, kps_r, sizeof(orbx_keypoint) * n_r, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(dd, desc_l, (size_t)32 * n_l, hipMemcpyHostToDevice, s);
+    if (n_r > 0) hipMemcpyAsync(dd + (size_t)32 * cap, desc_r, (size_t)32 * n_r, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(meta, hmeta, sizeof(hmeta), hipMemcpyHostToDevice, s);
+    // single images: frame strides 0, so frame indices 0 / 1 both address the handle's image
+    FramePtrs PL = left->last, PR = right->last;
+    PL.in_fstride = PL.pyr_fstride = 0;
+    PR.in_fstride = PR.pyr_fstride = 0;
+    float maxD;
+    int rband;
+    stereo_limits(left, bf, fx, &maxD, &rband);
+    launch_stereo(left->geom, left->d_geom, PL, PR, dk, dd, meta, cap, meta + 2, meta + 3, 1, bf, maxD, rband, du, dz,
+                  dsad, meta + 4, s);
+    orbx_status st = hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+    int ng = 0;
+    hipMemcpyAsync(u_right, du, sizeof(float) * n_l, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(depth, dz, sizeof(float) * n_l, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&ng, meta + 4, sizeof(int), hipMemcpyDeviceToHost, s);
+    hipFreeAsync(buf, s);
+    if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    *n_good = ng;
+    return st;
+}
+
+orbx_status orbx_stereo_batch_device(orbx_handle* h, const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                                     const int* d_counts, int cap, const int* d_left, const int* d_right, int npairs,
+                                     float bf, float fx, float* d_u_right, float* d_depth, int* d_n_good,
+                                     void* stream)
+{
+    if (!h || !d_kps || !d_desc || !d_counts || cap <= 0 || cap > 32767 || npairs < 0 || !d_left || !d_right ||
+        !d_u_right || !d_depth || !d_n_good || !(fx != 0.f) || !(bf != 0.f))
+        return ORBX_EINVAL;
+    if (!h->geom_ok || h->last_batch <= 0) return ORBX_EINVAL;
+    if (npairs == 0) return ORBX_OK;
+    hipSetDevice(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    int* dsad = nullptr;
+    if (hipMallocAsync((void**)&dsad, sizeof(int) * (size_t)npairs * cap, s) != hipSuccess) return ORBX_ENOMEM;
+    float maxD;
+    int rband;
+    stereo_limits(h, bf, fx, &maxD, &rband);
+    launch_stereo(h->geom, h->d_geom, h->last, h->last, d_kps, d_desc, d_counts, cap, d_left, d_right, npairs, bf,
+                  maxD, rband, d_u_right, d_depth, dsad, d_n_good, s);
+    hipFreeAsync(dsad, s);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b)

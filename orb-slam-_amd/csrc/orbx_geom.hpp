@@ -38,6 +38,7 @@ struct LevelGeom {
     float hX;                 // quadtree root width
     int qw, qh;               // maxX-minX, maxY-minY (quadtree frame)
     float scale;              // mvScaleFactor[l]
+    float inv_scale;          // mvInvScaleFactor[l]
     float patch_size;         // (float)(int)(PATCH_SIZE * scale)
 };
 

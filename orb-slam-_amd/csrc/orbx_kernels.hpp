@@ -65,4 +65,10 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
                         const int* pa, const int* pb, int npairs, int rows, int cols, int window, float nnratio,
                         int check_ori, void* scratch, int* m12, int* nm, hipStream_t s);
 
+size_t stereo_match_smem(const Geometry& g, int cap);
+void launch_stereo(const Geometry& g, const Geometry* d_geom, const FramePtrs& PL, const FramePtrs& PR,
+                   const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int cap, const int* fl,
+                   const int* fr, int npairs, float bf, float maxD, int rband, float* uright, float* depth, int* sad,
+                   int* ngood, hipStream_t s);
+
 }  // namespace orbx

@@ -34,7 +34,7 @@ EXPORTED = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_capacity", "orbx_extract", "orbx_get_level",
     "orbx_extract_batch_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
     "orbx_debug_pyramid", "orbx_debug_candidates", "orbm_descriptor_distance", "orbm_allpairs_device",
-    "orbm_search_init_batch_device",
+    "orbm_search_init_batch_device", "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
 ]
 
 
@@ -73,6 +73,10 @@ def _load():
     L.orbm_allpairs_device.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]
     L.orbm_search_init_batch_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int,
                                                 C.c_int, C.c_float, C.c_int, vp, vp, vp]
+    L.orbx_compute_stereo_matches.argtypes = [vp, vp, vp, u8p, C.c_int, vp, u8p, C.c_int, C.c_float, C.c_float,
+                                              f32p, f32p, i32p]
+    L.orbx_stereo_batch_device.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_float, C.c_float, vp, vp,
+                                           vp, vp]
     return L
 
 
@@ -195,6 +199,23 @@ class ORBextractor:
                                            _ptr(desc), _ptr(counts), cap, _stream(stream))
         _check("orbx_extract_batch_device", rc)
 
+    def stereo_batch_device(self, kps, desc, counts, left, right, bf, fx, u_right=None, depth=None, n_good=None,
+                            stream=None):
+        """Frame::ComputeStereoMatches on pairs (left[p], right[p]) of the last device batch.
+        Returns (u_right (P, cap) f32, depth (P, cap) f32, n_good (P,) i32) cuda tensors."""
+        import torch
+        npairs, cap = left.shape[0], kps.shape[1]
+        if u_right is None:
+            u_right = torch.empty((npairs, cap), dtype=torch.float32, device=kps.device)
+        if depth is None:
+            depth = torch.empty((npairs, cap), dtype=torch.float32, device=kps.device)
+        if n_good is None:
+            n_good = torch.empty((npairs,), dtype=torch.int32, device=kps.device)
+        rc = lib.orbx_stereo_batch_device(self._h, _ptr(kps), _ptr(desc), _ptr(counts), cap, _ptr(left), _ptr(right),
+                                          npairs, bf, fx, _ptr(u_right), _ptr(depth), _ptr(n_good), _stream(stream))
+        _check("orbx_stereo_batch_device", rc)
+        return u_right, depth, n_good
+
     def sync(self, stream=None):
         _check("orbx_sync", lib.orbx_sync(self._h, _stream(stream)))
 
@@ -223,6 +244,25 @@ class ORBextractor:
                                                                   out.ctypes.data_as(C.POINTER(C.c_int)), cap,
                                                                   C.byref(n)))
         return out[:n.value].copy()
+
+
+def compute_stereo_matches(left, right, kps_l, desc_l, kps_r, desc_r, bf, fx):
+    """Frame::ComputeStereoMatches (src/Frame.cc:630-872) for the host path: `left` / `right`
+    are the two ORBextractor objects right after extracting the left / right image.
+    Returns (mvuRight, mvDepth, n_good)."""
+    kl = np.ascontiguousarray(kps_l, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kps_r, KEYPOINT_DTYPE)
+    nl, nr = len(kl), len(kr)
+    dl = np.ascontiguousarray(desc_l if desc_l is not None else np.zeros((0, 32), np.uint8), np.uint8)
+    dr = np.ascontiguousarray(desc_r if desc_r is not None else np.zeros((0, 32), np.uint8), np.uint8)
+    ur = np.full(max(nl, 1), -1.0, np.float32)
+    dp = np.full(max(nl, 1), -1.0, np.float32)
+    ng = C.c_int(0)
+    f32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
+    _check("orbx_compute_stereo_matches",
+           lib.orbx_compute_stereo_matches(left._h, right._h, kl.ctypes.data, _u8(dl), nl, kr.ctypes.data, _u8(dr), nr,
+                                           bf, fx, f32(ur), f32(dp), C.byref(ng)))
+    return ur[:nl].copy(), dp[:nl].copy(), ng.value
 
 
 def keypoints_from_device(kps_i32, counts):
