@@ -69,3 +69,53 @@ class Gatherer:
         for w in dist.batch_isend_irecv(ops):
             w.wait()
         return [self.payload.buf] + self.recv if self.rank == 0 else None
+
+
+# ---- config 5: 10k x 10k brute-force Hamming sharded over ranks ----------------
+#
+# Targets are split into contiguous slices (shard_range); every rank computes the
+# (first-min index, best, second) triple of all queries against its slice, and
+# rank 0 merges the slices in rank order.  Merging in target order with a strict
+# `<` keeps the reference's first-min tie rule (src/ORBmatcher.cc:214-224): a
+# later slice only wins with a strictly smaller distance.
+
+def merge_top2(parts):
+    """parts: list (rank order) of (best_idx, best, second) int32 tensors, best_idx
+    already global (-1 for an empty slice).  Returns the merged triple."""
+    bi, b1, b2 = (p.clone() for p in parts[0])
+    for yi, y1, y2 in parts[1:]:
+        win = y1 < b1
+        nb2 = torch.where(win, torch.minimum(b1, y2), torch.minimum(b2, y1))
+        b1 = torch.where(win, y1, b1)
+        bi = torch.where(win, yi, bi)
+        b2 = nb2
+    return bi, b1, b2
+
+
+def sharded_top2(q, t, rank: int, world: int, top2_fn):
+    """This rank's slice of the all-pairs TOP2 search, gathered and merged on rank 0.
+
+    top2_fn(q, t_slice) -> (idx, best, second) is the device search (orbx.allpairs on
+    an MI355X).  Returns the merged triple on rank 0, None elsewhere."""
+    a, b = shard_range(t.shape[0], rank, world)
+    if b > a:
+        bi, b1, b2 = top2_fn(q, t[a:b])
+        bi = torch.where(bi >= 0, bi + a, bi)
+    else:
+        nq = q.shape[0]
+        bi = torch.full((nq,), -1, dtype=torch.int32, device=q.device)
+        b1 = torch.full((nq,), 256, dtype=torch.int32, device=q.device)
+        b2 = b1.clone()
+    mine = torch.stack([bi.to(torch.int32), b1.to(torch.int32), b2.to(torch.int32)])
+    if world == 1:
+        return bi, b1, b2
+    if rank == 0:
+        recv = [torch.empty_like(mine) for _ in range(world - 1)]
+        ops = [dist.P2POp(dist.irecv, recv[r - 1], r) for r in range(1, world)]
+    else:
+        ops = [dist.P2POp(dist.isend, mine, 0)]
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    if rank != 0:
+        return None
+    return merge_top2([(m[0], m[1], m[2]) for m in [mine] + recv])

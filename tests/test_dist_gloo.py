@@ -4,6 +4,7 @@ rank's padded {keypoints, descriptors, counts} payload intact."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -70,3 +71,50 @@ def test_shard_range_covers_frames():
                 a, b = orbx_dist.shard_range(n, r, world)
                 seen.extend(range(a, b))
             assert seen == list(range(n))
+
+
+def _np_top2(q, t):
+    x = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(axis=2).astype(np.int32)
+    bi = np.argmin(x, axis=1).astype(np.int32)                # first minimum
+    b1 = x[np.arange(len(q)), bi]
+    xs = x.copy()
+    xs[np.arange(len(q)), bi] = 1 << 20
+    b2 = xs.min(axis=1) if t.shape[0] > 1 else np.full(len(q), 256, np.int32)
+    return bi, b1, np.minimum(b2, 256).astype(np.int32)
+
+
+def _top2_worker(rank, world, port, nq, nt, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "orb-slam-_amd"))
+    import orbx_dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(55)
+        Q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+        T = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+        T[::7] = T[0]                       # duplicated targets: ties across slices
+        fn = lambda qq, tt: tuple(torch.from_numpy(a) for a in _np_top2(qq.numpy(), tt.numpy()))
+        out = orbx_dist.sharded_top2(torch.from_numpy(Q), torch.from_numpy(T), rank, world, fn)
+        if rank == 0:
+            want = _np_top2(Q, T)
+            q.put(all(np.array_equal(o.numpy(), w) for o, w in zip(out, want)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nt", [(2, 300), (4, 301), (4, 3)])
+def test_sharded_allpairs_top2(world, nt):
+    """Config 5 on G ranks: target slices + rank-0 merge == the single-device first-min top-2."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_top2_worker, args=(r, world, port, 50, nt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
