@@ -151,6 +151,61 @@ orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint
                                           int window, float nnratio, int check_ori,
                                           int* d_matches12, int* d_nmatches, void* stream);
 
+/* ---- Vocabulary-node searches (SearchByBoW x2, SearchForTriangulation) ----
+ * The candidate sets are the shared nodes of two DBoW2::FeatureVector maps
+ * (std::map<NodeId, vector<unsigned>>, Thirdparty/DBoW2/DBoW2/FeatureVector.h),
+ * passed as CSR: node ids ascending, the feature indices of node k at
+ * fv_idx[fv_ptr[k] .. fv_ptr[k+1]) in insertion order.  Nodes hold disjoint
+ * feature sets, so every shared node is one independent greedy search on the
+ * device; the rotation-consistency filter runs per pair afterwards. */
+typedef struct {
+    const orbx_keypoint* kps;   /* n keypoints: mvKeysUn (KeyFrame) or mvKeys (Frame) */
+    const uint8_t* desc;        /* n x 32 descriptors */
+    const uint8_t* has_mp;      /* n flags (see the modes below); NULL = all 0 */
+    const float* u_right;       /* n mvuRight values (triangulation); NULL = all -1 (monocular) */
+    const int32_t* fv_node;     /* [fv_nnodes] ascending node ids */
+    const int32_t* fv_ptr;      /* [fv_nnodes + 1] */
+    const int32_t* fv_idx;      /* [fv_ptr[fv_nnodes]] feature indices */
+    int32_t n;
+    int32_t fv_nnodes;
+} orbm_bow_view;
+
+enum {
+    /* ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, ...), src/ORBmatcher.cc:159-288.
+     * view1 = KF (has_mp = MapPoint present and !isBad), view2 = F.
+     * match[iF] = KF feature whose MapPoint is assigned to F feature iF, -1 none. */
+    ORBM_BOW_KF_F = 0,
+    /* ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, ...), :590-723.
+     * has_mp = MapPoint present and !isBad on both sides.  match[idx1] = idx2. */
+    ORBM_BOW_KF_KF = 1,
+    /* ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, ...), :725-891 (+ CheckDistEpipolarLine
+     * :140-157).  has_mp = GetMapPoint(idx) != NULL.  match[idx1] = idx2 (vMatchedPairs). */
+    ORBM_TRIANGULATION = 2
+};
+
+typedef struct {
+    float F12[9];        /* fundamental matrix KF1 -> KF2, row-major */
+    float ex, ey;        /* epipole of KF1's centre in KF2 (src/ORBmatcher.cc:731-736) */
+    float scale2[16];    /* KF2 mvScaleFactors */
+    float sigma2_2[16];  /* KF2 mvLevelSigma2 */
+    int32_t only_stereo; /* bOnlyStereo */
+} orbm_triang_params;
+
+/* Batched device path: `npairs` searches; d_view1 / d_view2 / d_tp are device arrays of
+ * the structs above whose pointers are device pointers (d_tp only for
+ * ORBM_TRIANGULATION).  max_nodes1 >= every view1 fv_nnodes; every view2.n <= 8192.  Outputs d_match[p *
+ * match_stride + i] (i < view2.n for ORBM_BOW_KF_F, view1.n otherwise) and
+ * d_nmatches[p].  nnratio = ORBmatcher::mfNNratio, check_ori = mbCheckOrientation.
+ * Asynchronous on `stream`. */
+orbx_status orbm_bow_search_device(int mode, const orbm_bow_view* d_view1, const orbm_bow_view* d_view2,
+                                   const orbm_triang_params* d_tp, int npairs, int max_nodes1, float nnratio,
+                                   int check_ori, int* d_match, int match_stride, int* d_nmatches, void* stream);
+
+/* Host path for one pair (host pointers in the views and tp), run on HIP device `device`.
+ * match: view2.n (ORBM_BOW_KF_F) or view1.n ints.  Synchronous. */
+orbx_status orbm_bow_search(int device, int mode, const orbm_bow_view* view1, const orbm_bow_view* view2,
+                            const orbm_triang_params* tp, float nnratio, int check_ori, int* match, int* nmatches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1032,3 +1032,205 @@ int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, co
     free(rcnt); free(ridx); free(rfill); free(vDistIdx);
     return good;
 }
+
+/* ---- a12 / a13: vocabulary-node candidate searches, src/ORBmatcher.cc ------
+ * DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>) as CSR: node ids
+ * ascending, ptr[k]..ptr[k+1] the feature indices of node k in insertion order.
+ * The merge-join over the two maps (:175-257) visits the shared node ids in
+ * ascending order. */
+static int fv_find(const orbref_featvec* f, int node, int from)
+{
+    int lo = from, hi = f->nnodes;   /* lower_bound */
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (f->node[mid] < node) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+static int rot_bin(float a1, float a2)
+{
+    const float factor = 1.0f / HISTO_LENGTH;
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == HISTO_LENGTH) bin = 0;
+    return bin;
+}
+
+/* rotation-consistency filter (:259-285 and twins): drop every match outside the three
+ * largest histogram bins.  match[] is indexed like bins[]; returns the matches removed. */
+static int rot_filter(const int* bins, int n, int* match)
+{
+    int hist[HISTO_LENGTH] = {0};
+    for (int i = 0; i < n; i++)
+        if (bins[i] >= 0) hist[bins[i]]++;
+    int a, b, c, removed = 0;
+    three_maxima(hist, &a, &b, &c);
+    for (int i = 0; i < n; i++) {
+        const int bin = bins[i];
+        if (bin < 0 || bin == a || bin == b || bin == c) continue;
+        match[i] = -1;
+        removed++;
+    }
+    return removed;
+}
+
+int orbref_search_by_bow_kf_f(const orbref_keypoint* kkf, const uint8_t* dkf, const uint8_t* kf_has_mp, int nkf,
+                              const orbref_featvec* fvkf, const orbref_keypoint* kf, const uint8_t* df, int nf,
+                              const orbref_featvec* fvf, float nnratio, int check_ori, int* match_f)
+{
+    /* src/ORBmatcher.cc:159-288 */
+    int* bins = (int*)malloc(sizeof(int) * ((size_t)nf + 1));
+    for (int i = 0; i < nf; i++) { match_f[i] = -1; bins[i] = -1; }
+    int nmatches = 0;
+    int ik = 0, jf = 0;
+    while (ik < fvkf->nnodes && jf < fvf->nnodes) {
+        const int nk = fvkf->node[ik], nfn = fvf->node[jf];
+        if (nk == nfn) {
+            for (int a = fvkf->ptr[ik]; a < fvkf->ptr[ik + 1]; a++) {
+                const int realIdxKF = fvkf->idx[a];
+                if (!kf_has_mp[realIdxKF]) continue;   /* !pMP || pMP->isBad() */
+                int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+                for (int b = fvf->ptr[jf]; b < fvf->ptr[jf + 1]; b++) {
+                    const int realIdxF = fvf->idx[b];
+                    if (match_f[realIdxF] >= 0) continue;
+                    const int dist = orbref_descriptor_distance(dkf + 32 * (size_t)realIdxKF, df + 32 * (size_t)realIdxF);
+                    if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdxF = realIdxF; }
+                    else if (dist < bestDist2) bestDist2 = dist;
+                }
+                if (bestDist1 <= TH_LOW && (float)bestDist1 < nnratio * (float)bestDist2) {
+                    match_f[bestIdxF] = realIdxKF;
+                    if (check_ori) bins[bestIdxF] = rot_bin(kkf[realIdxKF].angle, kf[bestIdxF].angle);
+                    nmatches++;
+                }
+            }
+            ik++;
+            jf++;
+        } else if (nk < nfn) {
+            ik = fv_find(fvkf, nfn, ik);
+        } else {
+            jf = fv_find(fvf, nk, jf);
+        }
+    }
+    if (check_ori) nmatches -= rot_filter(bins, nf, match_f);
+    free(bins);
+    return nmatches;
+}
+
+int orbref_search_by_bow_kf_kf(const orbref_keypoint* k1, const uint8_t* d1, const uint8_t* has_mp1, int n1,
+                               const orbref_featvec* fv1, const orbref_keypoint* k2, const uint8_t* d2,
+                               const uint8_t* has_mp2, int n2, const orbref_featvec* fv2, float nnratio,
+                               int check_ori, int* match12)
+{
+    /* src/ORBmatcher.cc:590-723 */
+    int* bins = (int*)malloc(sizeof(int) * ((size_t)n1 + 1));
+    uint8_t* matched2 = (uint8_t*)calloc((size_t)n2 + 1, 1);
+    for (int i = 0; i < n1; i++) { match12[i] = -1; bins[i] = -1; }
+    int nmatches = 0;
+    int i1 = 0, i2 = 0;
+    while (i1 < fv1->nnodes && i2 < fv2->nnodes) {
+        const int a1 = fv1->node[i1], a2 = fv2->node[i2];
+        if (a1 == a2) {
+            for (int a = fv1->ptr[i1]; a < fv1->ptr[i1 + 1]; a++) {
+                const int idx1 = fv1->idx[a];
+                if (!has_mp1[idx1]) continue;
+                int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+                for (int b = fv2->ptr[i2]; b < fv2->ptr[i2 + 1]; b++) {
+                    const int idx2 = fv2->idx[b];
+                    if (matched2[idx2] || !has_mp2[idx2]) continue;
+                    const int dist = orbref_descriptor_distance(d1 + 32 * (size_t)idx1, d2 + 32 * (size_t)idx2);
+                    if (dist < bestDist1) { bestDist2 = bestDist1; bestDist1 = dist; bestIdx2 = idx2; }
+                    else if (dist < bestDist2) bestDist2 = dist;
+                }
+                if (bestDist1 < TH_LOW && (float)bestDist1 < nnratio * (float)bestDist2) {   /* strict < (:666) */
+                    match12[idx1] = bestIdx2;
+                    matched2[bestIdx2] = 1;
+                    if (check_ori) bins[idx1] = rot_bin(k1[idx1].angle, k2[bestIdx2].angle);
+                    nmatches++;
+                }
+            }
+            i1++;
+            i2++;
+        } else if (a1 < a2) {
+            i1 = fv_find(fv1, a2, i1);
+        } else {
+            i2 = fv_find(fv2, a1, i2);
+        }
+    }
+    if (check_ori) nmatches -= rot_filter(bins, n1, match12);
+    free(bins);
+    free(matched2);
+    return nmatches;
+}
+
+/* CheckDistEpipolarLine (src/ORBmatcher.cc:140-157).  The reference is built with
+ * -O3 -march=native; GCC 11 contracts these expressions into the FMAs written here
+ * (verified on this host's g++ 11.4 at -march=x86-64-v3). */
+static int check_epipolar(const orbref_keypoint* kp1, const orbref_keypoint* kp2, const float* F, const float* sigma2)
+{
+    const float a = fmaf(kp1->x, F[0], kp1->y * F[3]) + F[6];
+    const float b = fmaf(kp1->x, F[1], kp1->y * F[4]) + F[7];
+    const float c = fmaf(kp1->y, F[5], kp1->x * F[2]) + F[8];
+    const float num = fmaf(b, kp2->y, a * kp2->x) + c;
+    const float den = fmaf(a, a, b * b);
+    if (den == 0) return 0;
+    const float dsqr = num * num / den;
+    return (double)dsqr < 3.84 * (double)sigma2[kp2->octave];
+}
+
+int orbref_search_for_triangulation(const orbref_keypoint* k1, const uint8_t* d1, const uint8_t* has_mp1,
+                                    const float* uright1, int n1, const orbref_featvec* fv1,
+                                    const orbref_keypoint* k2, const uint8_t* d2, const uint8_t* has_mp2,
+                                    const float* uright2, int n2, const orbref_featvec* fv2, const float* F12,
+                                    float ex, float ey, const float* scale2, const float* sigma2_2,
+                                    int only_stereo, int check_ori, int* match12)
+{
+    /* src/ORBmatcher.cc:725-891; vbMatched2 is never set, so every idx1 is independent */
+    int* bins = (int*)malloc(sizeof(int) * ((size_t)n1 + 1));
+    for (int i = 0; i < n1; i++) { match12[i] = -1; bins[i] = -1; }
+    int nmatches = 0;
+    int i1 = 0, i2 = 0;
+    while (i1 < fv1->nnodes && i2 < fv2->nnodes) {
+        const int a1 = fv1->node[i1], a2 = fv2->node[i2];
+        if (a1 == a2) {
+            for (int a = fv1->ptr[i1]; a < fv1->ptr[i1 + 1]; a++) {
+                const int idx1 = fv1->idx[a];
+                if (has_mp1[idx1]) continue;
+                const int bStereo1 = uright1[idx1] >= 0;
+                if (only_stereo && !bStereo1) continue;
+                const orbref_keypoint* kp1 = &k1[idx1];
+                int bestDist = TH_LOW, bestIdx2 = -1;
+                for (int b = fv2->ptr[i2]; b < fv2->ptr[i2 + 1]; b++) {
+                    const int idx2 = fv2->idx[b];
+                    if (has_mp2[idx2]) continue;   /* vbMatched2[idx2] is always false */
+                    const int bStereo2 = uright2[idx2] >= 0;
+                    if (only_stereo && !bStereo2) continue;
+                    const int dist = orbref_descriptor_distance(d1 + 32 * (size_t)idx1, d2 + 32 * (size_t)idx2);
+                    if (dist > TH_LOW || dist > bestDist) continue;
+                    const orbref_keypoint* kp2 = &k2[idx2];
+                    if (!bStereo1 && !bStereo2) {
+                        const float distex = ex - kp2->x;
+                        const float distey = ey - kp2->y;
+                        if (fmaf(distex, distex, distey * distey) < 100 * scale2[kp2->octave]) continue;
+                    }
+                    if (check_epipolar(kp1, kp2, F12, sigma2_2)) { bestIdx2 = idx2; bestDist = dist; }
+                }
+                if (bestIdx2 >= 0) {
+                    match12[idx1] = bestIdx2;
+                    nmatches++;
+                    if (check_ori) bins[idx1] = rot_bin(kp1->angle, k2[bestIdx2].angle);
+                }
+            }
+            i1++;
+            i2++;
+        } else if (a1 < a2) {
+            i1 = fv_find(fv1, a2, i1);
+        } else {
+            i2 = fv_find(fv2, a1, i2);
+        }
+    }
+    if (check_ori) nmatches -= rot_filter(bins, n1, match12);
+    free(bins);
+    return nmatches;
+}

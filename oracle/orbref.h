@@ -142,6 +142,40 @@ int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, co
                                   const orbref_keypoint* kR, const uint8_t* dR, int nR, float bf, float fx,
                                   float* uRight, float* depth, int* sad_out);
 
+/* DBoW2::FeatureVector as CSR: node ids ascending; the feature indices of node k are
+ * idx[ptr[k] .. ptr[k+1]) in insertion order (Thirdparty/DBoW2/DBoW2/FeatureVector.cpp:31-47). */
+typedef struct {
+    const int* node;
+    const int* ptr;
+    const int* idx;
+    int nnodes;
+} orbref_featvec;
+
+/* a13: ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches) (src/ORBmatcher.cc:159-288).
+ * kf_has_mp[i]: KF feature i has a MapPoint that is not bad.  match_f[iF] = the KF
+ * feature whose MapPoint was assigned (-1 none).  Returns nmatches. */
+int orbref_search_by_bow_kf_f(const orbref_keypoint* kkf, const uint8_t* dkf, const uint8_t* kf_has_mp, int nkf,
+                              const orbref_featvec* fvkf, const orbref_keypoint* kf, const uint8_t* df, int nf,
+                              const orbref_featvec* fvf, float nnratio, int check_ori, int* match_f);
+
+/* a13: ORBmatcher::SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12) (src/ORBmatcher.cc:590-723).
+ * match12[idx1] = idx2 whose MapPoint vpMatches12[idx1] receives (-1 none). */
+int orbref_search_by_bow_kf_kf(const orbref_keypoint* k1, const uint8_t* d1, const uint8_t* has_mp1, int n1,
+                               const orbref_featvec* fv1, const orbref_keypoint* k2, const uint8_t* d2,
+                               const uint8_t* has_mp2, int n2, const orbref_featvec* fv2, float nnratio,
+                               int check_ori, int* match12);
+
+/* a12: ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:725-891) + CheckDistEpipolarLine
+ * (:140-157).  F12 row-major 3x3, (ex, ey) the epipole of KF1 in KF2 (:733-740, computed by the
+ * caller), scale2 / sigma2_2 = KF2's mvScaleFactors / mvLevelSigma2.  match12[idx1] = idx2
+ * (vMatchedPairs in idx1 order).  Returns nmatches. */
+int orbref_search_for_triangulation(const orbref_keypoint* k1, const uint8_t* d1, const uint8_t* has_mp1,
+                                    const float* uright1, int n1, const orbref_featvec* fv1,
+                                    const orbref_keypoint* k2, const uint8_t* d2, const uint8_t* has_mp2,
+                                    const float* uright2, int n2, const orbref_featvec* fv2, const float* F12,
+                                    float ex, float ey, const float* scale2, const float* sigma2_2,
+                                    int only_stereo, int check_ori, int* match12);
+
 /* Config-5 brute force: per query best index (first min), best and second distance. */
 void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                           int* best_idx, int* best_d, int* second_d);

@@ -34,6 +34,11 @@ class Tables(C.Structure):
                 ("nfeat_level", C.c_int * MAX_LEVELS), ("umax", C.c_int * 16)]
 
 
+class FeatVec(C.Structure):
+    _fields_ = [("node", C.POINTER(C.c_int)), ("ptr", C.POINTER(C.c_int)), ("idx", C.POINTER(C.c_int)),
+                ("nnodes", C.c_int)]
+
+
 def build(force: bool = False) -> str:
     if force or not os.path.exists(_LIB_PATH):
         subprocess.check_call(["make", "-s", "-C", _HERE])
@@ -70,6 +75,14 @@ def lib():
         L.orbref_compute_stereo_matches.argtypes = [P(Params), C.c_int, C.c_int, u8p, u8p, C.c_void_p, u8p,
                                                      C.c_int, C.c_void_p, u8p, C.c_int, C.c_float, C.c_float,
                                                      f32p, f32p, i32p]
+        FV = P(FeatVec)
+        L.orbref_search_by_bow_kf_f.argtypes = [C.c_void_p, u8p, u8p, C.c_int, FV, C.c_void_p, u8p, C.c_int, FV,
+                                                C.c_float, C.c_int, i32p]
+        L.orbref_search_by_bow_kf_kf.argtypes = [C.c_void_p, u8p, u8p, C.c_int, FV, C.c_void_p, u8p, u8p, C.c_int,
+                                                 FV, C.c_float, C.c_int, i32p]
+        L.orbref_search_for_triangulation.argtypes = [C.c_void_p, u8p, u8p, f32p, C.c_int, FV, C.c_void_p, u8p, u8p,
+                                                      f32p, C.c_int, FV, f32p, C.c_float, C.c_float, f32p, f32p,
+                                                      C.c_int, C.c_int, i32p]
         L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
         _lib = L
     return _lib
@@ -249,6 +262,60 @@ def compute_stereo_matches(p: Params, left: ExtractResult, right: ExtractResult,
     if good < 0:
         raise RuntimeError("orbref_compute_stereo_matches failed: %d" % good)
     return ur[:n].copy(), dp[:n].copy(), sd[:n].copy(), good
+
+
+def _fv(fv):
+    node, ptr, idx = (np.ascontiguousarray(a, np.int32) for a in fv)
+    f = FeatVec(_i32(node), _i32(ptr), _i32(idx), len(node))
+    f._keep = (node, ptr, idx)
+    return f
+
+
+def _kp(k):
+    return np.ascontiguousarray(k, KEYPOINT_DTYPE)
+
+
+def search_by_bow_kf_f(kkf, dkf, kf_has_mp, fvkf, kf, df, fvf, nnratio=0.7, check_ori=True):
+    """SearchByBoW(KeyFrame*, Frame&): returns (nmatches, match_f[nF] = KF index or -1)."""
+    kkf, kf = _kp(kkf), _kp(kf)
+    dkf, df = np.ascontiguousarray(dkf, np.uint8), np.ascontiguousarray(df, np.uint8)
+    mp = np.ascontiguousarray(kf_has_mp, np.uint8)
+    out = np.empty(max(len(kf), 1), np.int32)
+    a, b = _fv(fvkf), _fv(fvf)
+    n = lib().orbref_search_by_bow_kf_f(kkf.ctypes.data, _u8(dkf), _u8(mp), len(kkf), C.byref(a), kf.ctypes.data,
+                                        _u8(df), len(kf), C.byref(b), nnratio, 1 if check_ori else 0, _i32(out))
+    return n, out[:len(kf)].copy()
+
+
+def search_by_bow_kf_kf(k1, d1, mp1, fv1, k2, d2, mp2, fv2, nnratio=0.75, check_ori=True):
+    """SearchByBoW(KeyFrame*, KeyFrame*): returns (nmatches, match12[n1] = idx2 or -1)."""
+    k1, k2 = _kp(k1), _kp(k2)
+    d1, d2 = np.ascontiguousarray(d1, np.uint8), np.ascontiguousarray(d2, np.uint8)
+    m1, m2 = np.ascontiguousarray(mp1, np.uint8), np.ascontiguousarray(mp2, np.uint8)
+    out = np.empty(max(len(k1), 1), np.int32)
+    a, b = _fv(fv1), _fv(fv2)
+    n = lib().orbref_search_by_bow_kf_kf(k1.ctypes.data, _u8(d1), _u8(m1), len(k1), C.byref(a), k2.ctypes.data,
+                                         _u8(d2), _u8(m2), len(k2), C.byref(b), nnratio, 1 if check_ori else 0,
+                                         _i32(out))
+    return n, out[:len(k1)].copy()
+
+
+def search_for_triangulation(k1, d1, mp1, ur1, fv1, k2, d2, mp2, ur2, fv2, F12, ex, ey, scale2, sigma2_2,
+                             only_stereo=False, check_ori=True):
+    """SearchForTriangulation: returns (nmatches, match12[n1] = idx2 or -1)."""
+    k1, k2 = _kp(k1), _kp(k2)
+    d1, d2 = np.ascontiguousarray(d1, np.uint8), np.ascontiguousarray(d2, np.uint8)
+    m1, m2 = np.ascontiguousarray(mp1, np.uint8), np.ascontiguousarray(mp2, np.uint8)
+    u1, u2 = np.ascontiguousarray(ur1, np.float32), np.ascontiguousarray(ur2, np.float32)
+    F = np.ascontiguousarray(F12, np.float32).reshape(9)
+    s2, g2 = np.ascontiguousarray(scale2, np.float32), np.ascontiguousarray(sigma2_2, np.float32)
+    out = np.empty(max(len(k1), 1), np.int32)
+    a, b = _fv(fv1), _fv(fv2)
+    n = lib().orbref_search_for_triangulation(k1.ctypes.data, _u8(d1), _u8(m1), _f32(u1), len(k1), C.byref(a),
+                                              k2.ctypes.data, _u8(d2), _u8(m2), _f32(u2), len(k2), C.byref(b),
+                                              _f32(F), ex, ey, _f32(s2), _f32(g2), 1 if only_stereo else 0,
+                                              1 if check_ori else 0, _i32(out))
+    return n, out[:len(k1)].copy()
 
 
 def allpairs_top2(q: np.ndarray, t: np.ndarray):

@@ -710,6 +710,129 @@ orbx_status orbx_stereo_batch_device(orbx_handle* h, const orbx_keypoint* d_kps,
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
+orbx_status orbm_bow_search_device(int mode, const orbm_bow_view* d_view1, const orbm_bow_view* d_view2,
+                                   const orbm_triang_params* d_tp, int npairs, int max_nodes1, float nnratio,
+                                   int check_ori, int* d_match, int match_stride, int* d_nmatches, void* stream)
+{
+    if (mode < ORBM_BOW_KF_F || mode > ORBM_TRIANGULATION || !d_view1 || !d_view2 || npairs < 0 ||
+        max_nodes1 < 0 || !d_match || match_stride <= 0 || !d_nmatches || (mode == ORBM_TRIANGULATION && !d_tp))
+        return ORBX_EINVAL;
+    if (npairs == 0) return ORBX_OK;
+    hipStream_t s = (hipStream_t)stream;
+    int* bins = nullptr;
+    if (hipMallocAsync((void**)&bins, sizeof(int) * (size_t)npairs * match_stride, s) != hipSuccess)
+        return ORBX_ENOMEM;
+    launch_bow(mode, d_view1, d_view2, d_tp, npairs, max_nodes1, nnratio, check_ori, d_match, bins, match_stride,
+               d_nmatches, s);
+    hipFreeAsync(bins, s);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+}  // extern "C"
+
+namespace {
+
+// host view -> bytes staged in one device buffer; returns the device view
+struct BowStage {
+    std::vector<uint8_t> host;
+    size_t add(const void* p, size_t bytes)
+    {
+        const size_t o = (host.size() + 15) & ~(size_t)15;
+        host.resize(o + bytes);
+        if (bytes && p) std::memcpy(host.data() + o, p, bytes);
+        return o;
+    }
+};
+
+bool bow_view_ok(const orbm_bow_view* v)
+{
+    if (!v || v->n < 0 || v->fv_nnodes < 0 || v->n > 8192) return false;
+    if (v->n > 0 && (!v->kps || !v->desc)) return false;
+    if (v->fv_nnodes > 0 && (!v->fv_node || !v->fv_ptr || !v->fv_idx)) return false;
+    for (int k = 0; k < v->fv_nnodes; ++k) {
+        if (v->fv_ptr[k] > v->fv_ptr[k + 1] || (k > 0 && v->fv_node[k] <= v->fv_node[k - 1])) return false;
+        for (int j = v->fv_ptr[k]; j < v->fv_ptr[k + 1]; ++j)
+            if (v->fv_idx[j] < 0 || v->fv_idx[j] >= v->n) return false;
+    }
+    return v->fv_nnodes == 0 || v->fv_ptr[0] == 0;
+}
+
+// offsets of one staged view (device pointers are patched in after the upload)
+struct BowOffs {
+    size_t kps, desc, mp, ur, node, ptr, idx;
+    bool has_mp, has_ur;
+};
+
+BowOffs bow_stage(BowStage& st, const orbm_bow_view* v)
+{
+    BowOffs o;
+    o.kps = st.add(v->kps, sizeof(orbx_keypoint) * (size_t)v->n);
+    o.desc = st.add(v->desc, (size_t)32 * v->n);
+    o.has_mp = v->has_mp != nullptr;
+    o.has_ur = v->u_right != nullptr;
+    o.mp = o.has_mp ? st.add(v->has_mp, (size_t)v->n) : 0;
+    o.ur = o.has_ur ? st.add(v->u_right, sizeof(float) * (size_t)v->n) : 0;
+    o.node = st.add(v->fv_node, sizeof(int32_t) * (size_t)v->fv_nnodes);
+    o.ptr = st.add(v->fv_ptr, sizeof(int32_t) * ((size_t)v->fv_nnodes + 1));
+    o.idx = st.add(v->fv_idx, sizeof(int32_t) * (size_t)(v->fv_nnodes ? v->fv_ptr[v->fv_nnodes] : 0));
+    return o;
+}
+
+orbm_bow_view bow_device_view(uint8_t* base, const BowOffs& o, const orbm_bow_view* v)
+{
+    orbm_bow_view d = *v;
+    d.kps = (const orbx_keypoint*)(base + o.kps);
+    d.desc = base + o.desc;
+    d.has_mp = o.has_mp ? base + o.mp : nullptr;
+    d.u_right = o.has_ur ? (const float*)(base + o.ur) : nullptr;
+    d.fv_node = (const int32_t*)(base + o.node);
+    d.fv_ptr = (const int32_t*)(base + o.ptr);
+    d.fv_idx = (const int32_t*)(base + o.idx);
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+orbx_status orbm_bow_search(int device, int mode, const orbm_bow_view* view1, const orbm_bow_view* view2,
+                            const orbm_triang_params* tp, float nnratio, int check_ori, int* match, int* nmatches)
+{
+    if (mode < ORBM_BOW_KF_F || mode > ORBM_TRIANGULATION || !bow_view_ok(view1) || !bow_view_ok(view2) ||
+        !nmatches || (mode == ORBM_TRIANGULATION && !tp))
+        return ORBX_EINVAL;
+    const int nout = mode == ORBM_BOW_KF_F ? view2->n : view1->n;
+    if (nout > 0 && !match) return ORBX_EINVAL;
+    *nmatches = 0;
+    if (nout == 0) return ORBX_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
+    hipSetDevice(device);
+    BowStage st;
+    const BowOffs o1 = bow_stage(st, view1), o2 = bow_stage(st, view2);
+    const size_t ov = st.add(nullptr, 2 * sizeof(orbm_bow_view) + sizeof(orbm_triang_params));
+    const size_t om = st.add(nullptr, sizeof(int) * ((size_t)nout + 1));
+    uint8_t* d = nullptr;
+    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
+    orbm_bow_view dv[2] = {bow_device_view(d, o1, view1), bow_device_view(d, o2, view2)};
+    std::memcpy(st.host.data() + ov, dv, sizeof(dv));
+    if (tp) std::memcpy(st.host.data() + ov + sizeof(dv), tp, sizeof(*tp));
+    orbx_status rc = ORBX_OK;
+    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
+    if (rc == ORBX_OK) {
+        const orbm_bow_view* d1 = (const orbm_bow_view*)(d + ov);
+        const orbm_triang_params* dtp = (const orbm_triang_params*)(d + ov + sizeof(dv));
+        int* dm = (int*)(d + om);
+        rc = orbm_bow_search_device(mode, d1, d1 + 1, dtp, 1, view1->fv_nnodes, nnratio, check_ori, dm + 1, nout, dm,
+                                    nullptr);
+        if (rc == ORBX_OK && (hipMemcpy(match, dm + 1, sizeof(int) * (size_t)nout, hipMemcpyDeviceToHost) != hipSuccess ||
+                              hipMemcpy(nmatches, dm, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess))
+            rc = ORBX_EDEVICE;
+    }
+    hipFree(d);
+    return rc;
+}
+
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b)
 {
     int d = 0;

@@ -71,4 +71,8 @@ void launch_stereo(const Geometry& g, const Geometry* d_geom, const FramePtrs& P
                    const int* fr, int npairs, float bf, float maxD, int rband, float* uright, float* depth, int* sad,
                    int* ngood, hipStream_t s);
 
+void launch_bow(int mode, const orbm_bow_view* v1, const orbm_bow_view* v2, const orbm_triang_params* tp,
+                int npairs, int max_nodes1, float nnratio, int check_ori, int* match, int* bins, int stride,
+                int* nmatches, hipStream_t s);
+
 }  // namespace orbx

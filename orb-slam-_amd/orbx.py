@@ -35,13 +35,28 @@ EXPORTED = [
     "orbx_extract_batch_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
     "orbx_debug_pyramid", "orbx_debug_candidates", "orbm_descriptor_distance", "orbm_allpairs_device",
     "orbm_search_init_batch_device", "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
+    "orbm_bow_search_device", "orbm_bow_search",
 ]
+BOW_KF_F, BOW_KF_KF, TRIANGULATION = 0, 1, 2
 
 
 class OrbxError(RuntimeError):
     def __init__(self, fn, code):
         super().__init__("%s failed with status %d" % (fn, code))
         self.code = code
+
+
+class BowView(C.Structure):
+    """orbm_bow_view: one side of a vocabulary-node search (host or device pointers)."""
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("has_mp", C.c_void_p), ("u_right", C.c_void_p),
+                ("fv_node", C.c_void_p), ("fv_ptr", C.c_void_p), ("fv_idx", C.c_void_p), ("n", C.c_int32),
+                ("fv_nnodes", C.c_int32)]
+
+
+class TriangParams(C.Structure):
+    """orbm_triang_params (SearchForTriangulation geometry)."""
+    _fields_ = [("F12", C.c_float * 9), ("ex", C.c_float), ("ey", C.c_float), ("scale2", C.c_float * 16),
+                ("sigma2_2", C.c_float * 16), ("only_stereo", C.c_int32)]
 
 
 class _Params(C.Structure):
@@ -77,6 +92,10 @@ def _load():
                                               f32p, f32p, i32p]
     L.orbx_stereo_batch_device.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_float, C.c_float, vp, vp,
                                            vp, vp]
+    L.orbm_bow_search_device.argtypes = [C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, C.c_int, vp, C.c_int,
+                                         vp, vp]
+    L.orbm_bow_search.argtypes = [C.c_int, C.c_int, P(BowView), P(BowView), P(TriangParams), C.c_float, C.c_int,
+                                  i32p, i32p]
     return L
 
 
@@ -273,7 +292,12 @@ def keypoints_from_device(kps_i32, counts):
 
 
 class ORBmatcher:
-    """ORBmatcher Hamming searches (include/ORBmatcher.h:37-102)."""
+    """ORBmatcher Hamming searches (include/ORBmatcher.h:37-102).
+
+    SearchByBoW(KF, F) / SearchByBoW(KF1, KF2) / SearchForTriangulation take the
+    per-side arrays the reference reads from its KeyFrame/Frame objects:
+    (keypoints, descriptors, FeatureVector CSR (node, ptr, idx), MapPoint flags
+    and, for triangulation, mvuRight)."""
 
     TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
 
@@ -286,6 +310,25 @@ class ORBmatcher:
         a = np.ascontiguousarray(a, np.uint8)
         b = np.ascontiguousarray(b, np.uint8)
         return lib.orbm_descriptor_distance(_u8(a), _u8(b))
+
+    def SearchByBoW_KF_F(self, kf, f, device=0):
+        """kf = (kps, desc, fv, has_mp), f = (kps, desc, fv).  Returns (nmatches, match_f)."""
+        v1 = _host_view(kf[0], kf[1], kf[2], has_mp=kf[3])
+        v2 = _host_view(f[0], f[1], f[2])
+        return bow_search(BOW_KF_F, v1, v2, None, self.mfNNratio, self.mbCheckOrientation, device)
+
+    def SearchByBoW_KF_KF(self, kf1, kf2, device=0):
+        """kf = (kps, desc, fv, has_mp).  Returns (nmatches, match12)."""
+        v1 = _host_view(kf1[0], kf1[1], kf1[2], has_mp=kf1[3])
+        v2 = _host_view(kf2[0], kf2[1], kf2[2], has_mp=kf2[3])
+        return bow_search(BOW_KF_KF, v1, v2, None, self.mfNNratio, self.mbCheckOrientation, device)
+
+    def SearchForTriangulation(self, kf1, kf2, F12, ex, ey, scale2, sigma2_2, bOnlyStereo=False, device=0):
+        """kf = (kps, desc, fv, has_mp, u_right).  Returns (nmatches, match12)."""
+        v1 = _host_view(kf1[0], kf1[1], kf1[2], has_mp=kf1[3], u_right=kf1[4])
+        v2 = _host_view(kf2[0], kf2[1], kf2[2], has_mp=kf2[3], u_right=kf2[4])
+        tp = triang_params(F12, ex, ey, scale2, sigma2_2, bOnlyStereo)
+        return bow_search(TRIANGULATION, v1, v2, tp, self.mfNNratio, self.mbCheckOrientation, device)
 
     def search_for_initialization_batch(self, kps, desc, counts, pair_a, pair_b, rows, cols, window=100,
                                         matches12=None, nmatches=None, stream=None):
@@ -306,6 +349,50 @@ class ORBmatcher:
         return matches12, nmatches
 
 
+def _host_view(kps, desc, fv, has_mp=None, u_right=None):
+    keep = [np.ascontiguousarray(kps, KEYPOINT_DTYPE), np.ascontiguousarray(desc, np.uint8)]
+    node, ptr, idx = (np.ascontiguousarray(a, np.int32) for a in fv)
+    keep += [node, ptr, idx]
+    mp = ur = None
+    if has_mp is not None:
+        mp = np.ascontiguousarray(has_mp, np.uint8)
+        keep.append(mp)
+    if u_right is not None:
+        ur = np.ascontiguousarray(u_right, np.float32)
+        keep.append(ur)
+    v = BowView(keep[0].ctypes.data, keep[1].ctypes.data, mp.ctypes.data if mp is not None else None,
+                ur.ctypes.data if ur is not None else None, node.ctypes.data, ptr.ctypes.data, idx.ctypes.data,
+                len(keep[0]), len(node))
+    v._keep = keep
+    return v
+
+
+def triang_params(F12, ex, ey, scale2, sigma2_2, only_stereo=False):
+    tp = TriangParams()
+    tp.F12[:] = [float(x) for x in np.asarray(F12, np.float32).reshape(9)]
+    tp.ex, tp.ey = ex, ey
+    s2 = np.zeros(16, np.float32)
+    g2 = np.zeros(16, np.float32)
+    s2[:len(scale2)] = scale2
+    g2[:len(sigma2_2)] = sigma2_2
+    tp.scale2[:] = [float(x) for x in s2]
+    tp.sigma2_2[:] = [float(x) for x in g2]
+    tp.only_stereo = 1 if only_stereo else 0
+    return tp
+
+
+def bow_search(mode, view1, view2, tp=None, nnratio=0.6, check_ori=True, device=0):
+    """Host path of the vocabulary-node searches; view1/view2 from _host_view.  Returns (nmatches, match)."""
+    nout = view2.n if mode == BOW_KF_F else view1.n
+    out = np.full(max(nout, 1), -1, np.int32)
+    nm = C.c_int(0)
+    _check("orbm_bow_search", lib.orbm_bow_search(device, mode, C.byref(view1), C.byref(view2),
+                                                  C.byref(tp) if tp is not None else None, nnratio,
+                                                  1 if check_ori else 0, out.ctypes.data_as(C.POINTER(C.c_int)),
+                                                  C.byref(nm)))
+    return nm.value, out[:nout].copy()
+
+
 def allpairs(q, t, mode=TOP2, stream=None):
     """Config-5 brute force: q (nq,32), t (nt,32) uint8 cuda tensors."""
     import torch
@@ -321,3 +408,69 @@ def allpairs(q, t, mode=TOP2, stream=None):
     _check("orbm_allpairs_device", lib.orbm_allpairs_device(_ptr(q), nq, _ptr(t), nt, FULL_U16, None, None, None,
                                                             _ptr(full), _stream(stream)))
     return full
+
+
+class BowBatch:
+    """Device-resident batch of vocabulary-node searches (orbm_bow_search_device).
+
+    sides1 / sides2: lists (one entry per pair) of dicts with keys kps, desc, fv=(node, ptr,
+    idx) and optionally has_mp, u_right -- host numpy arrays, uploaded once; or `kps`/`desc`
+    may already be cuda tensors (e.g. a slice of an extract batch), used in place.
+    tps: list of TriangParams for TRIANGULATION."""
+
+    def __init__(self, mode, sides1, sides2, tps=None, device=0):
+        import torch
+        self.mode = mode
+        self.dev = torch.device("cuda", device)
+        self._keep = []
+        v1 = [self._view(s) for s in sides1]
+        v2 = [self._view(s) for s in sides2]
+        self.npairs = len(v1)
+        self.max_nodes1 = max([v.fv_nnodes for v in v1] + [0])
+        n_out = [(b.n if mode == BOW_KF_F else a.n) for a, b in zip(v1, v2)]
+        self.stride = max(n_out + [1])
+        self.d_v1 = self._upload_structs(v1, BowView)
+        self.d_v2 = self._upload_structs(v2, BowView)
+        self.d_tp = self._upload_structs(tps, TriangParams) if tps else None
+        self.match = torch.empty((self.npairs, self.stride), dtype=torch.int32, device=self.dev)
+        self.nmatches = torch.empty((self.npairs,), dtype=torch.int32, device=self.dev)
+
+    def _t(self, a, dtype):
+        import torch
+        if isinstance(a, torch.Tensor):
+            t = a.contiguous()
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)
+        self._keep.append(t)
+        return t.data_ptr()
+
+    def _view(self, s):
+        import torch
+        kps = s["kps"]
+        n = kps.shape[0] if isinstance(kps, torch.Tensor) else len(kps)
+        if not isinstance(kps, torch.Tensor):
+            kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE).view(np.int32).reshape(-1, 7)
+        node, ptr, idx = (np.ascontiguousarray(a, np.int32) for a in s["fv"])
+        return BowView(self._t(kps, None), self._t(s["desc"], None),
+                       self._t(np.ascontiguousarray(s["has_mp"], np.uint8), None) if s.get("has_mp") is not None
+                       else None,
+                       self._t(np.ascontiguousarray(s["u_right"], np.float32), None) if s.get("u_right") is not None
+                       else None,
+                       self._t(node, None), self._t(ptr, None), self._t(idx if len(idx) else np.zeros(1, np.int32),
+                                                                         None),
+                       n, len(node))
+
+    def _upload_structs(self, items, cls):
+        import torch
+        raw = b"".join(bytes(memoryview(x)) for x in items)
+        t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.dev)
+        self._keep.append(t)
+        return t
+
+    def run(self, nnratio=0.6, check_ori=True, stream=None):
+        rc = lib.orbm_bow_search_device(self.mode, _ptr(self.d_v1), _ptr(self.d_v2),
+                                        _ptr(self.d_tp) if self.d_tp is not None else None, self.npairs,
+                                        self.max_nodes1, nnratio, 1 if check_ori else 0, _ptr(self.match),
+                                        self.stride, _ptr(self.nmatches), _stream(stream))
+        _check("orbm_bow_search_device", rc)
+        return self.match, self.nmatches

@@ -85,3 +85,81 @@ def stereo_pair(seed: int = 3, width: int = 752, height: int = 480):
 def random_descriptors(n: int, seed: int) -> np.ndarray:
     rng = np.random.default_rng(seed)
     return rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+
+
+# ---- vocabulary-node candidate sets (SearchByBoW / SearchForTriangulation inputs) ----
+#
+# ORBvoc.txt is not in the reference and there is no network, so the
+# FeatureVectors are made by a small vocabulary trained here with DBoW2's recipe:
+# hierarchical k-medians in Hamming space with bit-majority centres (FORB::meanValue,
+# Thirdparty/DBoW2/DBoW2/FORB.cpp), nodes numbered breadth-first from root 0, and
+# TemplatedVocabulary::transform's descent (first child at the strictly smallest
+# distance) recording the ancestor `levelsup` levels above the leaf
+# (TemplatedVocabulary.h:1127-1259).
+
+def _ham_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    x = np.bitwise_xor(a[:, None, :], b[None, :, :])
+    return np.unpackbits(x, axis=2).sum(axis=2).astype(np.int32)
+
+
+class Vocabulary:
+    def __init__(self, k: int, L: int, centers: np.ndarray):
+        self.k, self.L = k, L
+        self.centers = centers            # [n_nodes, 32]; row 0 (root) unused
+
+    @staticmethod
+    def train(descs: np.ndarray, k: int = 10, L: int = 3, seed: int = 0, iters: int = 3) -> "Vocabulary":
+        rng = np.random.default_rng(seed)
+        n_nodes = sum(k ** d for d in range(L + 1))
+        centers = np.zeros((n_nodes, 32), np.uint8)
+        groups = {0: np.asarray(descs, np.uint8)}
+        first = 1
+        for depth in range(1, L + 1):
+            ngroups = {}
+            for parent in range(first - k ** (depth - 1), first):
+                d = groups.get(parent)
+                child0 = first + (parent - (first - k ** (depth - 1))) * k
+                if d is None or len(d) == 0:
+                    centers[child0:child0 + k] = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+                    continue
+                c = d[rng.choice(len(d), k, replace=len(d) < k)]
+                for _ in range(iters):
+                    lab = np.argmin(_ham_matrix(d, c), axis=1)
+                    for j in range(k):
+                        m = d[lab == j]
+                        if len(m):
+                            bits = np.unpackbits(m, axis=1).mean(axis=0) > 0.5   # bit majority
+                            c[j] = np.packbits(bits)
+                lab = np.argmin(_ham_matrix(d, c), axis=1)
+                centers[child0:child0 + k] = c
+                for j in range(k):
+                    ngroups[child0 + j] = d[lab == j]
+            groups = ngroups
+            first += k ** depth
+        return Vocabulary(k, L, centers)
+
+    def feature_vector(self, descs: np.ndarray, levelsup: int = 1):
+        """FeatureVector as CSR (node ids ascending, ptr, feature indices in insertion order)."""
+        descs = np.asarray(descs, np.uint8)
+        n = len(descs)
+        node = np.zeros(n, np.int64)
+        target_depth = self.L - levelsup
+        rec = np.zeros(n, np.int64)
+        first_child = np.full(n, 1, np.int64)   # root's first child
+        level_first = 1
+        for depth in range(1, self.L + 1):
+            kids = first_child[:, None] + np.arange(self.k)[None, :]
+            dist = np.unpackbits(np.bitwise_xor(descs[:, None, :], self.centers[kids]), axis=2).sum(axis=2)
+            node = kids[np.arange(n), np.argmin(dist, axis=1)]   # first strict minimum
+            if depth == target_depth:
+                rec = node.copy()
+            next_first = level_first + self.k ** depth
+            first_child = next_first + (node - level_first) * self.k
+            level_first = next_first
+        if target_depth <= 0:
+            rec = np.zeros(n, np.int64)
+        ids = np.unique(rec)
+        order = np.argsort(rec, kind="stable")
+        counts = np.array([(rec == i).sum() for i in ids], np.int64)
+        ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+        return ids.astype(np.int32), ptr, order.astype(np.int32)
