@@ -39,6 +39,7 @@ import orbx_synth  # noqa: E402
 
 BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+VALU_PEAK_GINST = 614.4   # 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction
 W, H, NFEAT, NLEVELS, SCALE, INI, MINTH = 1241, 376, 2000, 8, 1.2, 20, 7
 WINDOW, NNRATIO = 100, 0.9
 
@@ -93,6 +94,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64, help="frames per GPU per step")
     ap.add_argument("--pool", type=int, default=8, help="distinct batches resident per GPU (defeats L3 reuse)")
+    ap.add_argument("--streams", type=int, default=3, help="pipeline depth (batches in flight per GPU); "
+                    "GPU_MAX_HW_QUEUES=4 leaves 3 besides the default stream")
+    ap.add_argument("--iso-steps", type=int, default=3, help="untimed one-stream steps for roofline_isolated")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -110,39 +114,48 @@ def main():
     # synthetic KITTI replay: each rank owns its own contiguous block of the sequence
     seq = orbx_synth.kitti_sequence(B * nb, start=rank * B * nb)
     frames = torch.from_numpy(seq).to(dev)
-    ex = orbx.ORBextractor(NFEAT, SCALE, NLEVELS, INI, MINTH, device=local)
+    # P-deep pipeline: step k runs on stream k % P with its own extractor workspace and
+    # payload, so the latency-bound stages of one batch (quadtree, greedy matching) overlap
+    # the throughput-bound stages of the next; each stream stays in order
+    # (extract -> match -> gather).
+    P = max(1, args.streams)
+    exs = [orbx.ORBextractor(NFEAT, SCALE, NLEVELS, INI, MINTH, device=local) for _ in range(P)]
+    ex = exs[0]
     cap = ex.capacity(H, W)
-    payload = orbx_dist.Payload(B, cap, dev)
-    gatherer = orbx_dist.Gatherer(payload, world, rank)
+    payloads = [orbx_dist.Payload(B, cap, dev) for _ in range(P)]
+    gatherers = [orbx_dist.Gatherer(pl, world, rank) for pl in payloads]
     matcher = orbx.ORBmatcher(NNRATIO, True)
     pa = torch.arange(0, B - 1, dtype=torch.int32, device=dev)
     pb = torch.arange(1, B, dtype=torch.int32, device=dev)
-    m12 = torch.empty((B - 1, cap), dtype=torch.int32, device=dev)
-    nm = torch.empty((B - 1,), dtype=torch.int32, device=dev)
-    stream = torch.cuda.Stream(device=dev)   # one dedicated stream: extract -> match -> gather in order
-    torch.cuda.set_stream(stream)
+    m12 = [torch.empty((B - 1, cap), dtype=torch.int32, device=dev) for _ in range(P)]
+    nm = [torch.empty((B - 1,), dtype=torch.int32, device=dev) for _ in range(P)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(P)]
     ev_m = []
 
-    def step(k, timed=False):
+    def step(k, timed=False, j=None):
         base = (k % nb) * B
-        ex.extract_batch_device(frames[base:base + B], payload.kps, payload.desc, payload.counts, stream)
+        j = k % P if j is None else j
+        s, pl = streams[j], payloads[j]
+        exs[j].extract_batch_device(frames[base:base + B], pl.kps, pl.desc, pl.counts, s)
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        matcher.search_for_initialization_batch(payload.kps, payload.desc, payload.counts, pa, pb, H, W, WINDOW,
-                                                m12, nm, stream)
+            e0.record(s)
+        matcher.search_for_initialization_batch(pl.kps, pl.desc, pl.counts, pa, pb, H, W, WINDOW, m12[j], nm[j], s)
         if timed:
-            e1.record(stream)
+            e1.record(s)
             ev_m.append((e0, e1))
-        gatherer.gather()
+        with torch.cuda.stream(s):
+            gatherers[j].gather()
 
     for k in range(args.warmup):
         step(k)
-    ex.sync(stream)
+    for j in range(P):
+        exs[j].sync(streams[j])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ex.set_timing(True)
+    for e in exs:
+        e.set_timing(True)
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, timed=True)
@@ -150,15 +163,32 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    ex.sync(stream)   # raises on device-side overflow
+    for j in range(P):
+        exs[j].sync(streams[j])   # raises on device-side overflow
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-
-    stage_ms = ex.stage_times()                    # sums over the timed steps
+    payload = payloads[(args.warmup + args.steps - 1) % P]
+    nm = nm[(args.warmup + args.steps - 1) % P]
+    used = sorted({(args.warmup + k) % P for k in range(args.steps)})
+    stage_ms = sum(exs[j].stage_times() for j in used)   # sums over the timed steps (all streams)
     match_ms = sum(a.elapsed_time(b) for a, b in ev_m)
+
+    # isolated pass (after the timed region, not part of `value`): the same steps one at a
+    # time on one stream, so every kernel's duration is its own (roofline_isolated)
+    iso_stage, iso_match = None, None
+    if args.iso_steps > 0 and P > 1:
+        ev_m.clear()
+        exs[0].set_timing(True)
+        for k in range(args.iso_steps):
+            step(k, timed=True, j=0)
+        torch.cuda.synchronize()
+        exs[0].sync(streams[0])
+        iso_stage = exs[0].stage_times() / args.iso_steps
+        iso_match = sum(a.elapsed_time(b) for a, b in ev_m) / args.iso_steps
+
     counts = payload.counts.cpu().numpy()
     nmatch = nm.cpu().numpy()
 
@@ -192,24 +222,46 @@ def main():
         "describe": B * (sum(A) + kept * (4 + 60)),
         "match": (B - 1) * 2 * kept * 60,
     }
-    dom = max(stages, key=lambda k: stages[k])
-    launches = {"pyramid": NLEVELS - 1}.get(dom, 1)
-    t_launch = stages[dom] / launches * 1e-3
-    achieved = alg[dom] / launches / t_launch / 1e9
-    kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree",
-             "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
-    # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
-    # same command (tools/collect_pmc.sh -> tools/pmc_summary.py); null when absent
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            d = json.load(open(pmc))
-            if d.get("batch") == B:
-                parts = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"]}.get(dom, [kname])
-                traffic = int(sum(d["kernels"][k]["bytes_per_launch"] for k in parts))
-        except Exception:
-            traffic = None
+    def roofline(st):
+        dom = max(st, key=lambda k: st[k])
+        launches = {"pyramid": NLEVELS - 1}.get(dom, 1)
+        t_launch = st[dom] / launches * 1e-3
+        achieved = alg[dom] / launches / t_launch / 1e9
+        kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree",
+                 "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
+        # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
+        # same command (tools/collect_pmc.sh -> tools/pmc_summary.py); null when absent
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                d = json.load(open(pmc))
+                if d.get("batch") == B:
+                    parts = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"]}.get(dom, [kname])
+                    traffic = int(sum(d["kernels"][k]["bytes_per_launch"] for k in parts))
+            except Exception:
+                traffic = None
+        r = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+             "alg_bytes_per_launch": int(alg[dom] / launches), "launch_ms": round(t_launch * 1e3, 4)}
+        # the path is integer VALU work: issue rate of the same kernel against the VALU peak
+        # (256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction), instruction count from
+        # the committed SQ_INSTS_VALU pass (tools/gpu_sq.sh -> profiles/sq_counters.json)
+        sq = os.path.join(ROOT, "profiles", "sq_counters.json")
+        if os.path.exists(sq):
+            try:
+                d = json.load(open(sq))
+                if d.get("batch") == B:
+                    parts = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"]}.get(dom, [kname])
+                    per = d["per_dispatch_averages"]
+                    ins = sum(per[k]["SQ_INSTS_VALU"] for k in parts)
+                    rate = ins / t_launch / 1e9
+                    r["valu"] = {"insts_per_launch": int(ins), "achieved": round(rate, 1), "peak": VALU_PEAK_GINST,
+                                 "unit": "G wave-instr/s", "frac": round(rate / VALU_PEAK_GINST, 4)}
+            except Exception:
+                pass
+        return r
+
     out = {
         "metric": BASELINE["metric"],
         "value": round(value, 2),
@@ -224,16 +276,18 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded KITTI-like 1241x376 replay, orb-slam-_amd/orbx_synth.py)",
         "config": {"workload": "config2_kitti_1241x376_2000feat_8lv_s1.2_extract+SearchForInitialization",
-                   "frames_per_gpu_per_step": B, "parallelism": "frames sharded, gather to rank 0" if world > 1
+                   "frames_per_gpu_per_step": B, "batches_in_flight": P, "parallelism": "frames sharded, gather to rank 0" if world > 1
                    else "single GPU", "pairs_per_gpu_per_step": B - 1, "window": WINDOW},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stages.items()},
         "keypoints_per_frame": round(kept, 1),
         "matches_per_pair": round(float(nmatch.mean()), 1),
-        "roofline": {"bound": "hbm", "kernel": kname,
-                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "alg_bytes_per_launch": int(alg[dom] / launches)},
+        "roofline": roofline(stages),
     }
+    if iso_stage is not None:
+        iso = {"pyramid": float(iso_stage[0]), "fast": float(iso_stage[1]), "quadtree": float(iso_stage[2]),
+               "describe": float(iso_stage[3]), "match": iso_match}
+        out["stage_ms_isolated"] = {k: round(v, 4) for k, v in iso.items()}
+        out["roofline_isolated"] = roofline(iso)
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(seq, args.cpu_seconds)
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)

@@ -342,12 +342,21 @@ orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_key
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
-orbx_status status_from_device(orbx_handle* h)
+// The handle's own stream serves the synchronous host paths only.  It is created on
+// first use: device-batch users bring their own streams, and every idle stream would
+// still take one of the process's few hardware queues (GPU_MAX_HW_QUEUES).
+hipStream_t own_stream(orbx_handle* h)
+{
+    if (!h->stream) hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    return h->stream;
+}
+
+orbx_status status_from_device(orbx_handle* h, hipStream_t s)
 {
     int st = 0;
-    if (hipMemcpyAsync(&st, h->d_status, sizeof(int), hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+    if (hipMemcpyAsync(&st, h->d_status, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
         return ORBX_EDEVICE;
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBX_EDEVICE;
+    if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
     if (st & kStatusCapOverflow) return ORBX_ENOSPC;
     if (st) return ORBX_EDEVICE;
     return ORBX_OK;
@@ -375,10 +384,6 @@ orbx_status orbx_create(const orbx_params* params, int device, orbx_handle** out
     }
     h->device = device;
     hipSetDevice(device);
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete h;
-        return ORBX_EDEVICE;
-    }
     h->h_levels.resize(kMaxLevels);
     h->level_cached.assign(kMaxLevels, false);
     *out = h;
@@ -459,14 +464,14 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
             return ORBX_ENOMEM;
         h->single_cap = ocap;
     }
-    hipStream_t s = h->stream;
+    hipStream_t s = own_stream(h);
     hipMemcpy2DAsync(h->d_img, pitch, img, step, cols, rows, hipMemcpyHostToDevice, s);
     FramePtrs P{h->d_img, need, pitch, h->d_pyr, (size_t)h->geom.pyr_bytes};
     st = run_pipeline(h, P, 1, h->d_kps, h->d_desc, h->d_counts, ocap, s);
     if (st != ORBX_OK) return st;
     int n = 0;
     hipMemcpyAsync(&n, h->d_counts, sizeof(int), hipMemcpyDeviceToHost, s);
-    if ((st = status_from_device(h)) != ORBX_OK) return st;
+    if ((st = status_from_device(h, s)) != ORBX_OK) return st;
     if (n > cap) return ORBX_ENOSPC;
     if (n > 0) {
         hipMemcpyAsync(kps, h->d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, s);
@@ -493,8 +498,8 @@ orbx_status orbx_get_level(orbx_handle* h, int level, const uint8_t** data, int*
             src = h->last.pyr + L.pyr_off;
             sp = (size_t)L.pitch;
         }
-        if (hipMemcpy2DAsync(v.data(), L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
-            hipStreamSynchronize(h->stream) != hipSuccess)
+        if (hipMemcpy2DAsync(v.data(), L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, own_stream(h)) != hipSuccess ||
+            hipStreamSynchronize(own_stream(h)) != hipSuccess)
             return ORBX_EDEVICE;
         h->level_cached[level] = true;
     }
@@ -526,7 +531,7 @@ orbx_status orbx_sync(orbx_handle* h, void* stream)
     hipSetDevice(h->device);
     if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return ORBX_EDEVICE;
     if (!h->d_status) return ORBX_OK;
-    return status_from_device(h);
+    return status_from_device(h, (hipStream_t)stream);
 }
 
 orbx_status orbx_set_timing(orbx_handle* h, int enable)
@@ -570,10 +575,10 @@ orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t o
             src = h->last.pyr + (size_t)frame * h->last.pyr_fstride + L.pyr_off;
             sp = (size_t)L.pitch;
         }
-        hipMemcpy2DAsync(out + o, L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, h->stream);
+        hipMemcpy2DAsync(out + o, L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, own_stream(h));
         o += (size_t)L.w * L.h;
     }
-    return hipStreamSynchronize(h->stream) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+    return hipStreamSynchronize(own_stream(h)) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
 orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys, int cap, int* n)
@@ -584,10 +589,10 @@ orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys
     std::vector<int> cnt(g.ncells);
     std::vector<uint32_t> sl(g.slots_per_frame);
     hipMemcpyAsync(cnt.data(), h->d_cell_counts + (size_t)frame * g.ncells, sizeof(int) * g.ncells,
-                   hipMemcpyDeviceToHost, h->stream);
+                   hipMemcpyDeviceToHost, own_stream(h));
     hipMemcpyAsync(sl.data(), h->d_slots + (size_t)frame * g.slots_per_frame, sizeof(uint32_t) * g.slots_per_frame,
-                   hipMemcpyDeviceToHost, h->stream);
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return ORBX_EDEVICE;
+                   hipMemcpyDeviceToHost, own_stream(h));
+    if (hipStreamSynchronize(own_stream(h)) != hipSuccess) return ORBX_EDEVICE;
     const LevelGeom& L = g.lv[level];
     int k = 0;
     for (int c = L.cell_begin; c < L.cell_begin + L.ncells; ++c) {
@@ -649,7 +654,7 @@ orbx_status orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, c
     const int cap = std::max(n_l, n_r);
     if (cap > 32767) return ORBX_EINVAL;
     hipSetDevice(left->device);
-    hipStream_t s = left->stream;
+    hipStream_t s = own_stream(left);
     const size_t kb = sizeof(orbx_keypoint) * 2 * (size_t)cap, db = (size_t)64 * cap;
     const size_t ob = sizeof(float) * (size_t)cap;
     uint8_t* buf = nullptr;
