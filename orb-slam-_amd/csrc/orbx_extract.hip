@@ -130,68 +130,75 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
 // (src/ORBextractor.cc:982-987).  Survivors are emitted row-major, i.e. in
 // OpenCV's emission order.
 // ---------------------------------------------------------------------------
-// ROI tile row pitch (dword aligned, +1 dword of slack for the 8-byte realigning read)
-__host__ __device__ inline int fast_tile_pitch(int max_roi_w) { return ((max_roi_w + 3) & ~3) + 4; }
-// per-wave LDS: ROI tile + zero-bordered strength map of the detection window + the
+// The ROI tile holds every pixel x as the f16 pair (1024 + x, 1024 + 255 - x).  Integers in
+// [1024, 2048) are exact f16 values with unit spacing (bit pattern 0x6400 + value - 1024), so
+// packed f16 max/min/sub are exact integer ops on both polarities at once, and gfx950's
+// v_pk_maximum3_f16 / v_pk_minimum3_f16 take three operands: a 9-arc max of x is the
+// "brighter" arc value and, in the other half, 255 - the 9-arc min ("darker").
+typedef _Float16 fh2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ fh2 as_fh2(uint32_t u) { return __builtin_bit_cast(fh2, u); }
+__device__ __forceinline__ fh2 pmax2(fh2 a, fh2 b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ fh2 pmin2(fh2 a, fh2 b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ fh2 pmax3(fh2 a, fh2 b, fh2 c) { return pmax2(pmax2(a, b), c); }
+__device__ __forceinline__ fh2 pmin3(fh2 a, fh2 b, fh2 c) { return pmin2(pmin2(a, b), c); }
+__device__ __forceinline__ uint32_t fast_pack(uint32_t x) { return 0x64FF6400u + x - (x << 16); }
+
+// packed tile row pitch in dwords (pixels), a multiple of 4 for 16-byte LDS stores
+__host__ __device__ inline int fast_tile_pitch(int max_roi_w) { return (max_roi_w + 3) & ~3; }
+// per-wave LDS: packed ROI tile + zero-bordered strength map of the detection window + the
 // candidate list (u16 pixel indices)
 __host__ __device__ inline size_t fast_wave_bytes(int max_roi_w, int max_roi_h)
 {
-    const size_t tile = (size_t)max_roi_h * fast_tile_pitch(max_roi_w);
-    const size_t map = (size_t)(max_roi_h - 4) * (max_roi_w - 4);
+    const size_t tile = (size_t)4 * max_roi_h * fast_tile_pitch(max_roi_w);
+    const size_t map = (((size_t)(max_roi_h - 4) * (max_roi_w - 4)) + 3) & ~(size_t)3;
     const size_t list = 2 * (size_t)(max_roi_h - 6) * (max_roi_w - 6);
-    return (((tile + map + 15) & ~(size_t)15) + list + 15) & ~(size_t)15;
+    return (tile + map + list + 15) & ~(size_t)15;
 }
 
-__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
-__device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
-
-// s = max(A, -B) from the raw ring values: A = v - min over arcs of max(arc),
-// -B = max over arcs of min(arc) - v (arcs = the 16 cyclic runs of 9 ring pixels).
-__device__ __forceinline__ int fast_strength(const uint8_t* c, int st)
+// max(v - minMax, maxMin - v) over the 16 cyclic 9-arcs of the Bresenham ring
+__device__ __forceinline__ int fast_strength(const uint32_t* c, int tp)
 {
-    const int v = c[0];
-    int x[16];
-    x[0] = c[3 * st];
-    x[1] = c[3 * st + 1];
-    x[2] = c[2 * st + 2];
-    x[3] = c[st + 3];
-    x[4] = c[3];
-    x[5] = c[-st + 3];
-    x[6] = c[-2 * st + 2];
-    x[7] = c[-3 * st + 1];
-    x[8] = c[-3 * st];
-    x[9] = c[-3 * st - 1];
-    x[10] = c[-2 * st - 2];
-    x[11] = c[-st - 3];
-    x[12] = c[-3];
-    x[13] = c[st - 3];
-    x[14] = c[2 * st - 2];
-    x[15] = c[3 * st - 1];
-    int M3[16], m3[16];
+    fh2 x[16];
+    x[0] = as_fh2(c[3 * tp]);
+    x[1] = as_fh2(c[3 * tp + 1]);
+    x[2] = as_fh2(c[2 * tp + 2]);
+    x[3] = as_fh2(c[tp + 3]);
+    x[4] = as_fh2(c[3]);
+    x[5] = as_fh2(c[-tp + 3]);
+    x[6] = as_fh2(c[-2 * tp + 2]);
+    x[7] = as_fh2(c[-3 * tp + 1]);
+    x[8] = as_fh2(c[-3 * tp]);
+    x[9] = as_fh2(c[-3 * tp - 1]);
+    x[10] = as_fh2(c[-2 * tp - 2]);
+    x[11] = as_fh2(c[-tp - 3]);
+    x[12] = as_fh2(c[-3]);
+    x[13] = as_fh2(c[tp - 3]);
+    x[14] = as_fh2(c[2 * tp - 2]);
+    x[15] = as_fh2(c[3 * tp - 1]);
+    fh2 m3[16], a[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        M3[k] = max3i(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
-        m3[k] = min3i(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
-    }
-    int minMax = 255, maxMin = 0;
+    for (int k = 0; k < 16; ++k) m3[k] = pmax3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        minMax = min(minMax, max3i(M3[k], M3[(k + 3) & 15], M3[(k + 6) & 15]));
-        maxMin = max(maxMin, min3i(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]));
-    }
-    return max(v - minMax, maxMin - v);
+    for (int k = 0; k < 16; ++k) a[k] = pmax3(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]);
+    const fh2 b0 = pmin3(a[0], a[1], a[2]), b1 = pmin3(a[3], a[4], a[5]), b2 = pmin3(a[6], a[7], a[8]);
+    const fh2 b3 = pmin3(a[9], a[10], a[11]), b4 = pmin3(a[12], a[13], a[14]);
+    const fh2 mm = pmin3(pmin3(b0, b1, b2), pmin2(b3, b4), a[15]);   // (minMax, 255 - maxMin)
+    const fh2 d = as_fh2(c[0]) - mm;                                  // (v - minMax, maxMin - v)
+    const _Float16 sv = d.x > d.y ? d.x : d.y;
+    return (int)sv;
 }
 
 // Necessary condition for s > t: a 9-arc holds two consecutive compass points
 // (ring positions 0, 4, 8, 12), so some consecutive pair is brighter than v+t or
 // some pair is darker than v-t.
-__device__ __forceinline__ bool fast_compass(const uint8_t* c, int st, int t)
+__device__ __forceinline__ bool fast_compass(const uint32_t* c, int tp, int t)
 {
-    const int v = c[0];
-    const int a = c[3 * st], b = c[3], d = c[-3 * st], e = c[-3];
-    const int br = max(max(min(a, b), min(b, d)), max(min(d, e), min(e, a)));
-    const int dk = min(min(max(a, b), max(b, d)), min(max(d, e), max(e, a)));
-    return br > v + t || dk < v - t;
+    const fh2 a = as_fh2(c[3 * tp]), b = as_fh2(c[3]), d = as_fh2(c[-3 * tp]), e = as_fh2(c[-3]);
+    const fh2 m = pmax2(pmax3(pmin2(a, b), pmin2(b, d), pmin2(d, e)), pmin2(e, a));   // (br, 255 - dk)
+    const fh2 q = m - as_fh2(c[0]);                                                  // (br - v, v - dk)
+    const _Float16 tt = (_Float16)t;
+    return q.x > tt || q.y > tt;
 }
 
 __device__ __forceinline__ bool nms_keep(const uint8_t* m, int p, int W2, int t)
@@ -209,139 +216,225 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* m, int p, int W2, int t)
     return true;
 }
 
+// ROI bytes of one cell staged in registers: up to kFastLd aligned dword pairs per lane
+// (a 37x38 ROI is 6 passes of 64 lanes); bigger ROIs load their remainder synchronously.
+constexpr int kFastLd = 6;
+constexpr int kCellsPerWave = 3;   // cells per wave: the next cell's ROI loads fly under this one's passes
+
+struct FastPrefetch {
+    uint32_t lo[kFastLd], hi[kFastLd], sh[kFastLd];
+    int dst[kFastLd];
+};
+
+struct FastCellSrc {
+    const uint8_t* src;   // ROI origin
+    int pitch, nd, ntot;
+    float inv_nd;
+};
+
+__device__ __forceinline__ void fast_issue(const FastCellSrc& S, int i0, int lane, int tp, FastPrefetch& F)
+{
+#pragma unroll
+    for (int u = 0; u < kFastLd; ++u) {
+        const int i = i0 + u * 64 + lane;
+        F.dst[u] = -1;
+        if (i < S.ntot) {
+            const int r = (int)(((float)i + 0.5f) * S.inv_nd), k = i - __mul24(r, S.nd);
+            const uintptr_t a = (uintptr_t)(S.src + __mul24(r, S.pitch) + 4 * k);
+            const __attribute__((address_space(1))) uint32_t* ap =
+                (const __attribute__((address_space(1))) uint32_t*)(a & ~(uintptr_t)3);
+            F.lo[u] = ap[0];
+            F.hi[u] = ap[1];
+            F.sh[u] = (uint32_t)(a & 3);
+            F.dst[u] = __mul24(r, tp) + 4 * k;
+        }
+    }
+}
+
+__device__ __forceinline__ void fast_commit(const FastPrefetch& F, uint32_t* tile)
+{
+#pragma unroll
+    for (int u = 0; u < kFastLd; ++u) {
+        if (F.dst[u] < 0) continue;
+        const uint32_t w = __builtin_amdgcn_alignbyte(F.hi[u], F.lo[u], F.sh[u]);
+        uint4 q;
+        q.x = fast_pack(w & 0xFFu);
+        q.y = fast_pack((w >> 8) & 0xFFu);
+        q.z = fast_pack((w >> 16) & 0xFFu);
+        q.w = fast_pack(w >> 24);
+        *(uint4*)(tile + F.dst[u]) = q;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                     const Cell* __restrict__ cells,
                                                     uint32_t* __restrict__ slots,
                                                     int* __restrict__ cell_counts)
 {
-    // per-wave LDS sized from the geometry's largest cell ROI (more resident waves per CU)
+    // per-wave LDS sized from the geometry's largest cell ROI
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
     const int kTileP = fast_tile_pitch(G->max_roi_w);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
-    const int c = (lb - f * gridDim.x) * 4 + wave;
-    if (c >= G->ncells) return;   // wave-uniform; no block barriers below
-    const Cell C = cells[c];
-    int pitch;
-    const uint8_t* img = level_base(P, G, f, C.level, pitch);
-    uint8_t* tile = s_fast + (size_t)wave * fast_wave_bytes(G->max_roi_w, G->max_roi_h);
-    uint8_t* map = tile + (size_t)G->max_roi_h * kTileP;
-    uint16_t* list = (uint16_t*)(tile + (((size_t)G->max_roi_h * kTileP +
-                                          (size_t)(G->max_roi_h - 4) * (G->max_roi_w - 4) + 15) & ~(size_t)15));
-    const int rw = C.roi_w, rh = C.roi_h;
-    const int dw = rw - 6, dh = rh - 6;
-    int* out_count = cell_counts + (size_t)f * G->ncells + c;
-    if (dw <= 0 || dh <= 0) {
-        if (lane == 0) *out_count = 0;
-        return;
-    }
-    // ROI -> LDS as aligned dwords (alignbyte realigns rows of any pitch); the ROI
-    // ends >= 16 px before the level's right edge, so the 8-byte read stays in the row
-    const uint8_t* src = img + (size_t)C.roi_y0 * pitch + C.roi_x0;
-    const int nd = (rw + 3) >> 2;
-    for (int i = lane; i < rh * nd; i += 64) {
-        const int r = i / nd, k = i - r * nd;
-        const uintptr_t a = (uintptr_t)(src + (size_t)r * pitch + 4 * k);
-        const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
-        const uint32_t lo = ap[0], hi = ap[1];
-        *(uint32_t*)(tile + r * kTileP + 4 * k) = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3));
-    }
-    const int W2 = dw + 2;
-    for (int i = lane; i < W2 * (dh + 2); i += 64) map[i] = 0;
-    wave_lds_sync();
-
-    // Pass 1: compass filter at the lower of the two thresholds; survivors listed in
-    // row-major order.  Pass 2: exact strength of the listed pixels into the map; the
-    // list keeps those above the lower threshold (in place: a round writes at or
-    // before the entries it has read).  Only listed pixels can pass either NMS test.
+    const int c0 = ((lb - f * gridDim.x) * 4 + wave) * kCellsPerWave;
+    const int c1 = min(c0 + kCellsPerWave, G->ncells);
+    if (c0 >= c1) return;   // wave-uniform; no block barriers below
+    uint32_t* tile = (uint32_t*)(s_fast + (size_t)wave * fast_wave_bytes(G->max_roi_w, G->max_roi_h));
+    uint8_t* map = (uint8_t*)(tile + (size_t)G->max_roi_h * kTileP);
+    uint16_t* list = (uint16_t*)(map + ((((size_t)(G->max_roi_h - 4) * (G->max_roi_w - 4)) + 3) & ~(size_t)3));
     const int tq = min(G->ini_th, G->min_th);
-    const int npx = dw * dh;
-    const float inv_dw = 1.0f / (float)dw;   // exact row/col split for npx < 4096
-    int n1 = 0;
-    for (int k0 = 0; k0 < npx; k0 += 64) {
-        const int k = k0 + lane;
-        bool in = false;
-        if (k < npx) {
-            const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
-            in = fast_compass(tile + (ii + 3) * kTileP + (jj + 3), kTileP, tq);
-        }
-        const unsigned long long m = __ballot(in);
-        if (in) list[n1 + lanes_below(m)] = (uint16_t)k;
-        n1 += __popcll(m);
-    }
-    wave_lds_sync();
-    int n2 = 0;
-    for (int j0 = 0; j0 < n1; j0 += 64) {
-        const int j = j0 + lane;
-        bool in = false;
-        int k = 0;
-        if (j < n1) {
-            k = list[j];
-            const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
-            const int s = fast_strength(tile + (ii + 3) * kTileP + (jj + 3), kTileP);
-            in = s > tq;
-            if (in) map[(ii + 1) * W2 + jj + 1] = (uint8_t)s;
-        }
-        const unsigned long long m = __ballot(in);
-        if (in) list[n2 + lanes_below(m)] = (uint16_t)k;
-        n2 += __popcll(m);
-    }
-    wave_lds_sync();
 
-    // NMS at iniThFAST over the list; survivors remembered per round (rounds <= 57)
-    const int rounds = (n2 + 63) >> 6;
-    unsigned long long keepmask = 0;
-    int t = G->ini_th;
-    int kept = 0;
-    for (int r = 0; r < rounds; ++r) {
-        const int j = lane + (r << 6);
-        bool keep = false;
-        if (j < n2) {
-            const int k = list[j];
-            const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
-            keep = nms_keep(map, (ii + 1) * W2 + jj + 1, W2, t);
+    // ROI -> LDS: aligned dword loads (alignbyte realigns rows of any pitch; the ROI ends >= 16
+    // px before the level's right edge, so the 8-byte read stays in the row), 4 packed pixels
+    // per 16-byte LDS store.  The next cell's loads are issued before this cell's passes.
+    auto cell_src = [&](const Cell& C) {
+        FastCellSrc S;
+        int pitch;
+        const uint8_t* img = level_base(P, G, f, C.level, pitch);
+        S.src = img + (size_t)C.roi_y0 * pitch + C.roi_x0;
+        S.pitch = pitch;
+        S.nd = (C.roi_w + 3) >> 2;
+        S.ntot = C.roi_h * S.nd;
+        S.inv_nd = 1.0f / (float)S.nd;   // exact row split for ntot < 4096
+        return S;
+    };
+    Cell C = cells[c0];
+    FastCellSrc S = cell_src(C);
+    FastPrefetch F;
+    fast_issue(S, 0, lane, kTileP, F);
+
+#pragma unroll 1
+    for (int c = c0; c < c1; ++c) {
+        const int rw = C.roi_w, rh = C.roi_h;
+        const int dw = rw - 6, dh = rh - 6;
+        const Cell Cc = C;
+        fast_commit(F, tile);
+        for (int i0 = 64 * kFastLd; i0 < S.ntot; i0 += 64 * kFastLd) {   // ROIs beyond 6 passes
+            FastPrefetch R;
+            fast_issue(S, i0, lane, kTileP, R);
+            fast_commit(R, tile);
         }
-        keepmask |= (unsigned long long)keep << r;
-        kept += __popcll(__ballot(keep));
-    }
-    if (kept == 0) {   // src/ORBextractor.cc:982-987: retry the cell at minThFAST
-        t = G->min_th;
-        keepmask = 0;
+        const int W2 = dw + 2;
+        const int mapn = W2 * (dh + 2);
+        for (int i = lane; i < (mapn + 3) >> 2; i += 64) ((uint32_t*)map)[i] = 0u;
+        wave_lds_sync();
+        if (c + 1 < c1) {   // prefetch the next cell (registers only; lands under the passes below)
+            C = cells[c + 1];
+            S = cell_src(C);
+            fast_issue(S, 0, lane, kTileP, F);
+        }
+        int* out_count = cell_counts + (size_t)f * G->ncells + c;
+        if (dw <= 0 || dh <= 0) {
+            if (lane == 0) *out_count = 0;
+            wave_lds_sync();
+            continue;
+        }
+
+        // Pass 1: compass filter at the lower of the two thresholds; survivors listed in
+        // row-major order as (row << 8 | col).  A pass covers 64 / cw rows of cw = 32 or 64
+        // columns, so lanes map to pixels without divisions and ballot order is row-major.
+        // Pass 2: exact strength of the listed pixels into the map; the list keeps those
+        // above the lower threshold (in place: a round writes at or before the entries it
+        // has read).  Only listed pixels can pass either NMS test.
+        const int cw_shift = dw <= 32 ? 5 : 6;
+        const int col = lane & ((1 << cw_shift) - 1);
+        const int rstep = 64 >> cw_shift;
+        int row = lane >> cw_shift;
+        const uint32_t* tp = tile + __mul24(row + 3, kTileP) + col + 3;
+        const int tpstep = __mul24(rstep, kTileP);
+        int n1 = 0;
+        for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {   // two row steps per trip: more LDS reads in flight
+            const bool ina = col < dw && row < dh && fast_compass(tp, kTileP, tq);
+            const bool inb = col < dw && row + rstep < dh && fast_compass(tp + tpstep, kTileP, tq);
+            const unsigned long long ma = __ballot(ina), mb = __ballot(inb);
+            if (ina) list[n1 + lanes_below(ma)] = (uint16_t)((row << 8) | col);
+            n1 += __popcll(ma);
+            if (inb) list[n1 + lanes_below(mb)] = (uint16_t)(((row + rstep) << 8) | col);
+            n1 += __popcll(mb);
+            row += 2 * rstep;
+            tp += 2 * tpstep;
+        }
+        wave_lds_sync();
+        int n2 = 0;
+        for (int j0 = 0; j0 < n1; j0 += 128) {   // two list entries per lane per trip
+            const int ja = j0 + lane, jb = ja + 64;
+            int ka = 0, kb = 0, sa = 0, sb = 0;
+            if (ja < n1) {
+                ka = list[ja];
+                sa = fast_strength(tile + __mul24((ka >> 8) + 3, kTileP) + ((ka & 0xFF) + 3), kTileP);
+            }
+            if (jb < n1) {
+                kb = list[jb];
+                sb = fast_strength(tile + __mul24((kb >> 8) + 3, kTileP) + ((kb & 0xFF) + 3), kTileP);
+            }
+            const bool ina = ja < n1 && sa > tq, inb = jb < n1 && sb > tq;
+            if (ina) map[__mul24((ka >> 8) + 1, W2) + (ka & 0xFF) + 1] = (uint8_t)sa;
+            if (inb) map[__mul24((kb >> 8) + 1, W2) + (kb & 0xFF) + 1] = (uint8_t)sb;
+            const unsigned long long ma = __ballot(ina), mb = __ballot(inb);
+            wave_lds_sync();   // both entries are read before the compaction overwrites the list
+            if (ina) list[n2 + lanes_below(ma)] = (uint16_t)ka;
+            n2 += __popcll(ma);
+            if (inb) list[n2 + lanes_below(mb)] = (uint16_t)kb;
+            n2 += __popcll(mb);
+        }
+        wave_lds_sync();
+
+        // NMS at iniThFAST over the list; survivors remembered per round (rounds <= 57)
+        const int rounds = (n2 + 63) >> 6;
+        unsigned long long keepmask = 0;
+        int t = G->ini_th;
+        int kept = 0;
         for (int r = 0; r < rounds; ++r) {
             const int j = lane + (r << 6);
             bool keep = false;
             if (j < n2) {
                 const int k = list[j];
-                const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
-                keep = nms_keep(map, (ii + 1) * W2 + jj + 1, W2, t);
+                keep = nms_keep(map, __mul24((k >> 8) + 1, W2) + (k & 0xFF) + 1, W2, t);
             }
             keepmask |= (unsigned long long)keep << r;
+            kept += __popcll(__ballot(keep));
         }
-    }
+        if (kept == 0) {   // src/ORBextractor.cc:982-987: retry the cell at minThFAST
+            t = G->min_th;
+            keepmask = 0;
+            for (int r = 0; r < rounds; ++r) {
+                const int j = lane + (r << 6);
+                bool keep = false;
+                if (j < n2) {
+                    const int k = list[j];
+                    keep = nms_keep(map, __mul24((k >> 8) + 1, W2) + (k & 0xFF) + 1, W2, t);
+                }
+                keepmask |= (unsigned long long)keep << r;
+            }
+        }
 
-    uint32_t* out = slots + (size_t)f * G->slots_per_frame + C.slot_base;
-    const int xr0 = C.roi_x0 + 3 - kMinBorder, yr0 = C.roi_y0 + 3 - kMinBorder;
-    int base = 0;
-    for (int r = 0; r < rounds; ++r) {
-        const bool keep = (keepmask >> r) & 1ull;
-        const unsigned long long m = __ballot(keep);
-        if (keep) {
-            const int k = list[lane + (r << 6)];
-            const int ii = (int)(((float)k + 0.5f) * inv_dw), jj = k - ii * dw;
-            const int idx = base + lanes_below(m);
-            out[idx] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + ii),
-                               (uint32_t)(map[(ii + 1) * W2 + jj + 1] - 1));
+        uint32_t* out = slots + (size_t)f * G->slots_per_frame + Cc.slot_base;
+        const int xr0 = Cc.roi_x0 + 3 - kMinBorder, yr0 = Cc.roi_y0 + 3 - kMinBorder;
+        int base = 0;
+        for (int r = 0; r < rounds; ++r) {
+            const bool keep = (keepmask >> r) & 1ull;
+            const unsigned long long m = __ballot(keep);
+            if (keep) {
+                const int k = list[lane + (r << 6)];
+                const int ii = k >> 8, jj = k & 0xFF;
+                const int idx = base + lanes_below(m);
+                out[idx] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + ii),
+                                   (uint32_t)(map[__mul24(ii + 1, W2) + jj + 1] - 1));
+            }
+            base += __popcll(m);
         }
-        base += __popcll(m);
+        if (lane == 0) *out_count = base;
+        wave_lds_sync();   // tile, map and list are rewritten by the next cell
     }
-    if (lane == 0) *out_count = base;
 }
 
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
-    dim3 grid((g.ncells + 3) / 4, batch);
+    const int per_block = 4 * kCellsPerWave;
+    dim3 grid((g.ncells + per_block - 1) / per_block, batch);
     const size_t smem = 4 * fast_wave_bytes(g.max_roi_w, g.max_roi_h);
+    hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts);
 }
 
@@ -842,11 +935,15 @@ __device__ __forceinline__ int reflect101(int p, int len)
     return p;
 }
 
+// wave sum: row (16-lane) sums with DPP, then the four rows by readlane (all lanes active)
 __device__ __forceinline__ int wave_sum(int v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true);   // row_half_mirror
+    v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true);   // row_mirror
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+           __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
 }
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
