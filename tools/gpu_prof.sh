@@ -3,7 +3,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=${1:-p}
-B=${2:-64}
+B=${2:-192}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/kt_$TAG -o run -- python3 $R/bench.py --batch $B --steps 10 --warmup 2 --no-cpu > $R/gpurun_out/kt_$TAG.json 2> $R/gpurun_out/kt_$TAG.err || { echo PROF_FAIL; tail -20 $R/gpurun_out/kt_$TAG.err; exit 1; }
 python3 - $R/gpurun_out/kt_$TAG/run_kernel_stats.csv <<'EOF'

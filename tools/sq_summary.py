@@ -7,6 +7,7 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
+save = sys.argv[sys.argv.index("--save") + 1] if "--save" in sys.argv else None
 vals = defaultdict(lambda: defaultdict(list))
 for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(fn)):
@@ -25,3 +26,15 @@ for k, c in sorted(vals.items()):
                                     avg.get("SQ_INSTS_SALU", 0) / w, avg.get("SQ_WAIT_ANY", 0) / max(wc, 1),
                                     avg.get("SQ_WAIT_INST_ANY", 0) / max(wc, 1),
                                     avg.get("SQ_ACTIVE_INST_VALU", 0) / max(wc, 1)))
+
+if save:
+    import json
+    out = {}
+    for k, c in vals.items():
+        if k.startswith("k_"):
+            out[k] = {n: sum(v) / len(v) for n, v in c.items()}
+            out[k]["dispatches"] = len(next(iter(c.values())))
+    json.dump({"batch": 192, "source": "rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU "
+               "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -- python3 bench.py --steps 3 "
+               "--warmup 1 --no-cpu --streams 1 --iso-steps 0 (tools/gpu_sq.sh)", "per_dispatch_averages": out},
+              open(save, "w"), indent=1)
