@@ -206,6 +206,42 @@ orbx_status orbm_bow_search_device(int mode, const orbm_bow_view* d_view1, const
 orbx_status orbm_bow_search(int device, int mode, const orbm_bow_view* view1, const orbm_bow_view* view2,
                             const orbm_triang_params* tp, float nnratio, int check_ori, int* match, int* nmatches);
 
+/* ---- DBoW2 vocabulary (TemplatedVocabulary, Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) ----
+ * Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:521-528, src/KeyFrame.cc:59-66) call
+ * transform(descriptors, mBowVec, mFeatVec, 4); the FeatureVector it produces is the
+ * candidate set of the SearchByBoW / SearchForTriangulation entry points above. */
+typedef struct orbx_vocabulary orbx_vocabulary;
+
+/* TemplatedVocabulary::loadFromTextFile (:1338-1424): header "k L scoring weighting", then one
+ * node per line "parent is_leaf d0 .. d31 weight" (node ids 1, 2, ... in file order). */
+orbx_status orbv_load_text(const char* path, int device, orbx_vocabulary** out);
+
+/* The same vocabulary from arrays: nnodes entries including the root (index 0, whose
+ * parent / is_leaf / descriptor / weight are ignored); parent[i] < i. */
+orbx_status orbv_create(int k, int L, int scoring, int weighting, int nnodes, const int32_t* parent,
+                        const uint8_t* is_leaf, const uint8_t* desc, const double* weight, int device,
+                        orbx_vocabulary** out);
+void orbv_destroy(orbx_vocabulary* v);
+orbx_status orbv_info(const orbx_vocabulary* v, int* k, int* L, int* scoring, int* weighting, int* nnodes,
+                      int* nwords);
+
+/* TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup) (:1125-1259) for
+ * one host descriptor set (n <= 8192).  BowVector: bow_n words ascending with their weights
+ * (n entries of room); FeatureVector as CSR: fv_nnodes node ids ascending, fv_ptr (n + 1),
+ * fv_idx (n).  Synchronous. */
+orbx_status orbv_transform(const orbx_vocabulary* v, const uint8_t* desc, int n, int levelsup, int32_t* bow_word,
+                           double* bow_weight, int* bow_n, int32_t* fv_node, int32_t* fv_ptr, int32_t* fv_idx,
+                           int* fv_nnodes);
+
+/* Batched device path over an extract batch (d_desc [nframes][cap][32], d_counts[nframes],
+ * cap <= 8192).  Per frame f: d_bow_word / d_bow_weight / d_fv_node / d_fv_idx at f * cap,
+ * d_fv_ptr at f * (cap + 1), counts d_bow_n[f] / d_fv_nnodes[f].  The FeatureVector CSR
+ * plugs straight into orbm_bow_view.  Asynchronous on `stream`. */
+orbx_status orbv_transform_batch_device(const orbx_vocabulary* v, const uint8_t* d_desc, const int* d_counts,
+                                        int nframes, int cap, int levelsup, int32_t* d_bow_word,
+                                        double* d_bow_weight, int* d_bow_n, int32_t* d_fv_node, int32_t* d_fv_ptr,
+                                        int32_t* d_fv_idx, int* d_fv_nnodes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1234,3 +1234,116 @@ int orbref_search_for_triangulation(const orbref_keypoint* k1, const uint8_t* d1
     free(bins);
     return nmatches;
 }
+
+/* ---- §8f row 2: DBoW2 TemplatedVocabulary::transform ---------------------
+ * Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1125-1259 (transform of a feature
+ * set and of one feature), BowVector.cpp:34-84 (addWeight / addIfNotExist /
+ * normalize), FeatureVector.cpp:31-45 (addFeature).  Nodes: node 0 is the root;
+ * node i > 0 has parent[i], a file leaf flag and a weight; the children of a node
+ * are the nodes naming it as parent, in id order (loadFromTextFile :1378-1386).
+ * isLeaf() is "no children" (:328); word ids number the flagged leaves in id order. */
+int orbref_voc_transform(int nnodes, const int* parent, const uint8_t* is_leaf_flag, const uint8_t* desc,
+                         const double* weight, int L, int scoring, int weighting, const uint8_t* feats, int n,
+                         int levelsup, int* bow_word, double* bow_weight, int* bow_n, int* fv_node, int* fv_ptr,
+                         int* fv_idx, int* fv_nnodes)
+{
+    if (nnodes < 2) { *bow_n = 0; *fv_nnodes = 0; fv_ptr[0] = 0; return 0; }
+    int* ccount = (int*)calloc((size_t)nnodes, sizeof(int));
+    int* cbegin = (int*)calloc((size_t)nnodes + 1, sizeof(int));
+    int* child = (int*)malloc(sizeof(int) * (size_t)nnodes);
+    int* word_of = (int*)calloc((size_t)nnodes, sizeof(int));
+    for (int i = 1; i < nnodes; i++) ccount[parent[i]]++;
+    for (int i = 0; i < nnodes; i++) cbegin[i + 1] = cbegin[i] + ccount[i];
+    int* fill = (int*)calloc((size_t)nnodes, sizeof(int));
+    int nwords = 0;
+    for (int i = 1; i < nnodes; i++) {
+        child[cbegin[parent[i]] + fill[parent[i]]++] = i;
+        if (is_leaf_flag[i]) word_of[i] = nwords++;
+    }
+    /* scoring -> mustNormalize (ScoringObject.h:74-89) */
+    const int must = scoring != 5;               /* DOT_PRODUCT does not normalise */
+    const int l2 = scoring == 1;                 /* L2_NORM; the others normalise with L1 */
+    const int nid_level = L - levelsup;
+    int* wid = (int*)malloc(sizeof(int) * ((size_t)n + 1));
+    int* nid = (int*)malloc(sizeof(int) * ((size_t)n + 1));
+    double* w = (double*)malloc(sizeof(double) * ((size_t)n + 1));
+    for (int f = 0; f < n; f++) {
+        const uint8_t* d = feats + 32 * (size_t)f;
+        int final_id = 0, level = 0, nd = 0;
+        do {   /* :1224-1248 */
+            ++level;
+            const int c0 = cbegin[final_id], c1 = cbegin[final_id + 1];
+            final_id = child[c0];
+            double best_d = (double)orbref_descriptor_distance(d, desc + 32 * (size_t)final_id);
+            for (int c = c0 + 1; c < c1; c++) {
+                const int id = child[c];
+                const double dd = (double)orbref_descriptor_distance(d, desc + 32 * (size_t)id);
+                if (dd < best_d) { best_d = dd; final_id = id; }
+            }
+            if (level == nid_level) nd = final_id;
+        } while (ccount[final_id] > 0);
+        if (nid_level <= 0) nd = 0;
+        else if (level < nid_level) nd = final_id;   /* unset in the reference (leaf above nid_level) */
+        wid[f] = word_of[final_id];
+        w[f] = weight[final_id];
+        nid[f] = nd;
+    }
+    /* BowVector (std::map by word id) and FeatureVector (std::map by node id) */
+    int nb = 0, nf = 0;
+    for (int f = 0; f < n; f++) {
+        if (!(w[f] > 0)) continue;   /* stopped word */
+        /* BowVector: lower_bound insert */
+        int lo = 0, hi = nb;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (bow_word[mid] < wid[f]) lo = mid + 1; else hi = mid; }
+        if (lo < nb && bow_word[lo] == wid[f]) {
+            if (weighting == 0 || weighting == 1) bow_weight[lo] += w[f];   /* addWeight; IDF/BINARY: addIfNotExist */
+        } else {
+            memmove(bow_word + lo + 1, bow_word + lo, sizeof(int) * (size_t)(nb - lo));
+            memmove(bow_weight + lo + 1, bow_weight + lo, sizeof(double) * (size_t)(nb - lo));
+            bow_word[lo] = wid[f];
+            bow_weight[lo] = w[f];
+            nb++;
+        }
+        /* FeatureVector: node list, each with its features in insertion order */
+        lo = 0; hi = nf;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (fv_node[mid] < nid[f]) lo = mid + 1; else hi = mid; }
+        if (!(lo < nf && fv_node[lo] == nid[f])) {
+            memmove(fv_node + lo + 1, fv_node + lo, sizeof(int) * (size_t)(nf - lo));
+            fv_node[lo] = nid[f];
+            nf++;
+        }
+    }
+    /* CSR of the FeatureVector: features in index order within each node */
+    for (int k = 0; k <= nf; k++) fv_ptr[k] = 0;
+    for (int f = 0; f < n; f++) {
+        if (!(w[f] > 0)) continue;
+        int lo = 0, hi = nf;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (fv_node[mid] < nid[f]) lo = mid + 1; else hi = mid; }
+        fv_ptr[lo + 1]++;
+    }
+    for (int k = 0; k < nf; k++) fv_ptr[k + 1] += fv_ptr[k];
+    int* pos = (int*)calloc((size_t)nf + 1, sizeof(int));
+    for (int f = 0; f < n; f++) {
+        if (!(w[f] > 0)) continue;
+        int lo = 0, hi = nf;
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (fv_node[mid] < nid[f]) lo = mid + 1; else hi = mid; }
+        fv_idx[fv_ptr[lo] + pos[lo]++] = f;
+    }
+    if (weighting == 0 || weighting == 1) {
+        if (nb > 0 && !must) {   /* :1155-1161 */
+            const double ndd = (double)nb;
+            for (int i = 0; i < nb; i++) bow_weight[i] /= ndd;
+        }
+    }
+    if (must) {   /* BowVector::normalize, BowVector.cpp:62-84 */
+        double norm = 0.0;
+        if (!l2) { for (int i = 0; i < nb; i++) norm += fabs(bow_weight[i]); }
+        else { for (int i = 0; i < nb; i++) norm += bow_weight[i] * bow_weight[i]; norm = sqrt(norm); }
+        if (norm > 0.0)
+            for (int i = 0; i < nb; i++) bow_weight[i] /= norm;
+    }
+    *bow_n = nb;
+    *fv_nnodes = nf;
+    free(ccount); free(cbegin); free(child); free(word_of); free(fill); free(wid); free(nid); free(w); free(pos);
+    return 0;
+}

@@ -176,6 +176,17 @@ int orbref_search_for_triangulation(const orbref_keypoint* k1, const uint8_t* d1
                                     float ex, float ey, const float* scale2, const float* sigma2_2,
                                     int only_stereo, int check_ori, int* match12);
 
+/* §8f row 2: DBoW2 TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup)
+ * (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1125-1259).  Vocabulary as loaded by
+ * loadFromTextFile: nnodes nodes (node 0 = root; parent/is_leaf_flag/desc/weight of node 0
+ * unused), L = depth, scoring / weighting = the file's ScoringType / WeightingType.
+ * Outputs: the BowVector (bow_n words ascending, their weights) and the FeatureVector as
+ * CSR (fv_nnodes node ids ascending, fv_ptr[fv_nnodes + 1], fv_idx).  Arrays sized n (+1). */
+int orbref_voc_transform(int nnodes, const int* parent, const uint8_t* is_leaf_flag, const uint8_t* desc,
+                         const double* weight, int L, int scoring, int weighting, const uint8_t* feats, int n,
+                         int levelsup, int* bow_word, double* bow_weight, int* bow_n, int* fv_node, int* fv_ptr,
+                         int* fv_idx, int* fv_nnodes);
+
 /* Config-5 brute force: per query best index (first min), best and second distance. */
 void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                           int* best_idx, int* best_d, int* second_d);

@@ -83,6 +83,9 @@ def lib():
         L.orbref_search_for_triangulation.argtypes = [C.c_void_p, u8p, u8p, f32p, C.c_int, FV, C.c_void_p, u8p, u8p,
                                                       f32p, C.c_int, FV, f32p, C.c_float, C.c_float, f32p, f32p,
                                                       C.c_int, C.c_int, i32p]
+        f64p = P(C.c_double)
+        L.orbref_voc_transform.argtypes = [C.c_int, i32p, u8p, u8p, f64p, C.c_int, C.c_int, C.c_int, u8p, C.c_int,
+                                           C.c_int, i32p, f64p, i32p, i32p, i32p, i32p, i32p]
         L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
         _lib = L
     return _lib
@@ -316,6 +319,29 @@ def search_for_triangulation(k1, d1, mp1, ur1, fv1, k2, d2, mp2, ur2, fv2, F12, 
                                               _f32(F), ex, ey, _f32(s2), _f32(g2), 1 if only_stereo else 0,
                                               1 if check_ori else 0, _i32(out))
     return n, out[:len(k1)].copy()
+
+
+def voc_transform(voc, desc, levelsup=4):
+    """DBoW2 transform with the oracle: voc has parent/is_leaf/desc/weight/L/scoring/weighting.
+    Returns (bow_word, bow_weight, (fv_node, fv_ptr, fv_idx))."""
+    desc = np.ascontiguousarray(desc, np.uint8)
+    n = len(desc)
+    par = np.ascontiguousarray(voc.parent, np.int32)
+    leaf = np.ascontiguousarray(voc.is_leaf, np.uint8)
+    vd = np.ascontiguousarray(voc.desc, np.uint8)
+    w = np.ascontiguousarray(voc.weight, np.float64)
+    bw = np.zeros(n + 1, np.int32)
+    bv = np.zeros(n + 1, np.float64)
+    fn = np.zeros(n + 1, np.int32)
+    fp = np.zeros(n + 2, np.int32)
+    fi = np.zeros(n + 1, np.int32)
+    nb, nn = C.c_int(0), C.c_int(0)
+    lib().orbref_voc_transform(len(par), _i32(par), _u8(leaf), _u8(vd), w.ctypes.data_as(C.POINTER(C.c_double)),
+                               voc.L, voc.scoring, voc.weighting, _u8(desc), n, levelsup, _i32(bw),
+                               bv.ctypes.data_as(C.POINTER(C.c_double)), C.byref(nb), _i32(fn), _i32(fp), _i32(fi),
+                               C.byref(nn))
+    k, m = nb.value, nn.value
+    return bw[:k].copy(), bv[:k].copy(), (fn[:m].copy(), fp[:m + 1].copy(), fi[:fp[m]].copy())
 
 
 def allpairs_top2(q: np.ndarray, t: np.ndarray):

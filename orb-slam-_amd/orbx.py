@@ -36,6 +36,7 @@ EXPORTED = [
     "orbx_debug_pyramid", "orbx_debug_candidates", "orbm_descriptor_distance", "orbm_allpairs_device",
     "orbm_search_init_batch_device", "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
     "orbm_bow_search_device", "orbm_bow_search",
+    "orbv_load_text", "orbv_create", "orbv_destroy", "orbv_info", "orbv_transform", "orbv_transform_batch_device",
 ]
 BOW_KF_F, BOW_KF_KF, TRIANGULATION = 0, 1, 2
 
@@ -92,6 +93,14 @@ def _load():
                                               f32p, f32p, i32p]
     L.orbx_stereo_batch_device.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_float, C.c_float, vp, vp,
                                            vp, vp]
+    f64p = P(C.c_double)
+    L.orbv_load_text.argtypes = [C.c_char_p, C.c_int, P(vp)]
+    L.orbv_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, i32p, u8p, u8p, f64p, C.c_int, P(vp)]
+    L.orbv_destroy.argtypes = [vp]
+    L.orbv_destroy.restype = None
+    L.orbv_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p, i32p]
+    L.orbv_transform.argtypes = [vp, u8p, C.c_int, C.c_int, i32p, f64p, i32p, i32p, i32p, i32p, i32p]
+    L.orbv_transform_batch_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
     L.orbm_bow_search_device.argtypes = [C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, C.c_int, vp, C.c_int,
                                          vp, vp]
     L.orbm_bow_search.argtypes = [C.c_int, C.c_int, P(BowView), P(BowView), P(TriangParams), C.c_float, C.c_int,
@@ -408,6 +417,84 @@ def allpairs(q, t, mode=TOP2, stream=None):
     _check("orbm_allpairs_device", lib.orbm_allpairs_device(_ptr(q), nq, _ptr(t), nt, FULL_U16, None, None, None,
                                                             _ptr(full), _stream(stream)))
     return full
+
+
+class ORBVocabulary:
+    """DBoW2 TemplatedVocabulary<FORB> on the device (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h):
+    loadFromTextFile, transform(features, BowVector, FeatureVector, levelsup)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        k, L, sc, wt, nn, nw = (C.c_int() for _ in range(6))
+        _check("orbv_info", lib.orbv_info(self._h, C.byref(k), C.byref(L), C.byref(sc), C.byref(wt), C.byref(nn),
+                                          C.byref(nw)))
+        self.k, self.L, self.scoring, self.weighting = k.value, L.value, sc.value, wt.value
+        self.nnodes, self.nwords = nn.value, nw.value
+
+    @staticmethod
+    def loadFromTextFile(path, device=0):
+        h = C.c_void_p()
+        _check("orbv_load_text", lib.orbv_load_text(str(path).encode(), device, C.byref(h)))
+        return ORBVocabulary(h)
+
+    @staticmethod
+    def from_arrays(k, L, parent, is_leaf, desc, weight, scoring=0, weighting=0, device=0):
+        par = np.ascontiguousarray(parent, np.int32)
+        leaf = np.ascontiguousarray(is_leaf, np.uint8)
+        d = np.ascontiguousarray(desc, np.uint8)
+        w = np.ascontiguousarray(weight, np.float64)
+        h = C.c_void_p()
+        _check("orbv_create", lib.orbv_create(k, L, scoring, weighting, len(par),
+                                              par.ctypes.data_as(C.POINTER(C.c_int)), _u8(leaf), _u8(d),
+                                              w.ctypes.data_as(C.POINTER(C.c_double)), device, C.byref(h)))
+        return ORBVocabulary(h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.orbv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def transform(self, desc, levelsup=4):
+        """Returns (bow_word, bow_weight, (fv_node, fv_ptr, fv_idx))."""
+        d = np.ascontiguousarray(desc if desc is not None else np.zeros((0, 32), np.uint8), np.uint8)
+        n = len(d)
+        bw = np.zeros(n + 1, np.int32)
+        bv = np.zeros(n + 1, np.float64)
+        fn = np.zeros(n + 1, np.int32)
+        fp = np.zeros(n + 2, np.int32)
+        fi = np.zeros(n + 1, np.int32)
+        nb, nn = C.c_int(0), C.c_int(0)
+        i32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+        _check("orbv_transform", lib.orbv_transform(self._h, _u8(d), n, levelsup, i32(bw),
+                                                    bv.ctypes.data_as(C.POINTER(C.c_double)), C.byref(nb), i32(fn),
+                                                    i32(fp), i32(fi), C.byref(nn)))
+        k, m = nb.value, nn.value
+        return bw[:k].copy(), bv[:k].copy(), (fn[:m].copy(), fp[:m + 1].copy(), fi[:fp[m]].copy())
+
+    def transform_batch_device(self, desc, counts, levelsup=4, stream=None):
+        """desc: (B, cap, 32) uint8 cuda tensor, counts (B,) int32.  Returns device tensors
+        (bow_word, bow_weight, bow_n, fv_node, fv_ptr, fv_idx, fv_nnodes)."""
+        import torch
+        B, cap = desc.shape[0], desc.shape[1]
+        dev = desc.device
+        bw = torch.empty((B, cap), dtype=torch.int32, device=dev)
+        bv = torch.empty((B, cap), dtype=torch.float64, device=dev)
+        bn = torch.empty((B,), dtype=torch.int32, device=dev)
+        fn = torch.empty((B, cap), dtype=torch.int32, device=dev)
+        fp = torch.empty((B, cap + 1), dtype=torch.int32, device=dev)
+        fi = torch.empty((B, cap), dtype=torch.int32, device=dev)
+        fnn = torch.empty((B,), dtype=torch.int32, device=dev)
+        _check("orbv_transform_batch_device",
+               lib.orbv_transform_batch_device(self._h, _ptr(desc), _ptr(counts), B, cap, levelsup, _ptr(bw),
+                                               _ptr(bv), _ptr(bn), _ptr(fn), _ptr(fp), _ptr(fi), _ptr(fnn),
+                                               _stream(stream)))
+        return bw, bv, bn, fn, fp, fi, fnn
 
 
 class BowBatch:

@@ -103,63 +103,118 @@ def _ham_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 
 class Vocabulary:
-    def __init__(self, k: int, L: int, centers: np.ndarray):
+    """A DBoW2-style vocabulary tree: k-ary, depth <= L, nodes numbered like
+    TemplatedVocabulary::HKmeansStep (the children of a node are consecutive ids,
+    parents before children), leaf weights idf = ln(N / n_i) over the training images
+    (setNodeWeights, TF_IDF).  Clusters of one descriptor become leaves early, so
+    the tree is unbalanced like real vocabularies."""
+
+    def __init__(self, k, L, parent, is_leaf, desc, weight, scoring=0, weighting=0):
         self.k, self.L = k, L
-        self.centers = centers            # [n_nodes, 32]; row 0 (root) unused
+        self.parent = np.asarray(parent, np.int32)      # [nnodes]; parent[0] unused
+        self.is_leaf = np.asarray(is_leaf, np.uint8)
+        self.desc = np.asarray(desc, np.uint8)          # [nnodes, 32]
+        self.weight = np.asarray(weight, np.float64)
+        self.scoring, self.weighting = scoring, weighting
+
+    @property
+    def nnodes(self):
+        return len(self.parent)
 
     @staticmethod
-    def train(descs: np.ndarray, k: int = 10, L: int = 3, seed: int = 0, iters: int = 3) -> "Vocabulary":
+    def train(images_descs, k: int = 10, L: int = 3, seed: int = 0, iters: int = 3) -> "Vocabulary":
+        """images_descs: list of [n_i, 32] uint8 arrays (one per training image)."""
         rng = np.random.default_rng(seed)
-        n_nodes = sum(k ** d for d in range(L + 1))
-        centers = np.zeros((n_nodes, 32), np.uint8)
-        groups = {0: np.asarray(descs, np.uint8)}
-        first = 1
-        for depth in range(1, L + 1):
-            ngroups = {}
-            for parent in range(first - k ** (depth - 1), first):
-                d = groups.get(parent)
-                child0 = first + (parent - (first - k ** (depth - 1))) * k
-                if d is None or len(d) == 0:
-                    centers[child0:child0 + k] = rng.integers(0, 256, (k, 32), dtype=np.uint8)
-                    continue
-                c = d[rng.choice(len(d), k, replace=len(d) < k)]
+        allx = np.concatenate(images_descs)
+        parent, desc = [0], [np.zeros(32, np.uint8)]
+        children = {0: []}
+
+        def step(pid, d, level):
+            if len(d) <= k:
+                cent = [x for x in d]
+            else:
+                c = d[rng.choice(len(d), k, replace=False)]
                 for _ in range(iters):
                     lab = np.argmin(_ham_matrix(d, c), axis=1)
                     for j in range(k):
                         m = d[lab == j]
                         if len(m):
-                            bits = np.unpackbits(m, axis=1).mean(axis=0) > 0.5   # bit majority
-                            c[j] = np.packbits(bits)
-                lab = np.argmin(_ham_matrix(d, c), axis=1)
-                centers[child0:child0 + k] = c
-                for j in range(k):
-                    ngroups[child0 + j] = d[lab == j]
-            groups = ngroups
-            first += k ** depth
-        return Vocabulary(k, L, centers)
+                            c[j] = np.packbits(np.unpackbits(m, axis=1).mean(axis=0) > 0.5)
+                cent = list(c)
+            lab = np.argmin(_ham_matrix(d, np.stack(cent)), axis=1)
+            ids = []
+            for j in range(len(cent)):
+                parent.append(pid)
+                desc.append(cent[j])
+                ids.append(len(parent) - 1)
+                children[ids[-1]] = []
+            children[pid] = ids
+            if level < L:
+                for j, cid in enumerate(ids):
+                    sub = d[lab == j]
+                    if len(sub) > 1:
+                        step(cid, sub, level + 1)
+
+        step(0, allx, 1)
+        n = len(parent)
+        is_leaf = np.array([1 if (i > 0 and not children[i]) else 0 for i in range(n)], np.uint8)
+        voc = Vocabulary(k, L, parent, is_leaf, np.stack(desc), np.zeros(n))
+        # idf of each leaf: ln(N / n_i), n_i = training images holding the word
+        N = len(images_descs)
+        seen = np.zeros(n, np.int64)
+        for d in images_descs:
+            words = np.unique(voc.leaf_of(d))
+            seen[words] += 1
+        w = np.zeros(n)
+        mask = (is_leaf == 1) & (seen > 0)
+        w[mask] = np.log(N / seen[mask])
+        voc.weight = w
+        return voc
+
+    def _children(self):
+        ch = [[] for _ in range(self.nnodes)]
+        for i in range(1, self.nnodes):
+            ch[self.parent[i]].append(i)
+        return ch
+
+    def leaf_of(self, descs):
+        ch = self._children()
+        out = np.zeros(len(descs), np.int64)
+        for f, d in enumerate(np.asarray(descs, np.uint8)):
+            node = 0
+            while ch[node]:
+                dist = np.unpackbits(np.bitwise_xor(self.desc[ch[node]], d), axis=1).sum(axis=1)
+                node = ch[node][int(np.argmin(dist))]
+            out[f] = node
+        return out
 
     def feature_vector(self, descs: np.ndarray, levelsup: int = 1):
-        """FeatureVector as CSR (node ids ascending, ptr, feature indices in insertion order)."""
+        """FeatureVector as CSR (node ids ascending, ptr, feature indices in insertion order);
+        features are grouped by their ancestor at depth L - levelsup (the leaf if shallower)."""
+        ch = self._children()
         descs = np.asarray(descs, np.uint8)
-        n = len(descs)
-        node = np.zeros(n, np.int64)
-        target_depth = self.L - levelsup
-        rec = np.zeros(n, np.int64)
-        first_child = np.full(n, 1, np.int64)   # root's first child
-        level_first = 1
-        for depth in range(1, self.L + 1):
-            kids = first_child[:, None] + np.arange(self.k)[None, :]
-            dist = np.unpackbits(np.bitwise_xor(descs[:, None, :], self.centers[kids]), axis=2).sum(axis=2)
-            node = kids[np.arange(n), np.argmin(dist, axis=1)]   # first strict minimum
-            if depth == target_depth:
-                rec = node.copy()
-            next_first = level_first + self.k ** depth
-            first_child = next_first + (node - level_first) * self.k
-            level_first = next_first
-        if target_depth <= 0:
-            rec = np.zeros(n, np.int64)
+        target = self.L - levelsup
+        rec = np.zeros(len(descs), np.int64)
+        for f, d in enumerate(descs):
+            node, level, nid = 0, 0, 0
+            while ch[node]:
+                level += 1
+                dist = np.unpackbits(np.bitwise_xor(self.desc[ch[node]], d), axis=1).sum(axis=1)
+                node = ch[node][int(np.argmin(dist))]
+                if level == target:
+                    nid = node
+            if target > 0 and level < target:
+                nid = node
+            rec[f] = nid if target > 0 else 0
         ids = np.unique(rec)
         order = np.argsort(rec, kind="stable")
-        counts = np.array([(rec == i).sum() for i in ids], np.int64)
-        ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+        ptr = np.concatenate([[0], np.cumsum([(rec == i).sum() for i in ids])]).astype(np.int32)
         return ids.astype(np.int32), ptr, order.astype(np.int32)
+
+    def save_text(self, path: str):
+        """DBoW2 text format (TemplatedVocabulary::saveToTextFile / loadFromTextFile)."""
+        with open(path, "w") as f:
+            f.write("%d %d %d %d\n" % (self.k, self.L, self.scoring, self.weighting))
+            for i in range(1, self.nnodes):
+                f.write("%d %d %s %r\n" % (self.parent[i], self.is_leaf[i], " ".join(str(int(x)) for x in self.desc[i]),
+                                          float(self.weight[i])))

@@ -11,7 +11,7 @@ PKG = os.path.join(ROOT, "orb-slam-_amd")
 def _declared():
     hdr = open(os.path.join(ROOT, "include", "orbx.h")).read()
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    return sorted(set(re.findall(r"\b(orb[xm]_[a-z0-9_]+)\s*\(", hdr)))
+    return sorted(set(re.findall(r"\b(orb[xmv]_[a-z0-9_]+)\s*\(", hdr)))
 
 
 def _lib():

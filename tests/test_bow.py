@@ -285,7 +285,7 @@ def _kitti_sides(orbref, nfeat=2000, seed=0):
     frames = orbx_synth.kitti_sequence(3, start=40)
     p = orbref.make_params(nfeat, 1.2, 8, 20, 7)
     r = [orbref.extract(f, p, want_pyramid=False) for f in frames]
-    voc = orbx_synth.Vocabulary.train(np.concatenate([x.descriptors for x in r]), 10, 3, seed)
+    voc = orbx_synth.Vocabulary.train([x.descriptors for x in r], 10, 3, seed)
     rng = np.random.default_rng(seed)
     out = []
     for x in r:
