@@ -206,6 +206,40 @@ orbx_status orbm_bow_search_device(int mode, const orbm_bow_view* d_view1, const
 orbx_status orbm_bow_search(int device, int mode, const orbm_bow_view* view1, const orbm_bow_view* view2,
                             const orbm_triang_params* tp, float nnratio, int check_ori, int* match, int* nmatches);
 
+/* ---- Projection search: ORBmatcher::SearchByProjection(Frame& F, vector<MapPoint*>, th) ----
+ * src/ORBmatcher.cc:44-129, the local-map search of Tracking::SearchLocalPoints (src/Tracking.cc:1234-1244),
+ * over Frame::GetFeaturesInArea (src/Frame.cc:410-495).  Per MapPoint, what Frame::isInFrustum left in it: */
+typedef struct {
+    float proj_x, proj_y, proj_xr;   /* mTrackProjX, mTrackProjY, mTrackProjXR */
+    float view_cos;                  /* mTrackViewCos */
+    int32_t level;                   /* mnTrackScaleLevel */
+    int32_t flags;                   /* bit 0: mbTrackInView && !isBad(); bit 1: Observations() > 0 */
+} orbm_proj_point;
+
+typedef struct {
+    float min_x, min_y;              /* Frame::mnMinX, mnMinY (image bounds, src/Frame.cc:563-621) */
+    float grid_w_inv, grid_h_inv;    /* mfGridElementWidthInv / HeightInv */
+    float th;                        /* the th argument */
+    float nnratio;                   /* ORBmatcher::mfNNratio */
+    float scale[16];                 /* F.mvScaleFactors */
+} orbm_proj_params;
+
+/* Batched device path: frame f has d_counts[f] keypoints (mvKeysUn), descriptors, mvuRight and
+ * d_claimed (F.mvpMapPoints[i] && Observations() > 0) at f * cap; d_npts[f] MapPoints and their
+ * descriptors at f * pcap.  Outputs d_match[f * cap + i] = the MapPoint (index) this call
+ * assigned to feature i, -1 (the last one when it overwrote), and d_nmatches[f] (the
+ * reference's return value).  cap <= 8192.  Asynchronous on `stream`. */
+orbx_status orbm_search_by_projection_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const float* d_uright,
+                                             const uint8_t* d_claimed, const int* d_counts, int nframes, int cap,
+                                             const orbm_proj_point* d_pts, const uint8_t* d_pdesc, const int* d_npts,
+                                             int pcap, const orbm_proj_params* params, int* d_match,
+                                             int* d_nmatches, void* stream);
+
+/* Host path for one frame (host arrays), on HIP device `device`.  Synchronous. */
+orbx_status orbm_search_by_projection(int device, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,
+                                      const uint8_t* claimed, int n, const orbm_proj_point* pts, const uint8_t* pdesc,
+                                      int np, const orbm_proj_params* params, int* match, int* nmatches);
+
 /* ---- DBoW2 vocabulary (TemplatedVocabulary, Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) ----
  * Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:521-528, src/KeyFrame.cc:59-66) call
  * transform(descriptors, mBowVec, mFeatVec, 4); the FeatureVector it produces is the

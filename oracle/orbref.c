@@ -1347,3 +1347,95 @@ int orbref_voc_transform(int nnodes, const int* parent, const uint8_t* is_leaf_f
     free(ccount); free(cbegin); free(child); free(word_of); free(fill); free(wid); free(nid); free(w); free(pos);
     return 0;
 }
+
+/* ---- §8f row 3: ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) ----
+ * src/ORBmatcher.cc:44-129 with Frame::GetFeaturesInArea (src/Frame.cc:410-495) over the
+ * frame grid (AssignFeaturesToGrid / PosInGrid, :292-311, 504-518).  Per MapPoint the
+ * caller supplies what Tracking::SearchLocalPoints leaves in it (mTrackProjX/Y/XR,
+ * mTrackViewCos, mnTrackScaleLevel, mbTrackInView && !isBad, Observations() > 0) and its
+ * descriptor.  claimed[i] = F.mvpMapPoints[i] && F.mvpMapPoints[i]->Observations() > 0 on
+ * entry; match[i] = the MapPoint this call assigned to F feature i (the last one), -1. */
+int orbref_search_by_projection(const orbref_keypoint* kps, const uint8_t* desc, const float* uright,
+                                const uint8_t* claimed_in, int n, float min_x, float min_y, float grid_w_inv,
+                                float grid_h_inv, const float* scale, const orbref_proj_point* pts,
+                                const uint8_t* pdesc, int np, float th, float nnratio, int* match)
+{
+    int* cnt = (int*)calloc(GRID_COLS * GRID_ROWS + 1, sizeof(int));
+    int* cellOf = (int*)malloc(sizeof(int) * ((size_t)n + 1));
+    for (int i = 0; i < n; i++) {   /* PosInGrid */
+        const int px = (int)roundf((kps[i].x - min_x) * grid_w_inv);
+        const int py = (int)roundf((kps[i].y - min_y) * grid_h_inv);
+        cellOf[i] = (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) ? -1 : px * GRID_ROWS + py;
+        if (cellOf[i] >= 0) cnt[cellOf[i] + 1]++;
+    }
+    for (int c = 0; c < GRID_COLS * GRID_ROWS; c++) cnt[c + 1] += cnt[c];
+    int* cells = (int*)malloc(sizeof(int) * ((size_t)n + 1));
+    int* fill = (int*)calloc(GRID_COLS * GRID_ROWS, sizeof(int));
+    for (int i = 0; i < n; i++)
+        if (cellOf[i] >= 0) cells[cnt[cellOf[i]] + fill[cellOf[i]]++] = i;
+    uint8_t* claimed = (uint8_t*)malloc((size_t)n + 1);
+    for (int i = 0; i < n; i++) { claimed[i] = claimed_in[i]; match[i] = -1; }
+
+    const int bFactor = th != 1.0;
+    int nmatches = 0;
+    for (int m = 0; m < np; m++) {
+        const orbref_proj_point* P = &pts[m];
+        if (!(P->flags & 1)) continue;                          /* !mbTrackInView || isBad() */
+        const int level = P->level;
+        float r = P->view_cos > 0.998 ? 2.5f : 4.0f;            /* RadiusByViewingCos, :130-136 */
+        if (bFactor) r *= th;
+        const float rr = r * scale[level];
+        const float x = P->proj_x, y = P->proj_y;
+        const int minLevel = level - 1, maxLevel = level;
+        const int nMinCellX = (int)floorf((x - min_x - rr) * grid_w_inv) > 0 ? (int)floorf((x - min_x - rr) * grid_w_inv) : 0;
+        if (nMinCellX >= GRID_COLS) continue;
+        const int cxm = (int)ceilf((x - min_x + rr) * grid_w_inv);
+        const int nMaxCellX = cxm < GRID_COLS - 1 ? cxm : GRID_COLS - 1;
+        if (nMaxCellX < 0) continue;
+        const int nMinCellY = (int)floorf((y - min_y - rr) * grid_h_inv) > 0 ? (int)floorf((y - min_y - rr) * grid_h_inv) : 0;
+        if (nMinCellY >= GRID_ROWS) continue;
+        const int cym = (int)ceilf((y - min_y + rr) * grid_h_inv);
+        const int nMaxCellY = cym < GRID_ROWS - 1 ? cym : GRID_ROWS - 1;
+        if (nMaxCellY < 0) continue;
+        const int bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1, any = 0;
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+                const int c = ix * GRID_ROWS + iy;
+                for (int j = cnt[c]; j < cnt[c + 1]; j++) {
+                    const int idx = cells[j];
+                    const orbref_keypoint* kp = &kps[idx];
+                    if (bCheckLevels) {
+                        if (kp->octave < minLevel) continue;
+                        if (maxLevel >= 0 && kp->octave > maxLevel) continue;
+                    }
+                    const float distx = kp->x - x, disty = kp->y - y;
+                    if (!(fabsf(distx) < rr && fabsf(disty) < rr)) continue;
+                    any = 1;   /* in vIndices */
+                    if (claimed[idx]) continue;                 /* :82-84 */
+                    if (uright[idx] > 0) {                      /* :86-91 */
+                        const float er = fabsf(P->proj_xr - uright[idx]);
+                        if (er > r * scale[level]) continue;
+                    }
+                    const int dist = orbref_descriptor_distance(pdesc + 32 * (size_t)m, desc + 32 * (size_t)idx);
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist; bestDist = dist;
+                        bestLevel2 = bestLevel; bestLevel = kp->octave;
+                        bestIdx = idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = kp->octave; bestDist2 = dist;
+                    }
+                }
+            }
+        }
+        if (!any) continue;
+        if (bestDist <= 100) {                                  /* TH_HIGH, :116-124 */
+            if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) continue;
+            match[bestIdx] = m;
+            claimed[bestIdx] = (P->flags & 2) ? 1 : 0;          /* F.mvpMapPoints[bestIdx] = pMP */
+            nmatches++;
+        }
+    }
+    free(cnt); free(cellOf); free(cells); free(fill); free(claimed);
+    return nmatches;
+}

@@ -187,6 +187,25 @@ int orbref_voc_transform(int nnodes, const int* parent, const uint8_t* is_leaf_f
                          int levelsup, int* bow_word, double* bow_weight, int* bow_n, int* fv_node, int* fv_ptr,
                          int* fv_idx, int* fv_nnodes);
 
+/* Per-MapPoint inputs of SearchByProjection(Frame&, vector<MapPoint*>, th) (what
+ * Frame::isInFrustum leaves in the MapPoint, src/Frame.cc:345-404). */
+typedef struct {
+    float proj_x, proj_y, proj_xr;   /* mTrackProjX, mTrackProjY, mTrackProjXR */
+    float view_cos;                  /* mTrackViewCos */
+    int32_t level;                   /* mnTrackScaleLevel */
+    int32_t flags;                   /* bit 0: mbTrackInView && !isBad(); bit 1: Observations() > 0 */
+} orbref_proj_point;
+
+/* §8f row 3: ORBmatcher::SearchByProjection(Frame& F, vector<MapPoint*>, th) (src/ORBmatcher.cc:44-129)
+ * with GetFeaturesInArea over F's 64x48 grid.  kps = F.mvKeysUn, uright = F.mvuRight,
+ * claimed_in[i] = F.mvpMapPoints[i] && Observations() > 0; grid bounds / inverse cell sizes are
+ * F.mnMinX, mnMinY, mfGridElementWidthInv, mfGridElementHeightInv; scale = mvScaleFactors.
+ * match[i] = the MapPoint index this call assigned to feature i (-1 none).  Returns nmatches. */
+int orbref_search_by_projection(const orbref_keypoint* kps, const uint8_t* desc, const float* uright,
+                                const uint8_t* claimed_in, int n, float min_x, float min_y, float grid_w_inv,
+                                float grid_h_inv, const float* scale, const orbref_proj_point* pts,
+                                const uint8_t* pdesc, int np, float th, float nnratio, int* match);
+
 /* Config-5 brute force: per query best index (first min), best and second distance. */
 void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                           int* best_idx, int* best_d, int* second_d);

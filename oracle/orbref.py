@@ -34,6 +34,15 @@ class Tables(C.Structure):
                 ("nfeat_level", C.c_int * MAX_LEVELS), ("umax", C.c_int * 16)]
 
 
+class ProjPoint(C.Structure):
+    _fields_ = [("proj_x", C.c_float), ("proj_y", C.c_float), ("proj_xr", C.c_float), ("view_cos", C.c_float),
+                ("level", C.c_int32), ("flags", C.c_int32)]
+
+
+PROJ_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+                       ("level", "<i4"), ("flags", "<i4")])
+
+
 class FeatVec(C.Structure):
     _fields_ = [("node", C.POINTER(C.c_int)), ("ptr", C.POINTER(C.c_int)), ("idx", C.POINTER(C.c_int)),
                 ("nnodes", C.c_int)]
@@ -86,6 +95,9 @@ def lib():
         f64p = P(C.c_double)
         L.orbref_voc_transform.argtypes = [C.c_int, i32p, u8p, u8p, f64p, C.c_int, C.c_int, C.c_int, u8p, C.c_int,
                                            C.c_int, i32p, f64p, i32p, i32p, i32p, i32p, i32p]
+        L.orbref_search_by_projection.argtypes = [C.c_void_p, u8p, f32p, u8p, C.c_int, C.c_float, C.c_float,
+                                                  C.c_float, C.c_float, f32p, C.c_void_p, u8p, C.c_int, C.c_float,
+                                                  C.c_float, i32p]
         L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
         _lib = L
     return _lib
@@ -342,6 +354,24 @@ def voc_transform(voc, desc, levelsup=4):
                                C.byref(nn))
     k, m = nb.value, nn.value
     return bw[:k].copy(), bv[:k].copy(), (fn[:m].copy(), fp[:m + 1].copy(), fi[:fp[m]].copy())
+
+
+def search_by_projection(kps, desc, uright, claimed, grid, scale, pts, pdesc, th=1.0, nnratio=0.8):
+    """SearchByProjection(Frame&, vector<MapPoint*>, th).  grid = (min_x, min_y, w_inv, h_inv);
+    pts: PROJ_DTYPE array.  Returns (nmatches, match[n])."""
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    ur = np.ascontiguousarray(uright, np.float32)
+    cl = np.ascontiguousarray(claimed, np.uint8)
+    sc = np.ascontiguousarray(scale, np.float32)
+    pts = np.ascontiguousarray(pts, PROJ_DTYPE)
+    pd = np.ascontiguousarray(pdesc, np.uint8)
+    n = len(kps)
+    out = np.full(max(n, 1), -1, np.int32)
+    nm = lib().orbref_search_by_projection(kps.ctypes.data, _u8(desc), _f32(ur), _u8(cl), n, grid[0], grid[1],
+                                           grid[2], grid[3], _f32(sc), pts.ctypes.data, _u8(pd), len(pts), th,
+                                           nnratio, _i32(out))
+    return nm, out[:n].copy()
 
 
 def allpairs_top2(q: np.ndarray, t: np.ndarray):

@@ -75,4 +75,10 @@ void launch_bow(int mode, const orbm_bow_view* v1, const orbm_bow_view* v2, cons
                 int npairs, int max_nodes1, float nnratio, int check_ori, int* match, int* bins, int stride,
                 int* nmatches, hipStream_t s);
 
+size_t proj_scratch_bytes(int nframes, int cap, int pcap);
+void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uright, const uint8_t* claimed,
+                 const int* counts, int nframes, int cap, const orbm_proj_point* pts, const uint8_t* pdesc,
+                 const int* npts, int pcap, const orbm_proj_params& P, void* scratch, int* match, int* nmatches,
+                 hipStream_t s);
+
 }  // namespace orbx

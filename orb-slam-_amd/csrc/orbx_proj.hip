@@ -1,0 +1,346 @@
+// gfx950 kernels of ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)
+// (src/ORBmatcher.cc:44-129), the local-map search of Tracking::SearchLocalPoints,
+// over Frame::GetFeaturesInArea (src/Frame.cc:410-495).  SURVEY.md §8f row 3.
+//
+// J1 k_pj_grid     one workgroup per frame: (cell, feature) keys of AssignFeaturesToGrid
+//                  sorted in LDS, so a window's columns are one key range and the keys
+//                  run in GetFeaturesInArea's visiting order (ix, then iy, then insertion)
+// J2 k_pj_points   one lane per MapPoint: the reference's sequential best / second scan
+//                  over its window, against the frame's claims on entry
+// J3 k_pj_resolve  one wave per frame replays the MapPoints in order: a MapPoint whose
+//                  best or second candidate was claimed earlier in this call is searched
+//                  again (wave-parallel) against the current claims; the others keep
+//                  their J2 result (a claim on any other candidate changes nothing).
+//                  Claims live in a per-lane register bitmap.
+#include <hip/hip_runtime.h>
+
+#include "orbx_kernels.hpp"
+
+namespace orbx {
+
+constexpr int kPjCols = 64, kPjRows = 48;   // FRAME_GRID_COLS / ROWS (include/Frame.h:37-38)
+
+__device__ __forceinline__ int pj_ham(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1)
+{
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+__device__ __forceinline__ int pj_lower_bound(const uint32_t* a, int n, uint32_t v)
+{
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_pj_grid(const orbx_keypoint* __restrict__ kps, const int* __restrict__ counts,
+                                                 int cap, orbm_proj_params P, uint32_t* __restrict__ gkeys,
+                                                 int* __restrict__ gn)
+{
+    extern __shared__ uint32_t s_keys[];
+    __shared__ int s_ng;
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = min(counts[f], cap);
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    if (tid == 0) s_ng = 0;
+    __syncthreads();
+    const orbx_keypoint* k = kps + (size_t)f * cap;
+    for (int i = tid; i < p2; i += 256) {
+        uint32_t key = 0xFFFFFFFFu;
+        if (i < n) {   // PosInGrid, src/Frame.cc:504-518
+            const int px = (int)roundf((k[i].x - P.min_x) * P.grid_w_inv);
+            const int py = (int)roundf((k[i].y - P.min_y) * P.grid_h_inv);
+            if (px >= 0 && px < kPjCols && py >= 0 && py < kPjRows) {
+                key = ((uint32_t)(px * kPjRows + py) << 16) | (uint32_t)i;
+                atomicAdd(&s_ng, 1);
+            }
+        }
+        s_keys[i] = key;
+    }
+    __syncthreads();
+    for (int size = 2; size <= p2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < (p2 >> 1); i += 256) {
+                const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+                const bool asc = (lo & size) == 0;
+                const uint32_t a = s_keys[lo], b = s_keys[hi];
+                if ((a > b) == asc) {
+                    s_keys[lo] = b;
+                    s_keys[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const int ng = s_ng;
+    for (int g = tid; g < ng; g += 256) gkeys[(size_t)f * cap + g] = s_keys[g];
+    if (tid == 0) gn[f] = ng;
+}
+
+// GetFeaturesInArea(x, y, r * scale[level], level - 1, level) window of one MapPoint
+struct PjWindow {
+    int lo, hi, cy0, cy1, minLevel, maxLevel;
+    float x, y, rr, rs;   // rr = window radius; rs = r * scale[level] for the stereo test
+    bool ok;
+};
+
+__device__ __forceinline__ PjWindow pj_window(const orbm_proj_point& M, const orbm_proj_params& P,
+                                              const uint32_t* keys, int ng)
+{
+    PjWindow w;
+    w.ok = false;
+    w.lo = w.hi = 0;
+    const int level = M.level;
+    if (level < 0 || level >= 16) return w;       // outside mvScaleFactors: UB in the reference
+    float r = M.view_cos > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos, src/ORBmatcher.cc:130-136
+    if (P.th != 1.0f) r *= P.th;
+    w.rr = r * P.scale[level];
+    w.rs = r * P.scale[level];
+    w.x = M.proj_x;
+    w.y = M.proj_y;
+    w.minLevel = level - 1;
+    w.maxLevel = level;
+    const int cx0 = max(0, (int)floorf((w.x - P.min_x - w.rr) * P.grid_w_inv));
+    if (cx0 >= kPjCols) return w;
+    const int cx1 = min(kPjCols - 1, (int)ceilf((w.x - P.min_x + w.rr) * P.grid_w_inv));
+    if (cx1 < 0) return w;
+    w.cy0 = max(0, (int)floorf((w.y - P.min_y - w.rr) * P.grid_h_inv));
+    if (w.cy0 >= kPjRows) return w;
+    w.cy1 = min(kPjRows - 1, (int)ceilf((w.y - P.min_y + w.rr) * P.grid_h_inv));
+    if (w.cy1 < 0) return w;
+    w.lo = pj_lower_bound(keys, ng, (uint32_t)(cx0 * kPjRows) << 16);
+    w.hi = pj_lower_bound(keys, ng, (uint32_t)((cx1 + 1) * kPjRows) << 16);
+    w.ok = true;
+    return w;
+}
+
+// candidate at key position p: the feature index if it is in the window (and not claimed,
+// and passes the stereo test), else -1
+__device__ __forceinline__ int pj_candidate(const PjWindow& w, const orbm_proj_point& M, const uint32_t* keys,
+                                            int p, const orbx_keypoint* kps, const float* uright)
+{
+    const uint32_t key = keys[p];
+    const int iy = (int)(key >> 16) % kPjRows;
+    if (iy < w.cy0 || iy > w.cy1) return -1;
+    const int idx = (int)(key & 0xFFFF);
+    const orbx_keypoint kp = kps[idx];
+    if (kp.octave < w.minLevel) return -1;   // bCheckLevels is true for level >= 0
+    if (w.maxLevel >= 0 && kp.octave > w.maxLevel) return -1;
+    const float distx = kp.x - w.x, disty = kp.y - w.y;
+    if (!(fabsf(distx) < w.rr && fabsf(disty) < w.rr)) return -1;
+    if (uright[idx] > 0) {   // src/ORBmatcher.cc:86-91
+        const float er = fabsf(M.proj_xr - uright[idx]);
+        if (er > w.rs) return -1;
+    }
+    return idx;
+}
+
+// J2 result per MapPoint: best / second candidate and the accept decision
+struct PjResult {
+    int best, second;   // feature indices (-1 none)
+    int accept;         // bestDist <= TH_HIGH and the same-level ratio test passed
+    int pad;
+};
+
+__device__ __forceinline__ bool pj_accept(int bestDist, int bestLevel, int bestDist2, int bestLevel2, float nnratio)
+{
+    if (!(bestDist <= 100)) return false;   // TH_HIGH
+    if (bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) return false;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_pj_points(const orbx_keypoint* __restrict__ kps,
+                                                   const uint8_t* __restrict__ desc, const float* __restrict__ uright,
+                                                   const uint8_t* __restrict__ claimed, int cap,
+                                                   const orbm_proj_point* __restrict__ pts,
+                                                   const uint8_t* __restrict__ pdesc, const int* __restrict__ npts,
+                                                   int pcap, orbm_proj_params P, const uint32_t* __restrict__ gkeys,
+                                                   const int* __restrict__ gn, PjResult* __restrict__ res)
+{
+    const int f = blockIdx.y, m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= min(npts[f], pcap)) return;
+    const size_t mo = (size_t)f * pcap + m;
+    PjResult R{-1, -1, 0, 0};
+    const orbm_proj_point M = pts[mo];
+    if (M.flags & 1) {
+        const uint32_t* keys = gkeys + (size_t)f * cap;
+        const PjWindow w = pj_window(M, P, keys, gn[f]);
+        if (w.ok) {
+            const orbx_keypoint* K = kps + (size_t)f * cap;
+            const float* U = uright + (size_t)f * cap;
+            const uint8_t* C = claimed + (size_t)f * cap;
+            const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
+            const uint4 q0 = qd[0], q1 = qd[1];
+            int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1, bestIdx2 = -1;
+            for (int p = w.lo; p < w.hi; ++p) {   // src/ORBmatcher.cc:78-113, in visiting order
+                const int idx = pj_candidate(w, M, keys, p, K, U);
+                if (idx < 0 || C[idx]) continue;
+                const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
+                const int dist = pj_ham(q0, q1, d[0], d[1]);
+                if (dist < bestDist) {
+                    bestDist2 = bestDist;
+                    bestDist = dist;
+                    bestLevel2 = bestLevel;
+                    bestLevel = K[idx].octave;
+                    bestIdx2 = bestIdx;
+                    bestIdx = idx;
+                } else if (dist < bestDist2) {
+                    bestLevel2 = K[idx].octave;
+                    bestDist2 = dist;
+                    bestIdx2 = idx;
+                }
+            }
+            R.best = bestIdx;
+            R.second = bestIdx2;
+            R.accept = bestIdx >= 0 && pj_accept(bestDist, bestLevel, bestDist2, bestLevel2, P.nnratio);
+        }
+    }
+    res[mo] = R;
+}
+
+__device__ __forceinline__ unsigned long long pj_wave_min_u64(unsigned long long v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(v, o);
+        v = y < v ? y : v;
+    }
+    return v;
+}
+
+constexpr int kPjBitWords = 2;   // per-lane u64 claim words: 64 lanes x 2 x 64 = 8192 features
+
+__global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restrict__ kps,
+                                                   const uint8_t* __restrict__ desc, const float* __restrict__ uright,
+                                                   const uint8_t* __restrict__ claimed, const int* __restrict__ counts,
+                                                   int cap, const orbm_proj_point* __restrict__ pts,
+                                                   const uint8_t* __restrict__ pdesc, const int* __restrict__ npts,
+                                                   int pcap, orbm_proj_params P, const uint32_t* __restrict__ gkeys,
+                                                   const int* __restrict__ gn, const PjResult* __restrict__ res,
+                                                   int* __restrict__ match, int* __restrict__ nmatches)
+{
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int n = min(counts[f], cap), np = min(npts[f], pcap);
+    int* Mo = match + (size_t)f * cap;
+    for (int i = lane; i < n; i += 64) Mo[i] = -1;
+    unsigned long long bits[kPjBitWords] = {0ull, 0ull};   // features claimed during this call
+    const uint32_t* keys = gkeys + (size_t)f * cap;
+    const orbx_keypoint* K = kps + (size_t)f * cap;
+    const float* U = uright + (size_t)f * cap;
+    const uint8_t* C = claimed + (size_t)f * cap;
+    const int ng = gn[f];
+    auto claimed_now = [&](int idx) -> bool {   // wave-uniform idx
+        const int word = idx >> 6, w = word & 63, h = word >> 6;
+        const unsigned long long b =
+            (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits[h], w) |
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits[h] >> 32), w) << 32);
+        return (b >> (idx & 63)) & 1ull;
+    };
+    int count = 0;
+    for (int base = 0; base < np; base += 64) {
+        const int mm = base + lane;
+        PjResult R{-1, -1, 0, 0};
+        int obs = 0;
+        if (mm < np) {
+            R = res[(size_t)f * pcap + mm];
+            obs = (pts[(size_t)f * pcap + mm].flags & 2) ? 1 : 0;
+        }
+        const int cnt = min(64, np - base);
+        for (int j = 0; j < cnt; ++j) {
+            int best = __builtin_amdgcn_readlane(R.best, j);
+            const int second = __builtin_amdgcn_readlane(R.second, j);
+            int accept = __builtin_amdgcn_readlane(R.accept, j);
+            const int o = __builtin_amdgcn_readlane(obs, j);
+            if (best < 0) continue;
+            if (claimed_now(best) || (second >= 0 && claimed_now(second))) {
+                // search again against the current claims: best = first min of (dist, position),
+                // second = first min of the rest (the sequential scan's result)
+                const int m = base + j;
+                const size_t mo = (size_t)f * pcap + m;
+                const orbm_proj_point Mp = pts[mo];
+                const PjWindow w = pj_window(Mp, P, keys, ng);
+                const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
+                const uint4 q0 = qd[0], q1 = qd[1];
+                // candidates in position order, 64 at a time; claims made during this call are
+                // tested one candidate lane at a time (claimed_now needs a uniform index)
+                unsigned long long b1 = ~0ull, b2 = ~0ull;
+                for (int p0 = w.lo; p0 < w.hi; p0 += 64) {
+                    const int p = p0 + lane;
+                    unsigned long long key = ~0ull;
+                    int idx = -1;
+                    if (p < w.hi) {
+                        idx = pj_candidate(w, Mp, keys, p, K, U);
+                        if (idx >= 0 && !C[idx]) {
+                            const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
+                            const int dist = pj_ham(q0, q1, d[0], d[1]);
+                            key = ((unsigned long long)dist << 32) | ((unsigned long long)p << 16) | (unsigned)idx;
+                        }
+                    }
+                    unsigned long long live = __ballot(key != ~0ull);
+                    while (live) {   // claims made in this call: test each candidate lane in turn
+                        const int l = __builtin_ctzll(live);
+                        live &= live - 1;
+                        const int cidx = __builtin_amdgcn_readlane(idx, l);
+                        if (claimed_now(cidx) && lane == l) key = ~0ull;
+                    }
+                    const unsigned long long c1 = pj_wave_min_u64(key);
+                    const unsigned long long c2 = pj_wave_min_u64(key == c1 ? ~0ull : key);
+                    // merge into the running (b1, b2): the multiset top two by (dist, position)
+                    if (c1 < b1) {
+                        b2 = min(b1, c2);
+                        b1 = c1;
+                    } else {
+                        b2 = min(b2, c1);
+                    }
+                }
+                best = b1 == ~0ull ? -1 : (int)(b1 & 0xFFFF);
+                accept = 0;
+                if (best >= 0) {
+                    const int bd = (int)(b1 >> 32);
+                    const int bl = K[best].octave;
+                    const int bd2 = b2 == ~0ull ? 256 : (int)(b2 >> 32);
+                    const int bl2 = b2 == ~0ull ? -1 : K[(int)(b2 & 0xFFFF)].octave;
+                    accept = pj_accept(bd, bl, bd2, bl2, P.nnratio);
+                }
+            }
+            if (best >= 0 && accept) {
+                if (lane == 0) Mo[best] = base + j;   // F.mvpMapPoints[bestIdx] = pMP (last writer)
+                ++count;
+                if (o) {
+                    const int word = best >> 6;
+                    if (lane == (word & 63)) bits[word >> 6] |= 1ull << (best & 63);
+                }
+            }
+        }
+    }
+    if (lane == 0) nmatches[f] = count;
+}
+
+size_t proj_scratch_bytes(int nframes, int cap, int pcap)
+{
+    return (size_t)nframes * cap * 4 + (size_t)nframes * 4 + (size_t)nframes * pcap * sizeof(PjResult) + 256;
+}
+
+void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uright, const uint8_t* claimed,
+                 const int* counts, int nframes, int cap, const orbm_proj_point* pts, const uint8_t* pdesc,
+                 const int* npts, int pcap, const orbm_proj_params& P, void* scratch, int* match, int* nmatches,
+                 hipStream_t s)
+{
+    uint32_t* gkeys = (uint32_t*)scratch;
+    int* gn = (int*)(gkeys + (size_t)nframes * cap);
+    PjResult* res = (PjResult*)(((uintptr_t)(gn + nframes) + 15) & ~(uintptr_t)15);
+    int p2 = 1;
+    while (p2 < cap) p2 <<= 1;
+    hipFuncSetAttribute((const void*)k_pj_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * p2));
+    hipLaunchKernelGGL(k_pj_grid, dim3(nframes), dim3(256), (size_t)4 * p2, s, kps, counts, cap, P, gkeys, gn);
+    hipLaunchKernelGGL(k_pj_points, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright, claimed,
+                       cap, pts, pdesc, npts, pcap, P, gkeys, gn, res);
+    hipLaunchKernelGGL(k_pj_resolve, dim3(nframes), dim3(64), 0, s, kps, desc, uright, claimed, counts, cap, pts,
+                       pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+}
+
+}  // namespace orbx

@@ -36,6 +36,7 @@ EXPORTED = [
     "orbx_debug_pyramid", "orbx_debug_candidates", "orbm_descriptor_distance", "orbm_allpairs_device",
     "orbm_search_init_batch_device", "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
     "orbm_bow_search_device", "orbm_bow_search",
+    "orbm_search_by_projection_device", "orbm_search_by_projection",
     "orbv_load_text", "orbv_create", "orbv_destroy", "orbv_info", "orbv_transform", "orbv_transform_batch_device",
 ]
 BOW_KF_F, BOW_KF_KF, TRIANGULATION = 0, 1, 2
@@ -58,6 +59,26 @@ class TriangParams(C.Structure):
     """orbm_triang_params (SearchForTriangulation geometry)."""
     _fields_ = [("F12", C.c_float * 9), ("ex", C.c_float), ("ey", C.c_float), ("scale2", C.c_float * 16),
                 ("sigma2_2", C.c_float * 16), ("only_stereo", C.c_int32)]
+
+
+PROJ_POINT_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"), ("view_cos", "<f4"),
+                             ("level", "<i4"), ("flags", "<i4")])
+
+
+class ProjParams(C.Structure):
+    """orbm_proj_params (Frame grid bounds, th, nnratio, mvScaleFactors)."""
+    _fields_ = [("min_x", C.c_float), ("min_y", C.c_float), ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float),
+                ("th", C.c_float), ("nnratio", C.c_float), ("scale", C.c_float * 16)]
+
+
+def proj_params(grid, scale, th=1.0, nnratio=0.8):
+    pp = ProjParams()
+    pp.min_x, pp.min_y, pp.grid_w_inv, pp.grid_h_inv = (float(g) for g in grid)
+    pp.th, pp.nnratio = th, nnratio
+    sc = np.zeros(16, np.float32)
+    sc[:len(scale)] = scale
+    pp.scale[:] = [float(x) for x in sc]
+    return pp
 
 
 class _Params(C.Structure):
@@ -101,6 +122,10 @@ def _load():
     L.orbv_info.argtypes = [vp, i32p, i32p, i32p, i32p, i32p, i32p]
     L.orbv_transform.argtypes = [vp, u8p, C.c_int, C.c_int, i32p, f64p, i32p, i32p, i32p, i32p, i32p]
     L.orbv_transform_batch_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.orbm_search_by_projection_device.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int,
+                                                   P(ProjParams), vp, vp, vp]
+    L.orbm_search_by_projection.argtypes = [C.c_int, vp, u8p, f32p, u8p, C.c_int, vp, u8p, C.c_int, P(ProjParams),
+                                            i32p, i32p]
     L.orbm_bow_search_device.argtypes = [C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, C.c_int, vp, C.c_int,
                                          vp, vp]
     L.orbm_bow_search.argtypes = [C.c_int, C.c_int, P(BowView), P(BowView), P(TriangParams), C.c_float, C.c_int,
@@ -338,6 +363,27 @@ class ORBmatcher:
         v2 = _host_view(kf2[0], kf2[1], kf2[2], has_mp=kf2[3], u_right=kf2[4])
         tp = triang_params(F12, ex, ey, scale2, sigma2_2, bOnlyStereo)
         return bow_search(TRIANGULATION, v1, v2, tp, self.mfNNratio, self.mbCheckOrientation, device)
+
+    def SearchByProjection(self, kps, desc, uright, claimed, grid, scale, pts, pdesc, th=1.0, device=0):
+        """SearchByProjection(Frame& F, vector<MapPoint*>, th) (src/ORBmatcher.cc:44-129).
+        kps = F.mvKeysUn, uright = F.mvuRight, claimed[i] = F.mvpMapPoints[i] && Observations() > 0,
+        grid = (mnMinX, mnMinY, mfGridElementWidthInv, mfGridElementHeightInv), scale = mvScaleFactors,
+        pts: PROJ_POINT_DTYPE per MapPoint, pdesc its descriptors.  Returns (nmatches, match[n])."""
+        k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+        d = np.ascontiguousarray(desc, np.uint8)
+        ur = np.ascontiguousarray(uright, np.float32)
+        cl = np.ascontiguousarray(claimed, np.uint8)
+        pp = np.ascontiguousarray(pts, PROJ_POINT_DTYPE)
+        pd = np.ascontiguousarray(pdesc, np.uint8)
+        n = len(k)
+        out = np.full(max(n, 1), -1, np.int32)
+        nm = C.c_int(0)
+        prm = proj_params(grid, scale, th, self.mfNNratio)
+        _check("orbm_search_by_projection",
+               lib.orbm_search_by_projection(device, k.ctypes.data, _u8(d), ur.ctypes.data_as(C.POINTER(C.c_float)),
+                                             _u8(cl), n, pp.ctypes.data, _u8(pd), len(pp), C.byref(prm),
+                                             out.ctypes.data_as(C.POINTER(C.c_int)), C.byref(nm)))
+        return nm.value, out[:n].copy()
 
     def search_for_initialization_batch(self, kps, desc, counts, pair_a, pair_b, rows, cols, window=100,
                                         matches12=None, nmatches=None, stream=None):
