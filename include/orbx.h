@@ -207,7 +207,7 @@ orbx_status orbm_bow_search(int device, int mode, const orbm_bow_view* view1, co
                             const orbm_triang_params* tp, float nnratio, int check_ori, int* match, int* nmatches);
 
 /* ---- Projection search: ORBmatcher::SearchByProjection(Frame& F, vector<MapPoint*>, th) ----
- * src/ORBmatcher.cc:44-129, the local-map search of Tracking::SearchLocalPoints (src/Tracking.cc:1234-1244),
+ * src/ORBmatcher.cc:45-129, the local-map search of Tracking::SearchLocalPoints (src/Tracking.cc:1234-1244),
  * over Frame::GetFeaturesInArea (src/Frame.cc:410-495).  Per MapPoint, what Frame::isInFrustum left in it: */
 typedef struct {
     float proj_x, proj_y, proj_xr;   /* mTrackProjX, mTrackProjY, mTrackProjXR */
@@ -239,6 +239,74 @@ orbx_status orbm_search_by_projection_device(const orbx_keypoint* d_kps, const u
 orbx_status orbm_search_by_projection(int device, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,
                                       const uint8_t* claimed, int n, const orbm_proj_point* pts, const uint8_t* pdesc,
                                       int np, const orbm_proj_params* params, int* match, int* nmatches);
+
+/* ---- Pose-projection searches: the other SearchByProjection overloads and Fuse ----
+ * Each projects MapPoints with a camera pose and keeps, per MapPoint, the first minimum Hamming
+ * distance over the GetFeaturesInArea window (Frame: src/Frame.cc:410-495, KeyFrame:
+ * src/KeyFrame.cc:569-608):
+ *   ORBM_PROJ_LAST_FRAME  SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+ *                         src/ORBmatcher.cc:1396-1538 (Tracking::TrackWithMotionModel, src/Tracking.cc:937)
+ *   ORBM_PROJ_KEYFRAME    SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, sAlreadyFound, th, ORBdist)
+ *                         src/ORBmatcher.cc:1540-1667 (Tracking::Relocalization, src/Tracking.cc:1504,1518)
+ *   ORBM_PROJ_SIM3        SearchByProjection(KeyFrame* pKF, Scw, vpPoints, vpMatched, th)
+ *                         src/ORBmatcher.cc:290-403 (LoopClosing::ComputeSim3, src/LoopClosing.cc:375)
+ *   ORBM_FUSE             Fuse(KeyFrame* pKF, vpMapPoints, th)            src/ORBmatcher.cc:893-1043
+ *                         (LocalMapping::SearchInNeighbors, src/LocalMapping.cc:489,514)
+ *   ORBM_FUSE_SIM3        Fuse(KeyFrame* pKF, Scw, vpPoints, th, vpReplacePoint)  src/ORBmatcher.cc:1045-1168
+ *                         (LoopClosing::SearchAndFuse, src/LoopClosing.cc:599)
+ * The three searches resolve the reference's in-call claims in MapPoint order (a feature taken
+ * earlier in the call is skipped by later MapPoints) and apply the rotation histogram; the two
+ * Fuse overloads make no claims during the search, so their per-MapPoint results are
+ * independent and the caller applies Replace / AddObservation in MapPoint order. */
+enum { ORBM_PROJ_LAST_FRAME = 0, ORBM_PROJ_KEYFRAME = 1, ORBM_PROJ_SIM3 = 2, ORBM_FUSE = 3, ORBM_FUSE_SIM3 = 4 };
+
+typedef struct {
+    float x, y, z;                /* MapPoint::GetWorldPos() */
+    float nx, ny, nz;             /* GetNormal() (SIM3 and the Fuse modes) */
+    float max_dist, min_dist;     /* mfMaxDistance, mfMinDistance (GetMax/MinDistanceInvariance's 1.2f / 0.8f applied inside) */
+    float angle;                  /* LAST_FRAME: LastFrame.mvKeysUn[i].angle; KEYFRAME: pKF->mvKeysUn[i].angle */
+    int32_t octave;               /* LAST_FRAME: LastFrame.mvKeys[i].octave */
+    int32_t flags;                /* bit 0: take part -- LAST_FRAME: pMP && !mvbOutlier[i]; KEYFRAME: pMP && !isBad() &&
+                                     !sAlreadyFound.count(pMP); SIM3 / FUSE_SIM3: !isBad() && not already found;
+                                     FUSE: pMP && !isBad() && !IsInKeyFrame(pKF).  bit 1: Observations() > 0 */
+    int32_t pad;
+} orbm_map_point;
+
+typedef struct {
+    float fx, fy, cx, cy, bf, b;            /* intrinsics, mbf, mb */
+    float min_x, max_x, min_y, max_y;       /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    float grid_w_inv, grid_h_inv;           /* mfGridElementWidthInv / HeightInv */
+    float log_scale;                        /* mfLogScaleFactor */
+    int32_t nlevels;                        /* mnScaleLevels (1..16) */
+    float th;                               /* the th argument */
+    int32_t mono;                           /* bMono (LAST_FRAME) */
+    int32_t orb_dist;                       /* ORBdist (KEYFRAME) */
+    int32_t check_ori;                      /* ORBmatcher::mbCheckOrientation (LAST_FRAME, KEYFRAME) */
+    float scale[16];                        /* mvScaleFactors */
+    float inv_sigma2[16];                   /* mvInvLevelSigma2 (FUSE) */
+} orbm_pose_params;
+
+/* Batched device path.  Frame / KeyFrame f: d_counts[f] keypoints (mvKeysUn), descriptors,
+ * mvuRight and d_claimed at f * cap (d_claimed[i] = the reference's "already taken" test on entry:
+ * LAST_FRAME mvpMapPoints[i] && Observations() > 0; KEYFRAME mvpMapPoints[i]; SIM3 vpMatched[i];
+ * ignored by the Fuse modes); d_pose[f * 24 ..]: row-major 3x4 mTcw (Scw for the SIM3 modes) then,
+ * for LAST_FRAME, LastFrame.mTcw; d_npts[f] MapPoints and their descriptors at f * pcap.
+ * Search modes: d_match[f * cap + i] = the MapPoint this call assigned to feature i (the last one),
+ * -1 untouched, -2 set to NULL by the rotation filter; d_nmatches[f] = the reference's return value.
+ * Fuse modes: d_match[f * pcap + m] = the feature MapPoint m fuses into (bestDist <= TH_LOW), -1;
+ * d_nmatches[f] = nFused.  cap <= 8192.  Asynchronous on `stream`. */
+orbx_status orbm_project_search_device(int mode, const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                                       const float* d_uright, const uint8_t* d_claimed, const int* d_counts,
+                                       int nframes, int cap, const float* d_pose, const orbm_map_point* d_pts,
+                                       const uint8_t* d_pdesc, const int* d_npts, int pcap,
+                                       const orbm_pose_params* params, int* d_match, int* d_nmatches, void* stream);
+
+/* Host path for one Frame / KeyFrame (host arrays; pose = 24 floats as above), on HIP device
+ * `device`.  match: n ints (search modes) or np ints (Fuse modes).  Synchronous. */
+orbx_status orbm_project_search(int device, int mode, const orbx_keypoint* kps, const uint8_t* desc,
+                                const float* uright, const uint8_t* claimed, int n, const float* pose,
+                                const orbm_map_point* pts, const uint8_t* pdesc, int np,
+                                const orbm_pose_params* params, int* match, int* nmatches);
 
 /* ---- DBoW2 vocabulary (TemplatedVocabulary, Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) ----
  * Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:521-528, src/KeyFrame.cc:59-66) call

@@ -1349,7 +1349,7 @@ int orbref_voc_transform(int nnodes, const int* parent, const uint8_t* is_leaf_f
 }
 
 /* ---- §8f row 3: ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th) ----
- * src/ORBmatcher.cc:44-129 with Frame::GetFeaturesInArea (src/Frame.cc:410-495) over the
+ * src/ORBmatcher.cc:45-129 with Frame::GetFeaturesInArea (src/Frame.cc:410-495) over the
  * frame grid (AssignFeaturesToGrid / PosInGrid, :292-311, 504-518).  Per MapPoint the
  * caller supplies what Tracking::SearchLocalPoints leaves in it (mTrackProjX/Y/XR,
  * mTrackViewCos, mnTrackScaleLevel, mbTrackInView && !isBad, Observations() > 0) and its
@@ -1437,5 +1437,244 @@ int orbref_search_by_projection(const orbref_keypoint* kps, const uint8_t* desc,
         }
     }
     free(cnt); free(cellOf); free(cells); free(fill); free(claimed);
+    return nmatches;
+}
+
+/* ---- §8f row 3: the pose-projection searches (SearchByProjection x3, Fuse x2) ----
+ * Arithmetic conventions (DESIGN.md "Projection arithmetic"):
+ *  - cv::Mat 3x3 * 3x1 (+ 3x1) follows OpenCV 3.x gemm's small-matrix path: float products
+ *    summed left to right, then the added column; Mat / double is convertTo(alpha = 1./s);
+ *    Mat::dot and cv::norm accumulate the float products in double.
+ *  - the reference's own float expressions carry the FMAs GCC -O3 -march=native forms.
+ *  - (int) conversions of doubles follow x86-64 cvttsd2si (NaN / out of range -> INT_MIN). */
+static inline int x86_int(double v)
+{
+    return (v >= -2147483648.0 && v < 2147483648.0) ? (int)v : INT_MIN;
+}
+
+static inline float mat3_row(const float* r, int stride, float x, float y, float z)
+{
+    return (r[0] * x + r[stride] * y) + r[2 * stride] * z;
+}
+
+typedef struct {
+    float R[9], t[3], Ow[3];
+    int fwd, bwd;
+} proj_cam;
+
+static void proj_camera(int mode, const float* pose, const orbref_pose_params* P, proj_cam* c)
+{
+    if (mode == ORBREF_PROJ_SIM3 || mode == ORBREF_FUSE_SIM3) {   /* Decompose Scw, :298-303 / :1053-1058 */
+        double d = 0.0;
+        for (int k = 0; k < 3; k++) d += (double)pose[k] * pose[k];
+        const float scw = (float)sqrt(d);
+        const float s = (float)(1.0 / (double)scw);
+        for (int r = 0; r < 3; r++) {
+            for (int k = 0; k < 3; k++) c->R[3 * r + k] = pose[4 * r + k] * s + 0.0f;
+            c->t[r] = pose[4 * r + 3] * s + 0.0f;
+        }
+    } else {
+        for (int r = 0; r < 3; r++) {
+            for (int k = 0; k < 3; k++) c->R[3 * r + k] = pose[4 * r + k];
+            c->t[r] = pose[4 * r + 3];
+        }
+    }
+    for (int r = 0; r < 3; r++)   /* Ow = -Rcw.t()*tcw (KeyFrame::SetPose forms GetCameraCenter alike) */
+        c->Ow[r] = -mat3_row(c->R + r, 3, c->t[0], c->t[1], c->t[2]);
+    c->fwd = c->bwd = 0;
+    if (mode == ORBREF_PROJ_LAST_FRAME) {   /* :1406-1417: twc = Ow, tlc = Rlw*twc+tlw */
+        const float* L = pose + 12;
+        const float tlc2 = mat3_row(L + 8, 1, c->Ow[0], c->Ow[1], c->Ow[2]) + L[11];
+        c->fwd = tlc2 > P->b && !P->mono;
+        c->bwd = -tlc2 > P->b && !P->mono;
+    }
+}
+
+/* MapPoint::PredictScale (src/MapPoint.cc:385-417) */
+static int predict_scale(float max_dist, float dist, const orbref_pose_params* P)
+{
+    const float ratio = max_dist / dist;
+    int n = x86_int(ceil(log((double)ratio) / (double)P->log_scale));
+    if (n < 0) n = 0;
+    else if (n >= P->nlevels) n = P->nlevels - 1;
+    return n;
+}
+
+typedef struct {
+    float u, v, r, ur;
+    int minLevel, maxLevel;
+} proj_win;
+
+/* The per-MapPoint part before the area query; 0 where the reference `continue`s. */
+static int proj_point(int mode, const proj_cam* c, const orbref_map_point* M, const orbref_pose_params* P,
+                      proj_win* w)
+{
+    const float X = M->x, Y = M->y, Z = M->z;
+    const float xc = mat3_row(c->R, 1, X, Y, Z) + c->t[0];
+    const float yc = mat3_row(c->R + 3, 1, X, Y, Z) + c->t[1];
+    const float zc = mat3_row(c->R + 6, 1, X, Y, Z) + c->t[2];
+    float u, v;
+    w->ur = 0.0f;
+    if (mode == ORBREF_PROJ_LAST_FRAME || mode == ORBREF_PROJ_KEYFRAME) {
+        const float invzc = (float)(1.0 / (double)zc);          /* :1433 / :1570 */
+        if (mode == ORBREF_PROJ_LAST_FRAME && invzc < 0) return 0;
+        u = fmaf(P->fx * xc, invzc, P->cx);                     /* fx*xc*invzc+cx */
+        v = fmaf(P->fy * yc, invzc, P->cy);
+        if (u < P->min_x || u > P->max_x) return 0;
+        if (v < P->min_y || v > P->max_y) return 0;
+        w->u = u;
+        w->v = v;
+        if (mode == ORBREF_PROJ_LAST_FRAME) {                  /* :1446-1458 */
+            const int L = M->octave;
+            w->r = P->th * P->scale[L];
+            if (c->fwd) { w->minLevel = L; w->maxLevel = -1; }
+            else if (c->bwd) { w->minLevel = 0; w->maxLevel = L; }
+            else { w->minLevel = L - 1; w->maxLevel = L + 1; }
+            w->ur = fmaf(-P->bf, invzc, u);                     /* u - mbf*invzc, :1477 */
+            return 1;
+        }
+    } else {
+        if (zc < 0.0f) return 0;
+        const float invz = mode == ORBREF_FUSE_SIM3 ? (float)(1.0 / (double)zc) : 1.0f / zc;
+        const float x = xc * invz, y = yc * invz;
+        u = fmaf(P->fx, x, P->cx);
+        v = fmaf(P->fy, y, P->cy);
+        if (!(u >= P->min_x && u < P->max_x && v >= P->min_y && v < P->max_y)) return 0;   /* IsInImage */
+        w->u = u;
+        w->v = v;
+        if (mode == ORBREF_FUSE) w->ur = fmaf(-P->bf, invz, u);   /* u-bf*invz, :938 */
+    }
+    const float maxD = 1.2f * M->max_dist, minD = 0.8f * M->min_dist;   /* Get{Max,Min}DistanceInvariance */
+    const float PO[3] = {X - c->Ow[0], Y - c->Ow[1], Z - c->Ow[2]};
+    double s = 0.0;
+    for (int k = 0; k < 3; k++) s += (double)PO[k] * PO[k];
+    const float dist = (float)sqrt(s);                          /* cv::norm(PO) */
+    if (dist < minD || dist > maxD) return 0;
+    if (mode != ORBREF_PROJ_KEYFRAME) {                        /* viewing angle < 60 deg */
+        double dot = 0.0;
+        dot += (double)PO[0] * M->nx;
+        dot += (double)PO[1] * M->ny;
+        dot += (double)PO[2] * M->nz;
+        if (dot < 0.5 * dist) return 0;
+    }
+    const int L = predict_scale(M->max_dist, dist, P);
+    w->r = P->th * P->scale[L];
+    w->minLevel = L - 1;
+    w->maxLevel = mode == ORBREF_PROJ_KEYFRAME ? L + 1 : L;
+    return 1;
+}
+
+/* Per-candidate tests of each mode other than the claims (level window, area, stereo). */
+static int proj_candidate_ok(int mode, const proj_win* w, const orbref_keypoint* kp, float ur,
+                             const orbref_pose_params* P)
+{
+    if (kp->octave < w->minLevel) return 0;
+    if (w->maxLevel >= 0 && kp->octave > w->maxLevel) return 0;
+    const float distx = kp->x - w->u, disty = kp->y - w->v;
+    if (!(fabsf(distx) < w->r && fabsf(disty) < w->r)) return 0;
+    if (mode == ORBREF_PROJ_LAST_FRAME && ur > 0) {            /* :1475-1481 */
+        const float er = fabsf(w->ur - ur);
+        if (er > w->r) return 0;
+    }
+    if (mode == ORBREF_FUSE) {                                  /* :982-1006 */
+        const float ex = w->u - kp->x, ey = w->v - kp->y;
+        if (ur >= 0) {
+            const float er = w->ur - ur;
+            const float e2 = fmaf(er, er, fmaf(ex, ex, ey * ey));
+            if ((double)(e2 * P->inv_sigma2[kp->octave]) > 7.8) return 0;
+        } else {
+            const float e2 = fmaf(ex, ex, ey * ey);
+            if ((double)(e2 * P->inv_sigma2[kp->octave]) > 5.99) return 0;
+        }
+    }
+    return 1;
+}
+
+int orbref_project_search(int mode, const orbref_keypoint* kps, const uint8_t* desc, const float* uright,
+                          const uint8_t* claimed_in, int n, const float* pose, const orbref_map_point* pts,
+                          const uint8_t* pdesc, int np, const orbref_pose_params* P, int* match)
+{
+    const int search = mode <= ORBREF_PROJ_SIM3;
+    const int rot = P->check_ori && (mode == ORBREF_PROJ_LAST_FRAME || mode == ORBREF_PROJ_KEYFRAME);
+    const int thr = mode == ORBREF_PROJ_LAST_FRAME ? 100 : (mode == ORBREF_PROJ_KEYFRAME ? P->orb_dist : TH_LOW);
+    int* cnt = (int*)calloc(GRID_COLS * GRID_ROWS + 1, sizeof(int));   /* AssignFeaturesToGrid */
+    int* cellOf = (int*)malloc(sizeof(int) * ((size_t)n + 1));
+    for (int i = 0; i < n; i++) {
+        const int px = (int)roundf((kps[i].x - P->min_x) * P->grid_w_inv);
+        const int py = (int)roundf((kps[i].y - P->min_y) * P->grid_h_inv);
+        cellOf[i] = (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) ? -1 : px * GRID_ROWS + py;
+        if (cellOf[i] >= 0) cnt[cellOf[i] + 1]++;
+    }
+    for (int c = 0; c < GRID_COLS * GRID_ROWS; c++) cnt[c + 1] += cnt[c];
+    int* cells = (int*)malloc(sizeof(int) * ((size_t)n + 1));
+    int* fill = (int*)calloc(GRID_COLS * GRID_ROWS, sizeof(int));
+    for (int i = 0; i < n; i++)
+        if (cellOf[i] >= 0) cells[cnt[cellOf[i]] + fill[cellOf[i]]++] = i;
+    uint8_t* claimed = (uint8_t*)calloc((size_t)n + 1, 1);
+    if (search)
+        for (int i = 0; i < n; i++) { claimed[i] = claimed_in ? claimed_in[i] : 0; match[i] = -1; }
+    else
+        for (int m = 0; m < np; m++) match[m] = -1;
+    int* ent_idx = (int*)malloc(sizeof(int) * ((size_t)np + 1));   /* rotHist entries in push order */
+    int* ent_bin = (int*)malloc(sizeof(int) * ((size_t)np + 1));
+    int nent = 0, nmatches = 0;
+    proj_cam cam;
+    proj_camera(mode, pose, P, &cam);
+
+    for (int m = 0; m < np; m++) {
+        const orbref_map_point* M = &pts[m];
+        if (!(M->flags & 1)) continue;
+        proj_win w;
+        if (!proj_point(mode, &cam, M, P, &w)) continue;
+        /* GetFeaturesInArea cell range (Frame.cc:410-495 / KeyFrame.cc:569-608) */
+        const int cx0 = x86_int(floorf((w.u - P->min_x - w.r) * P->grid_w_inv));
+        const int nMinCellX = cx0 > 0 ? cx0 : 0;
+        if (nMinCellX >= GRID_COLS) continue;
+        const int cx1 = x86_int(ceilf((w.u - P->min_x + w.r) * P->grid_w_inv));
+        const int nMaxCellX = cx1 < GRID_COLS - 1 ? cx1 : GRID_COLS - 1;
+        if (nMaxCellX < 0) continue;
+        const int cy0 = x86_int(floorf((w.v - P->min_y - w.r) * P->grid_h_inv));
+        const int nMinCellY = cy0 > 0 ? cy0 : 0;
+        if (nMinCellY >= GRID_ROWS) continue;
+        const int cy1 = x86_int(ceilf((w.v - P->min_y + w.r) * P->grid_h_inv));
+        const int nMaxCellY = cy1 < GRID_ROWS - 1 ? cy1 : GRID_ROWS - 1;
+        if (nMaxCellY < 0) continue;
+        int bestDist = 256, bestIdx = -1;
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+                const int c = ix * GRID_ROWS + iy;
+                for (int j = cnt[c]; j < cnt[c + 1]; j++) {
+                    const int idx = cells[j];
+                    if (!proj_candidate_ok(mode, &w, &kps[idx], uright[idx], P)) continue;
+                    if (search && claimed[idx]) continue;
+                    const int dist = orbref_descriptor_distance(pdesc + 32 * (size_t)m, desc + 32 * (size_t)idx);
+                    if (dist < bestDist) { bestDist = dist; bestIdx = idx; }
+                }
+            }
+        }
+        if (bestIdx < 0 || bestDist > thr) continue;
+        nmatches++;
+        if (!search) { match[m] = bestIdx; continue; }
+        match[bestIdx] = m;                                     /* mvpMapPoints[bestIdx] = pMP */
+        claimed[bestIdx] = mode != ORBREF_PROJ_LAST_FRAME || (M->flags & 2);
+        if (rot) {
+            ent_idx[nent] = bestIdx;
+            ent_bin[nent] = rot_bin(M->angle, kps[bestIdx].angle);
+            nent++;
+        }
+    }
+    if (rot) {   /* :1515-1535 / :1645-1664 */
+        int hist[HISTO_LENGTH] = {0};
+        for (int e = 0; e < nent; e++) hist[ent_bin[e]]++;
+        int a, b, c;
+        three_maxima(hist, &a, &b, &c);
+        for (int e = 0; e < nent; e++) {
+            const int bin = ent_bin[e];
+            if (bin == a || bin == b || bin == c) continue;
+            match[ent_idx[e]] = -2;                             /* mvpMapPoints[...] = NULL */
+            nmatches--;
+        }
+    }
+    free(cnt); free(cellOf); free(cells); free(fill); free(claimed); free(ent_idx); free(ent_bin);
     return nmatches;
 }

@@ -196,7 +196,7 @@ typedef struct {
     int32_t flags;                   /* bit 0: mbTrackInView && !isBad(); bit 1: Observations() > 0 */
 } orbref_proj_point;
 
-/* §8f row 3: ORBmatcher::SearchByProjection(Frame& F, vector<MapPoint*>, th) (src/ORBmatcher.cc:44-129)
+/* §8f row 3: ORBmatcher::SearchByProjection(Frame& F, vector<MapPoint*>, th) (src/ORBmatcher.cc:45-129)
  * with GetFeaturesInArea over F's 64x48 grid.  kps = F.mvKeysUn, uright = F.mvuRight,
  * claimed_in[i] = F.mvpMapPoints[i] && Observations() > 0; grid bounds / inverse cell sizes are
  * F.mnMinX, mnMinY, mfGridElementWidthInv, mfGridElementHeightInv; scale = mvScaleFactors.
@@ -205,6 +205,55 @@ int orbref_search_by_projection(const orbref_keypoint* kps, const uint8_t* desc,
                                 const uint8_t* claimed_in, int n, float min_x, float min_y, float grid_w_inv,
                                 float grid_h_inv, const float* scale, const orbref_proj_point* pts,
                                 const uint8_t* pdesc, int np, float th, float nnratio, int* match);
+
+/* §8f row 3, the pose-projection searches.  Each projects MapPoints with a camera pose
+ * into a Frame / KeyFrame and takes, per MapPoint, the first minimum Hamming distance over
+ * the GetFeaturesInArea window:
+ *   ORBREF_PROJ_LAST_FRAME  SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono)
+ *                           src/ORBmatcher.cc:1396-1538
+ *   ORBREF_PROJ_KEYFRAME    SearchByProjection(Frame& CurrentFrame, KeyFrame*, sAlreadyFound, th, ORBdist)
+ *                           src/ORBmatcher.cc:1540-1667
+ *   ORBREF_PROJ_SIM3        SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th)  :290-403
+ *   ORBREF_FUSE             Fuse(KeyFrame*, vpMapPoints, th)                             :893-1043
+ *   ORBREF_FUSE_SIM3        Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint)           :1045-1168
+ * Float arithmetic: see DESIGN.md "Projection arithmetic" (cv::Mat products as OpenCV 3.x's
+ * small-matrix gemm, the reference's own expressions with GCC -march=native contractions). */
+enum { ORBREF_PROJ_LAST_FRAME = 0, ORBREF_PROJ_KEYFRAME = 1, ORBREF_PROJ_SIM3 = 2, ORBREF_FUSE = 3,
+       ORBREF_FUSE_SIM3 = 4 };
+
+typedef struct {
+    float x, y, z;                /* MapPoint::GetWorldPos() */
+    float nx, ny, nz;             /* GetNormal() (Sim3 and Fuse modes) */
+    float max_dist, min_dist;     /* mfMaxDistance, mfMinDistance (the 1.2f / 0.8f factors applied inside) */
+    float angle;                  /* LAST_FRAME: LastFrame.mvKeysUn[i].angle; KEYFRAME: pKF->mvKeysUn[i].angle */
+    int32_t octave;               /* LAST_FRAME: LastFrame.mvKeys[i].octave */
+    int32_t flags;                /* bit 0: takes part (see orbx.h); bit 1: Observations() > 0 (LAST_FRAME claims) */
+    int32_t pad;
+} orbref_map_point;
+
+typedef struct {
+    float fx, fy, cx, cy, bf, b;            /* intrinsics, mbf, mb */
+    float min_x, max_x, min_y, max_y;       /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+    float grid_w_inv, grid_h_inv;           /* mfGridElementWidthInv / HeightInv */
+    float log_scale;                        /* mfLogScaleFactor */
+    int32_t nlevels;                        /* mnScaleLevels */
+    float th;                               /* the th argument */
+    int32_t mono;                           /* bMono (LAST_FRAME) */
+    int32_t orb_dist;                       /* ORBdist (KEYFRAME) */
+    int32_t check_ori;                      /* mbCheckOrientation (LAST_FRAME, KEYFRAME) */
+    float scale[16];                        /* mvScaleFactors */
+    float inv_sigma2[16];                   /* mvInvLevelSigma2 (FUSE) */
+} orbref_pose_params;
+
+/* pose[0..11]: row-major 3x4 mTcw (Scw for the Sim3 modes); pose[12..23]: LastFrame.mTcw (LAST_FRAME).
+ * kps = mvKeysUn, uright = mvuRight, claimed_in[i] = the reference's "already taken" test on entry
+ * (LAST_FRAME: mvpMapPoints[i] && Observations() > 0; KEYFRAME: mvpMapPoints[i]; SIM3: vpMatched[i];
+ * Fuse modes: unused).  Search modes: match[i] (n entries) = MapPoint index assigned to feature i,
+ * -1 untouched, -2 set to NULL by the rotation filter; returns nmatches.  Fuse modes: match[m]
+ * (np entries) = the feature MapPoint m fuses into (bestDist <= TH_LOW) or -1; returns nFused. */
+int orbref_project_search(int mode, const orbref_keypoint* kps, const uint8_t* desc, const float* uright,
+                          const uint8_t* claimed_in, int n, const float* pose, const orbref_map_point* pts,
+                          const uint8_t* pdesc, int np, const orbref_pose_params* P, int* match);
 
 /* Config-5 brute force: per query best index (first min), best and second distance. */
 void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,

@@ -43,6 +43,23 @@ PROJ_DTYPE = np.dtype([("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"),
                        ("level", "<i4"), ("flags", "<i4")])
 
 
+PROJ_LAST_FRAME, PROJ_KEYFRAME, PROJ_SIM3, FUSE, FUSE_SIM3 = 0, 1, 2, 3, 4
+
+MAP_POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                            ("max_dist", "<f4"), ("min_dist", "<f4"), ("angle", "<f4"), ("octave", "<i4"),
+                            ("flags", "<i4"), ("pad", "<i4")])
+assert MAP_POINT_DTYPE.itemsize == 48
+
+
+class PoseParams(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("b", C.c_float), ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float),
+                ("max_y", C.c_float), ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float),
+                ("log_scale", C.c_float), ("nlevels", C.c_int32), ("th", C.c_float), ("mono", C.c_int32),
+                ("orb_dist", C.c_int32), ("check_ori", C.c_int32), ("scale", C.c_float * 16),
+                ("inv_sigma2", C.c_float * 16)]
+
+
 class FeatVec(C.Structure):
     _fields_ = [("node", C.POINTER(C.c_int)), ("ptr", C.POINTER(C.c_int)), ("idx", C.POINTER(C.c_int)),
                 ("nnodes", C.c_int)]
@@ -98,6 +115,8 @@ def lib():
         L.orbref_search_by_projection.argtypes = [C.c_void_p, u8p, f32p, u8p, C.c_int, C.c_float, C.c_float,
                                                   C.c_float, C.c_float, f32p, C.c_void_p, u8p, C.c_int, C.c_float,
                                                   C.c_float, i32p]
+        L.orbref_project_search.argtypes = [C.c_int, C.c_void_p, u8p, f32p, u8p, C.c_int, f32p, C.c_void_p, u8p,
+                                            C.c_int, P(PoseParams), i32p]
         L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
         _lib = L
     return _lib
@@ -372,6 +391,26 @@ def search_by_projection(kps, desc, uright, claimed, grid, scale, pts, pdesc, th
                                            grid[2], grid[3], _f32(sc), pts.ctypes.data, _u8(pd), len(pts), th,
                                            nnratio, _i32(out))
     return nm, out[:n].copy()
+
+
+def project_search(mode, kps, desc, uright, claimed, pose, pts, pdesc, params: PoseParams):
+    """The pose-projection searches (orbref.h ORBREF_PROJ_* / ORBREF_FUSE*).  pose: 24 floats
+    (Tcw or Scw 3x4, then LastFrame Tcw).  Returns (n, match) with match[n] for the search
+    modes and match[np] for the Fuse modes."""
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    ur = np.ascontiguousarray(uright, np.float32)
+    cl = np.ascontiguousarray(claimed if claimed is not None else np.zeros(len(kps), np.uint8), np.uint8)
+    ps = np.zeros(24, np.float32)
+    pose = np.asarray(pose, np.float32).ravel()
+    ps[:len(pose)] = pose
+    pts = np.ascontiguousarray(pts, MAP_POINT_DTYPE)
+    pd = np.ascontiguousarray(pdesc, np.uint8)
+    nout = len(kps) if mode <= PROJ_SIM3 else len(pts)
+    out = np.full(max(nout, 1), -1, np.int32)
+    nm = lib().orbref_project_search(mode, kps.ctypes.data, _u8(desc), _f32(ur), _u8(cl), len(kps), _f32(ps),
+                                     pts.ctypes.data, _u8(pd), len(pts), C.byref(params), _i32(out))
+    return nm, out[:nout].copy()
 
 
 def allpairs_top2(q: np.ndarray, t: np.ndarray):

@@ -899,6 +899,79 @@ orbx_status orbm_search_by_projection(int device, const orbx_keypoint* kps, cons
     return rc;
 }
 
+orbx_status orbm_project_search_device(int mode, const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                                       const float* d_uright, const uint8_t* d_claimed, const int* d_counts,
+                                       int nframes, int cap, const float* d_pose, const orbm_map_point* d_pts,
+                                       const uint8_t* d_pdesc, const int* d_npts, int pcap,
+                                       const orbm_pose_params* params, int* d_match, int* d_nmatches, void* stream)
+{
+    if (mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_FUSE_SIM3 || !d_kps || !d_desc || !d_uright || !d_claimed ||
+        !d_counts || nframes < 0 || cap <= 0 || cap > 8192 || !d_pose || !d_pts || !d_pdesc || !d_npts ||
+        pcap <= 0 || !params || !d_match || !d_nmatches || params->nlevels < 1 || params->nlevels > 16)
+        return ORBX_EINVAL;
+    if (nframes == 0) return ORBX_OK;
+    hipStream_t s = (hipStream_t)stream;
+    void* scratch = nullptr;
+    if (hipMallocAsync(&scratch, pose_scratch_bytes(nframes, cap, pcap), s) != hipSuccess) return ORBX_ENOMEM;
+    launch_pose_search(mode, d_kps, d_desc, d_uright, d_claimed, d_counts, nframes, cap, d_pose, d_pts, d_pdesc,
+                       d_npts, pcap, *params, scratch, d_match, d_nmatches, s);
+    hipFreeAsync(scratch, s);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+orbx_status orbm_project_search(int device, int mode, const orbx_keypoint* kps, const uint8_t* desc,
+                                const float* uright, const uint8_t* claimed, int n, const float* pose,
+                                const orbm_map_point* pts, const uint8_t* pdesc, int np,
+                                const orbm_pose_params* params, int* match, int* nmatches)
+{
+    if (mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_FUSE_SIM3 || n < 0 || n > 8192 || np < 0 || !params ||
+        !nmatches || !pose || params->nlevels < 1 || params->nlevels > 16)
+        return ORBX_EINVAL;
+    const bool search = mode <= ORBM_PROJ_SIM3;
+    const int nout = search ? n : np;
+    *nmatches = 0;
+    if (nout > 0 && !match) return ORBX_EINVAL;
+    if ((n > 0 && (!kps || !desc || !uright || (search && !claimed))) || (np > 0 && (!pts || !pdesc)))
+        return ORBX_EINVAL;
+    for (int i = 0; i < n; ++i)
+        if (kps[i].octave < 0 || kps[i].octave >= 16) return ORBX_EINVAL;
+    if (mode == ORBM_PROJ_LAST_FRAME)
+        for (int i = 0; i < np; ++i)
+            if ((pts[i].flags & 1) && (pts[i].octave < 0 || pts[i].octave >= 16)) return ORBX_EINVAL;
+    for (int i = 0; i < nout; ++i) match[i] = -1;
+    if (n == 0 || np == 0) return ORBX_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
+    hipSetDevice(device);
+    BowStage st;
+    const size_t ok = st.add(kps, sizeof(orbx_keypoint) * (size_t)n);
+    const size_t od = st.add(desc, (size_t)32 * n);
+    const size_t ou = st.add(uright, sizeof(float) * (size_t)n);
+    const size_t oc = st.add(search ? claimed : nullptr, (size_t)n);
+    const size_t opo = st.add(pose, sizeof(float) * 24);
+    const size_t op = st.add(pts, sizeof(orbm_map_point) * (size_t)np);
+    const size_t opd = st.add(pdesc, (size_t)32 * np);
+    const int cn[2] = {n, np};
+    const size_t ocn = st.add(cn, sizeof(cn));
+    const size_t om = st.add(nullptr, sizeof(int) * ((size_t)nout + 1));
+    uint8_t* d = nullptr;
+    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
+    orbx_status rc = ORBX_OK;
+    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
+    if (rc == ORBX_OK) {
+        int* dm = (int*)(d + om);
+        rc = orbm_project_search_device(mode, (const orbx_keypoint*)(d + ok), d + od, (const float*)(d + ou), d + oc,
+                                        (const int*)(d + ocn), 1, n, (const float*)(d + opo),
+                                        (const orbm_map_point*)(d + op), d + opd, (const int*)(d + ocn) + 1, np,
+                                        params, dm + 1, dm, nullptr);
+        if (rc == ORBX_OK && (hipMemcpy(match, dm + 1, sizeof(int) * (size_t)nout, hipMemcpyDeviceToHost) != hipSuccess ||
+                              hipMemcpy(nmatches, dm, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess))
+            rc = ORBX_EDEVICE;
+    }
+    hipFree(d);
+    return rc;
+}
+
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b)
 {
     int d = 0;

@@ -81,4 +81,10 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
                  const int* npts, int pcap, const orbm_proj_params& P, void* scratch, int* match, int* nmatches,
                  hipStream_t s);
 
+size_t pose_scratch_bytes(int nframes, int cap, int pcap);
+void launch_pose_search(int mode, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,
+                        const uint8_t* claimed, const int* counts, int nframes, int cap, const float* pose,
+                        const orbm_map_point* pts, const uint8_t* pdesc, const int* npts, int pcap,
+                        const orbm_pose_params& P, void* scratch, int* match, int* nmatches, hipStream_t s);
+
 }  // namespace orbx

@@ -1,5 +1,5 @@
 // gfx950 kernels of ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th)
-// (src/ORBmatcher.cc:44-129), the local-map search of Tracking::SearchLocalPoints,
+// (src/ORBmatcher.cc:45-129), the local-map search of Tracking::SearchLocalPoints,
 // over Frame::GetFeaturesInArea (src/Frame.cc:410-495).  SURVEY.md §8f row 3.
 //
 // J1 k_pj_grid     one workgroup per frame: (cell, feature) keys of AssignFeaturesToGrid
@@ -37,8 +37,8 @@ __device__ __forceinline__ int pj_lower_bound(const uint32_t* a, int n, uint32_t
 }
 
 __global__ __launch_bounds__(256) void k_pj_grid(const orbx_keypoint* __restrict__ kps, const int* __restrict__ counts,
-                                                 int cap, orbm_proj_params P, uint32_t* __restrict__ gkeys,
-                                                 int* __restrict__ gn)
+                                                 int cap, float min_x, float min_y, float grid_w_inv,
+                                                 float grid_h_inv, uint32_t* __restrict__ gkeys, int* __restrict__ gn)
 {
     extern __shared__ uint32_t s_keys[];
     __shared__ int s_ng;
@@ -52,8 +52,8 @@ __global__ __launch_bounds__(256) void k_pj_grid(const orbx_keypoint* __restrict
     for (int i = tid; i < p2; i += 256) {
         uint32_t key = 0xFFFFFFFFu;
         if (i < n) {   // PosInGrid, src/Frame.cc:504-518
-            const int px = (int)roundf((k[i].x - P.min_x) * P.grid_w_inv);
-            const int py = (int)roundf((k[i].y - P.min_y) * P.grid_h_inv);
+            const int px = (int)roundf((k[i].x - min_x) * grid_w_inv);
+            const int py = (int)roundf((k[i].y - min_y) * grid_h_inv);
             if (px >= 0 && px < kPjCols && py >= 0 && py < kPjRows) {
                 key = ((uint32_t)(px * kPjRows + py) << 16) | (uint32_t)i;
                 atomicAdd(&s_ng, 1);
@@ -336,11 +336,449 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
     int p2 = 1;
     while (p2 < cap) p2 <<= 1;
     hipFuncSetAttribute((const void*)k_pj_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * p2));
-    hipLaunchKernelGGL(k_pj_grid, dim3(nframes), dim3(256), (size_t)4 * p2, s, kps, counts, cap, P, gkeys, gn);
+    hipLaunchKernelGGL(k_pj_grid, dim3(nframes), dim3(256), (size_t)4 * p2, s, kps, counts, cap, P.min_x, P.min_y,
+                       P.grid_w_inv, P.grid_h_inv, gkeys, gn);
     hipLaunchKernelGGL(k_pj_points, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright, claimed,
                        cap, pts, pdesc, npts, pcap, P, gkeys, gn, res);
     hipLaunchKernelGGL(k_pj_resolve, dim3(nframes), dim3(64), 0, s, kps, desc, uright, claimed, counts, cap, pts,
                        pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+}
+
+// =====================================================================================
+// Pose-projection searches: SearchByProjection(CurrentFrame, LastFrame) (:1396-1538),
+// SearchByProjection(CurrentFrame, pKF, sAlreadyFound) (:1540-1667), SearchByProjection(pKF,
+// Scw, ...) (:290-403), Fuse(pKF, ...) (:893-1043), Fuse(pKF, Scw, ...) (:1045-1168).
+//
+// J1 k_pj_grid     as above
+// J2 k_ps_points   one lane per MapPoint: project with the frame pose, scan the window in
+//                  GetFeaturesInArea order against the claims on entry (first minimum).
+//                  The Fuse overloads claim nothing during the search: they finish here.
+// J3 k_ps_resolve  one wave per frame replays the three searches in MapPoint order; a
+//                  MapPoint whose best candidate was taken earlier in the call searches
+//                  again against the current claims; then the rotation histogram.
+// Float arithmetic is oracle/orbref.c proj_* operation for operation (no contraction in this
+// file; the reference's GCC -march=native FMAs are explicit).
+// =====================================================================================
+
+__device__ __forceinline__ int ps_x86_int(double v)   // cvttsd2si: NaN / out of range -> INT_MIN
+{
+    return (v >= -2147483648.0 && v < 2147483648.0) ? (int)v : (-2147483647 - 1);
+}
+
+__device__ __forceinline__ float ps_row(const float* r, int stride, float x, float y, float z)
+{
+    return (r[0] * x + r[stride] * y) + r[2 * stride] * z;   // OpenCV 3.x gemm small-matrix order
+}
+
+struct PsCam {
+    float R[9], t[3], Ow[3];
+    int fwd, bwd;
+};
+
+__device__ __forceinline__ PsCam ps_camera(int mode, const float* __restrict__ pose, const orbm_pose_params& P)
+{
+    PsCam c;
+    if (mode == ORBM_PROJ_SIM3 || mode == ORBM_FUSE_SIM3) {   // Decompose Scw (:298-303)
+        double d = 0.0;
+        for (int k = 0; k < 3; ++k) d += (double)pose[k] * (double)pose[k];
+        const float scw = (float)__builtin_sqrt(d);
+        const float s = (float)(1.0 / (double)scw);
+        for (int r = 0; r < 3; ++r) {
+            for (int k = 0; k < 3; ++k) c.R[3 * r + k] = pose[4 * r + k] * s + 0.0f;
+            c.t[r] = pose[4 * r + 3] * s + 0.0f;
+        }
+    } else {
+        for (int r = 0; r < 3; ++r) {
+            for (int k = 0; k < 3; ++k) c.R[3 * r + k] = pose[4 * r + k];
+            c.t[r] = pose[4 * r + 3];
+        }
+    }
+    for (int r = 0; r < 3; ++r) c.Ow[r] = -ps_row(c.R + r, 3, c.t[0], c.t[1], c.t[2]);   // -Rcw.t()*tcw
+    c.fwd = c.bwd = 0;
+    if (mode == ORBM_PROJ_LAST_FRAME) {   // tlc = Rlw*twc+tlw (:1409-1417)
+        const float tlc2 = ps_row(pose + 20, 1, c.Ow[0], c.Ow[1], c.Ow[2]) + pose[23];
+        c.fwd = tlc2 > P.b && !P.mono;
+        c.bwd = -tlc2 > P.b && !P.mono;
+    }
+    return c;
+}
+
+struct PsWin {
+    float u, v, r, ur;
+    int minLevel, maxLevel, cy0, cy1, lo, hi;
+};
+
+// MapPoint::PredictScale (src/MapPoint.cc:385-417)
+__device__ __forceinline__ int ps_predict_scale(float max_dist, float dist, const orbm_pose_params& P)
+{
+    const float ratio = max_dist / dist;
+    int n = ps_x86_int(__builtin_ceil(log((double)ratio) / (double)P.log_scale));
+    if (n < 0) n = 0;
+    else if (n >= P.nlevels) n = P.nlevels - 1;
+    return n;
+}
+
+// the per-MapPoint part before GetFeaturesInArea; false where the reference `continue`s
+template <int MODE>
+__device__ __forceinline__ bool ps_project(const PsCam& c, const orbm_map_point& M, const orbm_pose_params& P,
+                                           PsWin& w)
+{
+    const float X = M.x, Y = M.y, Z = M.z;
+    const float xc = ps_row(c.R, 1, X, Y, Z) + c.t[0];
+    const float yc = ps_row(c.R + 3, 1, X, Y, Z) + c.t[1];
+    const float zc = ps_row(c.R + 6, 1, X, Y, Z) + c.t[2];
+    w.ur = 0.0f;
+    if (MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME) {
+        const float invzc = (float)(1.0 / (double)zc);
+        if (MODE == ORBM_PROJ_LAST_FRAME && invzc < 0) return false;
+        const float u = __builtin_fmaf(P.fx * xc, invzc, P.cx);   // fx*xc*invzc+cx
+        const float v = __builtin_fmaf(P.fy * yc, invzc, P.cy);
+        if (u < P.min_x || u > P.max_x) return false;
+        if (v < P.min_y || v > P.max_y) return false;
+        w.u = u;
+        w.v = v;
+        if (MODE == ORBM_PROJ_LAST_FRAME) {   // :1446-1458
+            const int L = M.octave & 15;
+            w.r = P.th * P.scale[L];
+            if (c.fwd) { w.minLevel = L; w.maxLevel = -1; }
+            else if (c.bwd) { w.minLevel = 0; w.maxLevel = L; }
+            else { w.minLevel = L - 1; w.maxLevel = L + 1; }
+            w.ur = __builtin_fmaf(-P.bf, invzc, u);   // u - mbf*invzc
+            return true;
+        }
+    } else {
+        if (zc < 0.0f) return false;
+        const float invz = MODE == ORBM_FUSE_SIM3 ? (float)(1.0 / (double)zc) : 1.0f / zc;
+        const float x = xc * invz, y = yc * invz;
+        const float u = __builtin_fmaf(P.fx, x, P.cx);
+        const float v = __builtin_fmaf(P.fy, y, P.cy);
+        if (!(u >= P.min_x && u < P.max_x && v >= P.min_y && v < P.max_y)) return false;   // IsInImage
+        w.u = u;
+        w.v = v;
+        if (MODE == ORBM_FUSE) w.ur = __builtin_fmaf(-P.bf, invz, u);
+    }
+    const float maxD = 1.2f * M.max_dist, minD = 0.8f * M.min_dist;
+    const float PO0 = X - c.Ow[0], PO1 = Y - c.Ow[1], PO2 = Z - c.Ow[2];
+    double s = 0.0;
+    s += (double)PO0 * (double)PO0;
+    s += (double)PO1 * (double)PO1;
+    s += (double)PO2 * (double)PO2;
+    const float dist = (float)__builtin_sqrt(s);   // cv::norm(PO)
+    if (dist < minD || dist > maxD) return false;
+    if (MODE != ORBM_PROJ_KEYFRAME) {   // PO.dot(Pn) < 0.5*dist
+        double dot = 0.0;
+        dot += (double)PO0 * (double)M.nx;
+        dot += (double)PO1 * (double)M.ny;
+        dot += (double)PO2 * (double)M.nz;
+        if (dot < 0.5 * (double)dist) return false;
+    }
+    const int L = ps_predict_scale(M.max_dist, dist, P);
+    w.r = P.th * P.scale[L & 15];
+    w.minLevel = L - 1;
+    w.maxLevel = MODE == ORBM_PROJ_KEYFRAME ? L + 1 : L;
+    return true;
+}
+
+__device__ __forceinline__ bool ps_window(PsWin& w, const orbm_pose_params& P, const uint32_t* keys, int ng)
+{
+    const int cx0 = max(0, ps_x86_int(floorf((w.u - P.min_x - w.r) * P.grid_w_inv)));
+    if (cx0 >= kPjCols) return false;
+    const int cx1 = min(kPjCols - 1, ps_x86_int(ceilf((w.u - P.min_x + w.r) * P.grid_w_inv)));
+    if (cx1 < 0) return false;
+    w.cy0 = max(0, ps_x86_int(floorf((w.v - P.min_y - w.r) * P.grid_h_inv)));
+    if (w.cy0 >= kPjRows) return false;
+    w.cy1 = min(kPjRows - 1, ps_x86_int(ceilf((w.v - P.min_y + w.r) * P.grid_h_inv)));
+    if (w.cy1 < 0) return false;
+    w.lo = pj_lower_bound(keys, ng, (uint32_t)(cx0 * kPjRows) << 16);
+    w.hi = pj_lower_bound(keys, ng, (uint32_t)((cx1 + 1) * kPjRows) << 16);
+    return true;
+}
+
+// feature index at key position p if it passes the mode's window / level / stereo tests
+template <int MODE>
+__device__ __forceinline__ int ps_candidate(const PsWin& w, const uint32_t* keys, int p, const orbx_keypoint* K,
+                                            const float* U, const orbm_pose_params& P)
+{
+    const uint32_t key = keys[p];
+    const int iy = (int)(key >> 16) % kPjRows;
+    if (iy < w.cy0 || iy > w.cy1) return -1;
+    const int idx = (int)(key & 0xFFFF);
+    const orbx_keypoint kp = K[idx];
+    if (kp.octave < w.minLevel) return -1;
+    if (w.maxLevel >= 0 && kp.octave > w.maxLevel) return -1;
+    const float distx = kp.x - w.u, disty = kp.y - w.v;
+    if (!(fabsf(distx) < w.r && fabsf(disty) < w.r)) return -1;
+    if (MODE == ORBM_PROJ_LAST_FRAME) {   // :1475-1481
+        const float ur = U[idx];
+        if (ur > 0 && fabsf(w.ur - ur) > w.r) return -1;
+    }
+    if (MODE == ORBM_FUSE) {   // :982-1006
+        const float ur = U[idx];
+        const float ex = w.u - kp.x, ey = w.v - kp.y;
+        const float is2 = P.inv_sigma2[kp.octave & 15];
+        if (ur >= 0) {
+            const float er = w.ur - ur;
+            const float e2 = __builtin_fmaf(er, er, __builtin_fmaf(ex, ex, ey * ey));
+            if ((double)(e2 * is2) > 7.8) return -1;
+        } else {
+            const float e2 = __builtin_fmaf(ex, ex, ey * ey);
+            if ((double)(e2 * is2) > 5.99) return -1;
+        }
+    }
+    return idx;
+}
+
+template <int MODE>
+__device__ __forceinline__ int ps_threshold(const orbm_pose_params& P)
+{
+    return MODE == ORBM_PROJ_LAST_FRAME ? 100 : (MODE == ORBM_PROJ_KEYFRAME ? P.orb_dist : 50);   // TH_HIGH / TH_LOW
+}
+
+struct PsResult {
+    int best, accept;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_ps_points(const orbx_keypoint* __restrict__ kps,
+                                                   const uint8_t* __restrict__ desc, const float* __restrict__ uright,
+                                                   const uint8_t* __restrict__ claimed, int cap,
+                                                   const float* __restrict__ pose, const orbm_map_point* __restrict__ pts,
+                                                   const uint8_t* __restrict__ pdesc, const int* __restrict__ npts,
+                                                   int pcap, orbm_pose_params P, const uint32_t* __restrict__ gkeys,
+                                                   const int* __restrict__ gn, PsResult* __restrict__ res,
+                                                   int* __restrict__ match, int* __restrict__ nmatches)
+{
+    constexpr bool kSearch = MODE <= ORBM_PROJ_SIM3;
+    const int f = blockIdx.y, m = blockIdx.x * 256 + threadIdx.x;
+    if (m >= min(npts[f], pcap)) return;
+    const size_t mo = (size_t)f * pcap + m;
+    int bestIdx = -1, accept = 0;
+    const orbm_map_point M = pts[mo];
+    if (M.flags & 1) {
+        const PsCam c = ps_camera(MODE, pose + (size_t)f * 24, P);
+        const uint32_t* keys = gkeys + (size_t)f * cap;
+        PsWin w;
+        if (ps_project<MODE>(c, M, P, w) && ps_window(w, P, keys, gn[f])) {
+            const orbx_keypoint* K = kps + (size_t)f * cap;
+            const float* U = uright + (size_t)f * cap;
+            const uint8_t* C = claimed + (size_t)f * cap;
+            const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
+            const uint4 q0 = qd[0], q1 = qd[1];
+            int bestDist = 256;
+            for (int p = w.lo; p < w.hi; ++p) {
+                const int idx = ps_candidate<MODE>(w, keys, p, K, U, P);
+                if (idx < 0 || (kSearch && C[idx])) continue;
+                const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
+                const int dist = pj_ham(q0, q1, d[0], d[1]);
+                if (dist < bestDist) {
+                    bestDist = dist;
+                    bestIdx = idx;
+                }
+            }
+            accept = bestIdx >= 0 && bestDist <= ps_threshold<MODE>(P);
+        }
+    }
+    if (kSearch) {
+        res[mo] = PsResult{bestIdx, accept};
+    } else {
+        match[mo] = accept ? bestIdx : -1;
+        if (accept) atomicAdd(&nmatches[f], 1);
+    }
+}
+
+__device__ __forceinline__ int ps_rot_bin(float a1, float a2)
+{
+    const float factor = 1.0f / 30;   // 1/HISTO_LENGTH
+    float rot = a1 - a2;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == 30) bin = 0;
+    return bin;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restrict__ kps,
+                                                   const uint8_t* __restrict__ desc, const float* __restrict__ uright,
+                                                   const uint8_t* __restrict__ claimed, const int* __restrict__ counts,
+                                                   int cap, const float* __restrict__ pose,
+                                                   const orbm_map_point* __restrict__ pts,
+                                                   const uint8_t* __restrict__ pdesc, const int* __restrict__ npts,
+                                                   int pcap, orbm_pose_params P, const uint32_t* __restrict__ gkeys,
+                                                   const int* __restrict__ gn, const PsResult* __restrict__ res,
+                                                   int* __restrict__ ent, int* __restrict__ match,
+                                                   int* __restrict__ nmatches)
+{
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int n = min(counts[f], cap), np = min(npts[f], pcap);
+    int* Mo = match + (size_t)f * cap;
+    for (int i = lane; i < n; i += 64) Mo[i] = -1;
+    __threadfence();
+    unsigned long long bits[kPjBitWords] = {0ull, 0ull};   // features claimed during this call
+    const uint32_t* keys = gkeys + (size_t)f * cap;
+    const orbx_keypoint* K = kps + (size_t)f * cap;
+    const float* U = uright + (size_t)f * cap;
+    const uint8_t* C = claimed + (size_t)f * cap;
+    const int ng = gn[f];
+    const PsCam cam = ps_camera(MODE, pose + (size_t)f * 24, P);
+    const bool rot = P.check_ori && (MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME);
+    int* E = ent + (size_t)f * pcap;
+    auto claimed_now = [&](int idx) -> bool {   // wave-uniform idx
+        const int word = idx >> 6, w = word & 63, h = word >> 6;
+        const unsigned long long b =
+            (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits[h], w) |
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits[h] >> 32), w) << 32);
+        return (b >> (idx & 63)) & 1ull;
+    };
+    int count = 0, nent = 0, hist = 0;   // lane b holds rotHist[b].size()
+    for (int base = 0; base < np; base += 64) {
+        const int mm = base + lane;
+        PsResult R{-1, 0};
+        int obs = 0;
+        float ang = 0.0f;
+        if (mm < np) {
+            R = res[(size_t)f * pcap + mm];
+            const orbm_map_point& Mp = pts[(size_t)f * pcap + mm];
+            obs = MODE != ORBM_PROJ_LAST_FRAME || (Mp.flags & 2);
+            ang = Mp.angle;
+        }
+        const int cnt = min(64, np - base);
+        for (int j = 0; j < cnt; ++j) {
+            int best = __builtin_amdgcn_readlane(R.best, j);
+            int accept = __builtin_amdgcn_readlane(R.accept, j);
+            if (best < 0) continue;   // no candidate on entry: claims only remove candidates
+            if (claimed_now(best)) {
+                const int m = base + j;
+                const size_t mo = (size_t)f * pcap + m;
+                const orbm_map_point Mp = pts[mo];
+                PsWin w;
+                ps_project<MODE>(cam, Mp, P, w);   // true and non-empty: J2 found `best` in it
+                ps_window(w, P, keys, ng);
+                const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
+                const uint4 q0 = qd[0], q1 = qd[1];
+                unsigned long long b1 = ~0ull;
+                for (int p0 = w.lo; p0 < w.hi; p0 += 64) {
+                    const int p = p0 + lane;
+                    unsigned long long key = ~0ull;
+                    int idx = -1;
+                    if (p < w.hi) {
+                        idx = ps_candidate<MODE>(w, keys, p, K, U, P);
+                        if (idx >= 0 && !C[idx]) {
+                            const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
+                            const int dist = pj_ham(q0, q1, d[0], d[1]);
+                            key = ((unsigned long long)dist << 32) | ((unsigned long long)p << 16) | (unsigned)idx;
+                        }
+                    }
+                    unsigned long long live = __ballot(key != ~0ull);
+                    while (live) {
+                        const int l = __builtin_ctzll(live);
+                        live &= live - 1;
+                        const int cidx = __builtin_amdgcn_readlane(idx, l);
+                        if (claimed_now(cidx) && lane == l) key = ~0ull;
+                    }
+                    const unsigned long long c1 = pj_wave_min_u64(key);
+                    b1 = c1 < b1 ? c1 : b1;
+                }
+                best = b1 == ~0ull ? -1 : (int)(b1 & 0xFFFF);
+                accept = best >= 0 && (int)(b1 >> 32) <= ps_threshold<MODE>(P);
+            }
+            if (best < 0 || !accept) continue;
+            if (lane == 0) Mo[best] = base + j;   // mvpMapPoints[bestIdx] = pMP
+            ++count;
+            if (__builtin_amdgcn_readlane(obs, j)) {
+                const int word = best >> 6;
+                if (lane == (word & 63)) bits[word >> 6] |= 1ull << (best & 63);
+            }
+            if (rot) {
+                const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), j));
+                const int bin = ps_rot_bin(a1, K[best].angle);
+                if (lane == 0) E[nent] = (best << 8) | bin;
+                ++nent;
+                hist += lane == bin;
+            }
+        }
+    }
+    if (rot) {   // ComputeThreeMaxima (:1679-1723) and the NULL-ing of the other bins
+        __threadfence();
+        int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;
+        for (int i = 0; i < 30; ++i) {
+            const int s = __builtin_amdgcn_readlane(hist, i);
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
+        int removed = 0;
+        for (int e = lane; e < nent; e += 64) {
+            const int v = E[e], bin = v & 255;
+            if (bin != ind1 && bin != ind2 && bin != ind3) {
+                Mo[v >> 8] = -2;
+                ++removed;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) removed += __shfl_xor(removed, o);
+        count -= removed;
+    }
+    if (lane == 0) nmatches[f] = count;
+}
+
+size_t pose_scratch_bytes(int nframes, int cap, int pcap)
+{
+    return (size_t)nframes * cap * 4 + (size_t)nframes * 4 + (size_t)nframes * pcap * (sizeof(PsResult) + 4) + 256;
+}
+
+template <int MODE>
+static void ps_launch(const orbx_keypoint* kps, const uint8_t* desc, const float* uright, const uint8_t* claimed,
+                      const int* counts, int nframes, int cap, const float* pose, const orbm_map_point* pts,
+                      const uint8_t* pdesc, const int* npts, int pcap, const orbm_pose_params& P,
+                      const uint32_t* gkeys, const int* gn, PsResult* res, int* ent, int* match, int* nmatches,
+                      hipStream_t s)
+{
+    if (MODE >= ORBM_FUSE) hipMemsetAsync(nmatches, 0, sizeof(int) * (size_t)nframes, s);
+    hipLaunchKernelGGL(k_ps_points<MODE>, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright,
+                       claimed, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+    if (MODE <= ORBM_PROJ_SIM3)
+        hipLaunchKernelGGL(k_ps_resolve<MODE>, dim3(nframes), dim3(64), 0, s, kps, desc, uright, claimed, counts, cap,
+                           pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, ent, match, nmatches);
+}
+
+void launch_pose_search(int mode, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,
+                        const uint8_t* claimed, const int* counts, int nframes, int cap, const float* pose,
+                        const orbm_map_point* pts, const uint8_t* pdesc, const int* npts, int pcap,
+                        const orbm_pose_params& P, void* scratch, int* match, int* nmatches, hipStream_t s)
+{
+    uint32_t* gkeys = (uint32_t*)scratch;
+    int* gn = (int*)(gkeys + (size_t)nframes * cap);
+    PsResult* res = (PsResult*)(((uintptr_t)(gn + nframes) + 15) & ~(uintptr_t)15);
+    int* ent = (int*)(res + (size_t)nframes * pcap);
+    int p2 = 1;
+    while (p2 < cap) p2 <<= 1;
+    hipFuncSetAttribute((const void*)k_pj_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * p2));
+    hipLaunchKernelGGL(k_pj_grid, dim3(nframes), dim3(256), (size_t)4 * p2, s, kps, counts, cap, P.min_x, P.min_y,
+                       P.grid_w_inv, P.grid_h_inv, gkeys, gn);
+    switch (mode) {
+    case ORBM_PROJ_LAST_FRAME:
+        ps_launch<ORBM_PROJ_LAST_FRAME>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap,
+                                        P, gkeys, gn, res, ent, match, nmatches, s);
+        break;
+    case ORBM_PROJ_KEYFRAME:
+        ps_launch<ORBM_PROJ_KEYFRAME>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap,
+                                      P, gkeys, gn, res, ent, match, nmatches, s);
+        break;
+    case ORBM_PROJ_SIM3:
+        ps_launch<ORBM_PROJ_SIM3>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap, P,
+                                  gkeys, gn, res, ent, match, nmatches, s);
+        break;
+    case ORBM_FUSE:
+        ps_launch<ORBM_FUSE>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap, P, gkeys,
+                             gn, res, ent, match, nmatches, s);
+        break;
+    default:
+        ps_launch<ORBM_FUSE_SIM3>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap, P,
+                                  gkeys, gn, res, ent, match, nmatches, s);
+        break;
+    }
 }
 
 }  // namespace orbx

@@ -37,6 +37,7 @@ EXPORTED = [
     "orbm_search_init_batch_device", "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
     "orbm_bow_search_device", "orbm_bow_search",
     "orbm_search_by_projection_device", "orbm_search_by_projection",
+    "orbm_project_search_device", "orbm_project_search",
     "orbv_load_text", "orbv_create", "orbv_destroy", "orbv_info", "orbv_transform", "orbv_transform_batch_device",
 ]
 BOW_KF_F, BOW_KF_KF, TRIANGULATION = 0, 1, 2
@@ -78,6 +79,49 @@ def proj_params(grid, scale, th=1.0, nnratio=0.8):
     sc = np.zeros(16, np.float32)
     sc[:len(scale)] = scale
     pp.scale[:] = [float(x) for x in sc]
+    return pp
+
+
+PROJ_LAST_FRAME, PROJ_KEYFRAME, PROJ_SIM3, FUSE, FUSE_SIM3 = 0, 1, 2, 3, 4
+
+MAP_POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                            ("max_dist", "<f4"), ("min_dist", "<f4"), ("angle", "<f4"), ("octave", "<i4"),
+                            ("flags", "<i4"), ("pad", "<i4")])
+
+
+class PoseParams(C.Structure):
+    """orbm_pose_params (camera, image bounds, grid, scale pyramid, the search arguments)."""
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("b", C.c_float), ("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float),
+                ("max_y", C.c_float), ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float),
+                ("log_scale", C.c_float), ("nlevels", C.c_int32), ("th", C.c_float), ("mono", C.c_int32),
+                ("orb_dist", C.c_int32), ("check_ori", C.c_int32), ("scale", C.c_float * 16),
+                ("inv_sigma2", C.c_float * 16)]
+
+
+def pose_params(K, bounds, scale, inv_sigma2=None, log_scale=None, bf=0.0, th=1.0, mono=False, orb_dist=100,
+                check_ori=True):
+    """K = (fx, fy, cx, cy); bounds = (mnMinX, mnMaxX, mnMinY, mnMaxY); scale = mvScaleFactors.
+    The grid cell sizes follow Frame's constructor (64 x 48 cells over the bounds);
+    log_scale defaults to (float)log(scale[1]) like Frame::mfLogScaleFactor."""
+    pp = PoseParams()
+    pp.fx, pp.fy, pp.cx, pp.cy = (float(v) for v in K)
+    pp.bf = float(bf)
+    pp.b = float(np.float32(bf) / np.float32(K[0])) if K[0] else 0.0
+    pp.min_x, pp.max_x, pp.min_y, pp.max_y = (float(v) for v in bounds)
+    pp.grid_w_inv = float(np.float32(64) / np.float32(np.float32(bounds[1]) - np.float32(bounds[0])))
+    pp.grid_h_inv = float(np.float32(48) / np.float32(np.float32(bounds[3]) - np.float32(bounds[2])))
+    sc = np.zeros(16, np.float32)
+    sc[:len(scale)] = scale
+    pp.scale[:] = [float(x) for x in sc]
+    pp.nlevels = len(scale)
+    if inv_sigma2 is None:
+        inv_sigma2 = np.float32(1) / (np.asarray(scale, np.float32) * np.asarray(scale, np.float32))
+    s2 = np.zeros(16, np.float32)
+    s2[:len(inv_sigma2)] = inv_sigma2
+    pp.inv_sigma2[:] = [float(x) for x in s2]
+    pp.log_scale = float(np.float32(np.log(np.float64(np.float32(scale[1]))))) if log_scale is None else log_scale
+    pp.th, pp.mono, pp.orb_dist, pp.check_ori = float(th), int(bool(mono)), int(orb_dist), int(bool(check_ori))
     return pp
 
 
@@ -126,6 +170,10 @@ def _load():
                                                    P(ProjParams), vp, vp, vp]
     L.orbm_search_by_projection.argtypes = [C.c_int, vp, u8p, f32p, u8p, C.c_int, vp, u8p, C.c_int, P(ProjParams),
                                             i32p, i32p]
+    L.orbm_project_search_device.argtypes = [C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, vp, vp, vp, vp, C.c_int,
+                                             P(PoseParams), vp, vp, vp]
+    L.orbm_project_search.argtypes = [C.c_int, C.c_int, vp, u8p, f32p, u8p, C.c_int, f32p, vp, u8p, C.c_int,
+                                      P(PoseParams), i32p, i32p]
     L.orbm_bow_search_device.argtypes = [C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, C.c_int, vp, C.c_int,
                                          vp, vp]
     L.orbm_bow_search.argtypes = [C.c_int, C.c_int, P(BowView), P(BowView), P(TriangParams), C.c_float, C.c_int,
@@ -365,7 +413,7 @@ class ORBmatcher:
         return bow_search(TRIANGULATION, v1, v2, tp, self.mfNNratio, self.mbCheckOrientation, device)
 
     def SearchByProjection(self, kps, desc, uright, claimed, grid, scale, pts, pdesc, th=1.0, device=0):
-        """SearchByProjection(Frame& F, vector<MapPoint*>, th) (src/ORBmatcher.cc:44-129).
+        """SearchByProjection(Frame& F, vector<MapPoint*>, th) (src/ORBmatcher.cc:45-129).
         kps = F.mvKeysUn, uright = F.mvuRight, claimed[i] = F.mvpMapPoints[i] && Observations() > 0,
         grid = (mnMinX, mnMinY, mfGridElementWidthInv, mfGridElementHeightInv), scale = mvScaleFactors,
         pts: PROJ_POINT_DTYPE per MapPoint, pdesc its descriptors.  Returns (nmatches, match[n])."""
@@ -384,6 +432,65 @@ class ORBmatcher:
                                              _u8(cl), n, pp.ctypes.data, _u8(pd), len(pp), C.byref(prm),
                                              out.ctypes.data_as(C.POINTER(C.c_int)), C.byref(nm)))
         return nm.value, out[:n].copy()
+
+    def project_search(self, mode, kps, desc, uright, claimed, pose, pts, pdesc, params, device=0):
+        """The pose-projection searches (include/orbx.h ORBM_PROJ_* / ORBM_FUSE*) on host arrays.
+        pose: Tcw (Scw for the Sim3 modes) 3x4 [+ LastFrame Tcw 3x4]; pts: MAP_POINT_DTYPE;
+        params: PoseParams (check_ori is taken from this matcher).  Returns (n, match)."""
+        k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+        d = np.ascontiguousarray(desc, np.uint8)
+        ur = np.ascontiguousarray(uright, np.float32)
+        cl = np.ascontiguousarray(claimed if claimed is not None else np.zeros(len(k), np.uint8), np.uint8)
+        ps = np.zeros(24, np.float32)
+        pz = np.asarray(pose, np.float32).ravel()
+        ps[:len(pz)] = pz
+        pp = np.ascontiguousarray(pts, MAP_POINT_DTYPE)
+        pd = np.ascontiguousarray(pdesc, np.uint8)
+        nout = len(k) if mode <= PROJ_SIM3 else len(pp)
+        out = np.full(max(nout, 1), -1, np.int32)
+        nm = C.c_int(0)
+        prm = PoseParams.from_buffer_copy(params)
+        prm.check_ori = int(self.mbCheckOrientation)
+        f32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
+        _check("orbm_project_search",
+               lib.orbm_project_search(device, mode, k.ctypes.data, _u8(d), f32(ur), _u8(cl), len(k), f32(ps),
+                                       pp.ctypes.data, _u8(pd), len(pp), C.byref(prm),
+                                       out.ctypes.data_as(C.POINTER(C.c_int)), C.byref(nm)))
+        return nm.value, out[:nout].copy()
+
+    def SearchByProjectionLastFrame(self, cur, last_pts, last_pdesc, Tcw, Tlw, params, th, bMono, device=0):
+        """SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono) (src/ORBmatcher.cc:1396-1538).
+        cur = (mvKeysUn, mDescriptors, mvuRight, taken) with taken[i] = mvpMapPoints[i] && Observations() > 0."""
+        prm = PoseParams.from_buffer_copy(params)
+        prm.th, prm.mono = float(th), int(bool(bMono))
+        pose = np.concatenate([np.asarray(Tcw, np.float32).reshape(-1)[:12], np.asarray(Tlw, np.float32).reshape(-1)[:12]])
+        return self.project_search(PROJ_LAST_FRAME, cur[0], cur[1], cur[2], cur[3], pose, last_pts, last_pdesc, prm,
+                                   device)
+
+    def SearchByProjectionKeyFrame(self, cur, kf_pts, kf_pdesc, Tcw, params, th, ORBdist, device=0):
+        """SearchByProjection(Frame& CurrentFrame, KeyFrame*, sAlreadyFound, th, ORBdist) (:1540-1667).
+        taken[i] = CurrentFrame.mvpMapPoints[i] != NULL."""
+        prm = PoseParams.from_buffer_copy(params)
+        prm.th, prm.orb_dist = float(th), int(ORBdist)
+        return self.project_search(PROJ_KEYFRAME, cur[0], cur[1], cur[2], cur[3], Tcw, kf_pts, kf_pdesc, prm, device)
+
+    def SearchByProjectionSim3(self, kf, pts, pdesc, Scw, params, th, device=0):
+        """SearchByProjection(KeyFrame*, Scw, vpPoints, vpMatched, th) (:290-403); taken[i] = vpMatched[i]."""
+        prm = PoseParams.from_buffer_copy(params)
+        prm.th = float(int(th))
+        return self.project_search(PROJ_SIM3, kf[0], kf[1], kf[2], kf[3], Scw, pts, pdesc, prm, device)
+
+    def Fuse(self, kf, pts, pdesc, Tcw, params, th=3.0, device=0):
+        """Fuse(KeyFrame*, vpMapPoints, th) (:893-1043): per MapPoint the KeyFrame feature it fuses into."""
+        prm = PoseParams.from_buffer_copy(params)
+        prm.th = float(th)
+        return self.project_search(FUSE, kf[0], kf[1], kf[2], None, Tcw, pts, pdesc, prm, device)
+
+    def FuseSim3(self, kf, pts, pdesc, Scw, params, th, device=0):
+        """Fuse(KeyFrame*, Scw, vpPoints, th, vpReplacePoint) (:1045-1168)."""
+        prm = PoseParams.from_buffer_copy(params)
+        prm.th = float(th)
+        return self.project_search(FUSE_SIM3, kf[0], kf[1], kf[2], None, Scw, pts, pdesc, prm, device)
 
     def search_for_initialization_batch(self, kps, desc, counts, pair_a, pair_b, rows, cols, window=100,
                                         matches12=None, nmatches=None, stream=None):

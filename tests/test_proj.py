@@ -1,5 +1,5 @@
 """Projection search, SURVEY.md §8f row 3:
-  ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, th)  src/ORBmatcher.cc:44-129
+  ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, th)  src/ORBmatcher.cc:45-129
   (Tracking::SearchLocalPoints, src/Tracking.cc:1234-1244) over Frame::GetFeaturesInArea.
 
 The per-MapPoint inputs are what Frame::isInFrustum leaves in the MapPoint (projection,
