@@ -308,6 +308,28 @@ orbx_status orbm_project_search(int device, int mode, const orbx_keypoint* kps, 
                                 const orbm_map_point* pts, const uint8_t* pdesc, int np,
                                 const orbm_pose_params* params, int* match, int* nmatches);
 
+/* ---- Image ingest ----
+ * The per-frame preparation in front of ORBextractor::operator():
+ *   cv::remap(im, imRect, M1, M2, cv::INTER_LINEAR) with the CV_32F maps of initUndistortRectifyMap and the
+ *   default BORDER_CONSTANT 0 (Examples/Stereo/stereo_euroc.cc:97-98, 136-137), applied per channel, then
+ *   cvtColor(CV_RGB2GRAY / CV_BGR2GRAY / CV_RGBA2GRAY / CV_BGRA2GRAY) for 3- and 4-channel input
+ *   (Tracking::GrabImageStereo / GrabImageRGBD / GrabImageMonocular, src/Tracking.cc:180-270).
+ * Frame f: d_src + f * src_frame_stride, rows x cols, `channels` (1, 3, 4) interleaved u8, row pitch
+ * src_step; rgb = Tracking::mbRGB.  Maps: NULL for no remap (dst_rows x dst_cols must equal rows x cols),
+ * else nmaps pairs of dst_rows x dst_cols floats, frame f using pair f % nmaps (2 for a batch holding
+ * L0 R0 L1 R1 ...).  Output: gray u8 at d_dst + f * dst_frame_stride, pitch dst_step -- the input
+ * layout of orbx_extract_batch_device.  Asynchronous on `stream`. */
+orbx_status orbx_ingest_batch_device(const uint8_t* d_src, int batch, int rows, int cols, int channels, int rgb,
+                                     size_t src_step, size_t src_frame_stride, const float* d_map_x,
+                                     const float* d_map_y, int nmaps, int dst_rows, int dst_cols, uint8_t* d_dst,
+                                     size_t dst_step, size_t dst_frame_stride, void* stream);
+
+/* GrabImageRGBD's imDepth.convertTo(imDepth, CV_32F, mDepthMapFactor) (src/Tracking.cc:234-235; the caller
+ * keeps the reference's condition for calling it).  depth_type 0: u16, 1: f32 input. */
+orbx_status orbx_depth_batch_device(const void* d_src, int depth_type, int batch, int rows, int cols,
+                                    size_t src_step, size_t src_frame_stride, float factor, float* d_dst,
+                                    size_t dst_step, size_t dst_frame_stride, void* stream);
+
 /* ---- DBoW2 vocabulary (TemplatedVocabulary, Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) ----
  * Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:521-528, src/KeyFrame.cc:59-66) call
  * transform(descriptors, mBowVec, mFeatVec, 4); the FeatureVector it produces is the

@@ -1678,3 +1678,63 @@ int orbref_project_search(int mode, const orbref_keypoint* kps, const uint8_t* d
     free(cnt); free(cellOf); free(cells); free(fill); free(claimed); free(ent_idx); free(ent_bin);
     return nmatches;
 }
+
+/* ---- §8f row 4: image ingest (remap INTER_LINEAR + cvtColor to gray, depth convertTo) ---- */
+
+/* cvRound(float) on x86-64 (cvtss2si): ties to even; NaN and out of range give INT_MIN */
+static inline int cv_round_x86(float v)
+{
+    return (v >= -2147483648.0f && v < 2147483648.0f) ? (int)lrintf(v) : INT_MIN;
+}
+
+static inline int sat_short(int v) { return v < SHRT_MIN ? SHRT_MIN : (v > SHRT_MAX ? SHRT_MAX : v); }
+
+void orbref_ingest(const uint8_t* src, int rows, int cols, int channels, int rgb, size_t src_step,
+                   const float* map_x, const float* map_y, int dst_rows, int dst_cols, uint8_t* dst,
+                   size_t dst_step)
+{
+    /* RGB2Gray<uchar> (color.cpp): tab[src[0]] + tab[src[1]+256] + tab[src[2]+512], the rounding
+     * constant folded into the third table; blueIdx 0 (BGR) weights src[0] with B2Y */
+    const int w0 = rgb ? 4899 : 1868, w1 = 9617, w2 = rgb ? 1868 : 4899;
+    if (!map_x) { dst_rows = rows; dst_cols = cols; }
+    for (int y = 0; y < dst_rows; y++) {
+        for (int x = 0; x < dst_cols; x++) {
+            int val[4] = {0, 0, 0, 0};
+            if (map_x) {   /* RemapInvoker: XY = cvRound(m*INTER_TAB_SIZE) >> INTER_BITS, A = fractions */
+                const int sx32 = cv_round_x86(map_x[(size_t)y * dst_cols + x] * 32.0f);
+                const int sy32 = cv_round_x86(map_y[(size_t)y * dst_cols + x] * 32.0f);
+                const int fx = sx32 & 31, fy = sy32 & 31;
+                const int sx = sat_short(sx32 >> 5), sy = sat_short(sy32 >> 5);
+                /* BilinearTab_i: (1-fy, fy) x (1-fx, fx) in 1/32 steps, scaled by 2^15.  The (0,0) entry
+                 * saturates to 32767 in OpenCV; for u8 sources that cannot change a result. */
+                const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
+                const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
+                const int in_x0 = sx >= 0 && sx < cols, in_x1 = sx + 1 >= 0 && sx + 1 < cols;
+                const int in_y0 = sy >= 0 && sy < rows, in_y1 = sy + 1 >= 0 && sy + 1 < rows;
+                for (int k = 0; k < channels; k++) {   /* remapBilinear, BORDER_CONSTANT cval 0 */
+                    const int v00 = in_x0 && in_y0 ? src[(size_t)sy * src_step + (size_t)sx * channels + k] : 0;
+                    const int v01 = in_x1 && in_y0 ? src[(size_t)sy * src_step + (size_t)(sx + 1) * channels + k] : 0;
+                    const int v10 = in_x0 && in_y1 ? src[(size_t)(sy + 1) * src_step + (size_t)sx * channels + k] : 0;
+                    const int v11 = in_x1 && in_y1 ? src[(size_t)(sy + 1) * src_step + (size_t)(sx + 1) * channels + k] : 0;
+                    const int s = v00 * w00 + v01 * w01 + v10 * w10 + v11 * w11;
+                    val[k] = sat_u8((s + (1 << 14)) >> 15);
+                }
+            } else {
+                for (int k = 0; k < channels; k++) val[k] = src[(size_t)y * src_step + (size_t)x * channels + k];
+            }
+            const int g = channels == 1 ? val[0] : (val[0] * w0 + val[1] * w1 + val[2] * w2 + (1 << 13)) >> 14;
+            dst[(size_t)y * dst_step + x] = (uint8_t)g;
+        }
+    }
+}
+
+void orbref_depth_convert(const void* src, int depth_type, int rows, int cols, size_t src_step, float factor,
+                          float* dst, size_t dst_step)
+{
+    for (int y = 0; y < rows; y++)
+        for (int x = 0; x < cols; x++) {
+            const uint8_t* row = (const uint8_t*)src + (size_t)y * src_step;
+            const float v = depth_type == 0 ? (float)((const uint16_t*)row)[x] : ((const float*)row)[x];
+            ((float*)((uint8_t*)dst + (size_t)y * dst_step))[x] = v * factor + 0.0f;   /* cvtScale_, WT = float */
+        }
+}

@@ -255,6 +255,21 @@ int orbref_project_search(int mode, const orbref_keypoint* kps, const uint8_t* d
                           const uint8_t* claimed_in, int n, const float* pose, const orbref_map_point* pts,
                           const uint8_t* pdesc, int np, const orbref_pose_params* P, int* match);
 
+/* §8f row 4, image ingest.  cv::remap(src, dst, M1, M2, INTER_LINEAR) with CV_32FC1 maps and the
+ * default BORDER_CONSTANT 0 (Examples/Stereo/stereo_euroc.cc:136-137; OpenCV 3.x RemapInvoker +
+ * remapBilinear, fixed point: coordinates cvRound(m*32), weights (32-f)*..*32, (sum + 2^14) >> 15), then
+ * cvtColor RGB/BGR(A)2GRAY (src/Tracking.cc:185-210; OpenCV 3.x RGB2Gray<uchar>: R 4899, G 9617,
+ * B 1868, (sum + 2^13) >> 14).  map_x == NULL: no remap (dst is rows x cols).  channels 1, 3 or 4;
+ * rgb = Tracking::mbRGB.  dst: dst_rows x dst_cols, pitch dst_step. */
+void orbref_ingest(const uint8_t* src, int rows, int cols, int channels, int rgb, size_t src_step,
+                   const float* map_x, const float* map_y, int dst_rows, int dst_cols, uint8_t* dst,
+                   size_t dst_step);
+
+/* GrabImageRGBD: imDepth.convertTo(imDepth, CV_32F, mDepthMapFactor) (src/Tracking.cc:234-235):
+ * (float)d * factor + 0.0f for u16 (depth_type 0) or f32 (depth_type 1) input. */
+void orbref_depth_convert(const void* src, int depth_type, int rows, int cols, size_t src_step, float factor,
+                          float* dst, size_t dst_step);
+
 /* Config-5 brute force: per query best index (first min), best and second distance. */
 void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                           int* best_idx, int* best_d, int* second_d);

@@ -117,6 +117,12 @@ def lib():
                                                   C.c_float, i32p]
         L.orbref_project_search.argtypes = [C.c_int, C.c_void_p, u8p, f32p, u8p, C.c_int, f32p, C.c_void_p, u8p,
                                             C.c_int, P(PoseParams), i32p]
+        L.orbref_ingest.argtypes = [u8p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_size_t, f32p, f32p, C.c_int, C.c_int,
+                                    u8p, C.c_size_t]
+        L.orbref_ingest.restype = None
+        L.orbref_depth_convert.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_float, f32p,
+                                           C.c_size_t]
+        L.orbref_depth_convert.restype = None
         L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
         _lib = L
     return _lib
@@ -411,6 +417,35 @@ def project_search(mode, kps, desc, uright, claimed, pose, pts, pdesc, params: P
     nm = lib().orbref_project_search(mode, kps.ctypes.data, _u8(desc), _f32(ur), _u8(cl), len(kps), _f32(ps),
                                      pts.ctypes.data, _u8(pd), len(pts), C.byref(params), _i32(out))
     return nm, out[:nout].copy()
+
+
+def ingest(src, rgb=False, map_x=None, map_y=None):
+    """remap(INTER_LINEAR, BORDER_CONSTANT) then cvtColor to gray.  src: (H, W) or (H, W, C) uint8."""
+    src = np.ascontiguousarray(src, np.uint8)
+    rows, cols = src.shape[:2]
+    ch = 1 if src.ndim == 2 else src.shape[2]
+    if map_x is not None:
+        mx = np.ascontiguousarray(map_x, np.float32)
+        my = np.ascontiguousarray(map_y, np.float32)
+        dr, dc = mx.shape
+    else:
+        mx = my = None
+        dr, dc = rows, cols
+    out = np.zeros((dr, dc), np.uint8)
+    lib().orbref_ingest(_u8(src), rows, cols, ch, int(bool(rgb)), cols * ch, _f32(mx) if mx is not None else None,
+                        _f32(my) if my is not None else None, dr, dc, _u8(out), dc)
+    return out
+
+
+def depth_convert(src, factor):
+    src = np.ascontiguousarray(src)
+    dt = 0 if src.dtype == np.uint16 else 1
+    if dt == 1:
+        src = src.astype(np.float32, copy=False)
+    rows, cols = src.shape
+    out = np.zeros((rows, cols), np.float32)
+    lib().orbref_depth_convert(src.ctypes.data, dt, rows, cols, src.strides[0], factor, _f32(out), cols * 4)
+    return out
 
 
 def allpairs_top2(q: np.ndarray, t: np.ndarray):

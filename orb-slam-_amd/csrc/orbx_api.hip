@@ -972,6 +972,40 @@ orbx_status orbm_project_search(int device, int mode, const orbx_keypoint* kps, 
     return rc;
 }
 
+orbx_status orbx_ingest_batch_device(const uint8_t* d_src, int batch, int rows, int cols, int channels, int rgb,
+                                     size_t src_step, size_t src_frame_stride, const float* d_map_x,
+                                     const float* d_map_y, int nmaps, int dst_rows, int dst_cols, uint8_t* d_dst,
+                                     size_t dst_step, size_t dst_frame_stride, void* stream)
+{
+    if (!d_src || !d_dst || batch < 0 || rows <= 0 || cols <= 0 || (channels != 1 && channels != 3 && channels != 4) ||
+        src_step < (size_t)cols * channels || dst_rows <= 0 || dst_cols <= 0 || dst_step < (size_t)dst_cols ||
+        (!d_map_x) != (!d_map_y) || rows > 32767 || cols > 32767)
+        return ORBX_EINVAL;
+    if (d_map_x && nmaps <= 0) return ORBX_EINVAL;
+    if (!d_map_x && (dst_rows != rows || dst_cols != cols)) return ORBX_EINVAL;
+    if (batch > 1 && (src_frame_stride < src_step * rows || dst_frame_stride < dst_step * dst_rows))
+        return ORBX_EINVAL;
+    if (batch == 0) return ORBX_OK;
+    launch_ingest(d_src, batch, rows, cols, channels, rgb ? 1 : 0, src_step, src_frame_stride, d_map_x, d_map_y,
+                  d_map_x ? nmaps : 1, dst_rows, dst_cols, d_dst, dst_step, dst_frame_stride, (hipStream_t)stream);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+orbx_status orbx_depth_batch_device(const void* d_src, int depth_type, int batch, int rows, int cols,
+                                    size_t src_step, size_t src_frame_stride, float factor, float* d_dst,
+                                    size_t dst_step, size_t dst_frame_stride, void* stream)
+{
+    const size_t esz = depth_type == 0 ? 2 : 4;
+    if (!d_src || !d_dst || (depth_type != 0 && depth_type != 1) || batch < 0 || rows <= 0 || cols <= 0 ||
+        src_step < esz * cols || dst_step < 4 * (size_t)cols || src_step % esz || dst_step % 4 ||
+        (batch > 1 && (src_frame_stride < src_step * rows || dst_frame_stride < dst_step * rows)))
+        return ORBX_EINVAL;
+    if (batch == 0) return ORBX_OK;
+    launch_depth(d_src, depth_type, batch, rows, cols, src_step, src_frame_stride, factor, d_dst, dst_step,
+                 dst_frame_stride, (hipStream_t)stream);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b)
 {
     int d = 0;

@@ -1,0 +1,128 @@
+// gfx950 image ingest, SURVEY.md §8f row 4: the per-frame input preparation in front of
+// ORBextractor::operator().
+//
+// I1 k_ingest  cv::remap(src, dst, M1, M2, INTER_LINEAR) with CV_32F maps and the default
+//              BORDER_CONSTANT 0 (Examples/Stereo/stereo_euroc.cc:136-137), per channel, then
+//              cvtColor {RGB,BGR,RGBA,BGRA}2GRAY (Tracking::GrabImage*, src/Tracking.cc:185-210).
+//              One lane produces 4 adjacent output pixels (one dword store).  The maps are shared
+//              by every frame of a batch (nmaps pairs, frame f uses f % nmaps), so after the first
+//              frame they are served from L2 / MALL; HBM traffic is src + dst.
+// I2 k_depth   GrabImageRGBD's imDepth.convertTo(CV_32F, mDepthMapFactor) (src/Tracking.cc:234-235).
+//
+// Arithmetic is OpenCV 3.x's fixed-point path (oracle/orbref.c orbref_ingest): coordinates
+// cvRound(m * 32) split into an integer part (saturated to short) and 5-bit fractions, weights
+// (32-fx)(32-fy)*32 ..., (sum + 2^14) >> 15; gray = (w0*c0 + 9617*c1 + w2*c2 + 2^13) >> 14.
+#include <hip/hip_runtime.h>
+
+#include "orbx_kernels.hpp"
+
+namespace orbx {
+
+__device__ __forceinline__ int ig_round_x86(float v)   // cvRound (cvtss2si): NaN / out of range -> INT_MIN
+{
+    return (v >= -2147483648.0f && v < 2147483648.0f) ? __float2int_rn(v) : (-2147483647 - 1);
+}
+
+template <int CH>
+__device__ __forceinline__ uint32_t ig_pixel(const uint8_t* __restrict__ S, int rows, int cols, size_t sstep,
+                                             const float* __restrict__ mx, const float* __restrict__ my, size_t mo,
+                                             int y, int x, int w0, int w2)
+{
+    int val[CH > 1 ? 3 : 1];
+    if (mx) {
+        const int sx32 = ig_round_x86(mx[mo] * 32.0f);
+        const int sy32 = ig_round_x86(my[mo] * 32.0f);
+        const int fx = sx32 & 31, fy = sy32 & 31;
+        const int sx = min(max(sx32 >> 5, -32768), 32767), sy = min(max(sy32 >> 5, -32768), 32767);
+        const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
+        const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
+        const bool x0 = (unsigned)sx < (unsigned)cols, x1 = (unsigned)(sx + 1) < (unsigned)cols;
+        const bool y0 = (unsigned)sy < (unsigned)rows, y1 = (unsigned)(sy + 1) < (unsigned)rows;
+        const uint8_t* r0 = S + (size_t)(y0 ? sy : 0) * sstep;
+        const uint8_t* r1 = S + (size_t)(y1 ? sy + 1 : 0) * sstep;
+        const int c0 = (x0 ? sx : 0) * CH, c1 = (x1 ? sx + 1 : 0) * CH;
+#pragma unroll
+        for (int k = 0; k < (CH > 1 ? 3 : 1); ++k) {
+            const int v00 = x0 && y0 ? r0[c0 + k] : 0, v01 = x1 && y0 ? r0[c1 + k] : 0;
+            const int v10 = x0 && y1 ? r1[c0 + k] : 0, v11 = x1 && y1 ? r1[c1 + k] : 0;
+            val[k] = (v00 * w00 + v01 * w01 + v10 * w10 + v11 * w11 + (1 << 14)) >> 15;
+        }
+    } else {
+        const uint8_t* p = S + (size_t)y * sstep + (size_t)x * CH;
+#pragma unroll
+        for (int k = 0; k < (CH > 1 ? 3 : 1); ++k) val[k] = p[k];
+    }
+    if (CH == 1) return (uint32_t)val[0];
+    return (uint32_t)((val[0] * w0 + val[1] * 9617 + val[2 < CH ? 2 : 0] * w2 + (1 << 13)) >> 14);
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void k_ingest(const uint8_t* __restrict__ src, int rows, int cols, int rgb,
+                                                size_t sstep, size_t sfs, const float* __restrict__ mx,
+                                                const float* __restrict__ my, int nmaps, int drows, int dcols,
+                                                uint8_t* __restrict__ dst, size_t dstep, size_t dfs, int gpr)
+{
+    const int f = blockIdx.y;
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int y = g / gpr, x0 = (g - y * gpr) * 4;
+    if (y >= drows) return;
+    const uint8_t* S = src + (size_t)f * sfs;
+    const size_t mbase = (size_t)(f % nmaps) * drows * dcols + (size_t)y * dcols;
+    const int w0 = rgb ? 4899 : 1868, w2 = rgb ? 1868 : 4899;   // RGB2Gray<uchar> coefficient order
+    uint8_t* D = dst + (size_t)f * dfs + (size_t)y * dstep;
+    const int n = min(4, dcols - x0);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (k < n) packed |= ig_pixel<CH>(S, rows, cols, sstep, mx, my, mbase + x0 + k, y, x0 + k, w0, w2) << (8 * k);
+    if (n == 4 && ((uintptr_t)(D + x0) & 3) == 0) {
+        *reinterpret_cast<uint32_t*>(D + x0) = packed;
+    } else {
+        for (int k = 0; k < n; ++k) D[x0 + k] = (uint8_t)(packed >> (8 * k));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_depth(const uint8_t* __restrict__ src, int depth_type, int rows, int cols,
+                                               size_t sstep, size_t sfs, float factor, float* __restrict__ dst,
+                                               size_t dstep, size_t dfs)
+{
+    const int f = blockIdx.y;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)rows * cols) return;
+    const int y = (int)(i / cols), x = (int)(i - (size_t)y * cols);
+    const uint8_t* row = src + (size_t)f * sfs + (size_t)y * sstep;
+    const float v = depth_type == 0 ? (float)reinterpret_cast<const uint16_t*>(row)[x] : reinterpret_cast<const float*>(row)[x];
+    reinterpret_cast<float*>(reinterpret_cast<uint8_t*>(dst) + (size_t)f * dfs + (size_t)y * dstep)[x] = v * factor + 0.0f;
+}
+
+void launch_ingest(const uint8_t* src, int batch, int rows, int cols, int channels, int rgb, size_t sstep,
+                   size_t sfs, const float* mx, const float* my, int nmaps, int drows, int dcols, uint8_t* dst,
+                   size_t dstep, size_t dfs, hipStream_t s)
+{
+    const int gpr = (dcols + 3) / 4;
+    const dim3 grid((unsigned)(((size_t)gpr * drows + 255) / 256), batch);
+    switch (channels) {
+    case 1:
+        hipLaunchKernelGGL(k_ingest<1>, grid, dim3(256), 0, s, src, rows, cols, rgb, sstep, sfs, mx, my, nmaps, drows,
+                           dcols, dst, dstep, dfs, gpr);
+        break;
+    case 3:
+        hipLaunchKernelGGL(k_ingest<3>, grid, dim3(256), 0, s, src, rows, cols, rgb, sstep, sfs, mx, my, nmaps, drows,
+                           dcols, dst, dstep, dfs, gpr);
+        break;
+    default:
+        hipLaunchKernelGGL(k_ingest<4>, grid, dim3(256), 0, s, src, rows, cols, rgb, sstep, sfs, mx, my, nmaps, drows,
+                           dcols, dst, dstep, dfs, gpr);
+        break;
+    }
+}
+
+void launch_depth(const void* src, int depth_type, int batch, int rows, int cols, size_t sstep, size_t sfs,
+                  float factor, float* dst, size_t dstep, size_t dfs, hipStream_t s)
+{
+    const dim3 grid((unsigned)(((size_t)rows * cols + 255) / 256), batch);
+    hipLaunchKernelGGL(k_depth, grid, dim3(256), 0, s, (const uint8_t*)src, depth_type, rows, cols, sstep, sfs, factor,
+                       dst, dstep, dfs);
+}
+
+}  // namespace orbx

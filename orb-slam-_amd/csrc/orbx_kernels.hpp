@@ -81,6 +81,12 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
                  const int* npts, int pcap, const orbm_proj_params& P, void* scratch, int* match, int* nmatches,
                  hipStream_t s);
 
+void launch_ingest(const uint8_t* src, int batch, int rows, int cols, int channels, int rgb, size_t sstep,
+                   size_t sfs, const float* mx, const float* my, int nmaps, int drows, int dcols, uint8_t* dst,
+                   size_t dstep, size_t dfs, hipStream_t s);
+void launch_depth(const void* src, int depth_type, int batch, int rows, int cols, size_t sstep, size_t sfs,
+                  float factor, float* dst, size_t dstep, size_t dfs, hipStream_t s);
+
 size_t pose_scratch_bytes(int nframes, int cap, int pcap);
 void launch_pose_search(int mode, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,
                         const uint8_t* claimed, const int* counts, int nframes, int cap, const float* pose,

@@ -37,7 +37,7 @@ EXPORTED = [
     "orbm_search_init_batch_device", "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
     "orbm_bow_search_device", "orbm_bow_search",
     "orbm_search_by_projection_device", "orbm_search_by_projection",
-    "orbm_project_search_device", "orbm_project_search",
+    "orbm_project_search_device", "orbm_project_search", "orbx_ingest_batch_device", "orbx_depth_batch_device",
     "orbv_load_text", "orbv_create", "orbv_destroy", "orbv_info", "orbv_transform", "orbv_transform_batch_device",
 ]
 BOW_KF_F, BOW_KF_KF, TRIANGULATION = 0, 1, 2
@@ -174,6 +174,10 @@ def _load():
                                              P(PoseParams), vp, vp, vp]
     L.orbm_project_search.argtypes = [C.c_int, C.c_int, vp, u8p, f32p, u8p, C.c_int, f32p, vp, u8p, C.c_int,
                                       P(PoseParams), i32p, i32p]
+    L.orbx_ingest_batch_device.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_size_t,
+                                           vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_size_t, C.c_size_t, vp]
+    L.orbx_depth_batch_device.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_float,
+                                          vp, C.c_size_t, C.c_size_t, vp]
     L.orbm_bow_search_device.argtypes = [C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, C.c_int, vp, C.c_int,
                                          vp, vp]
     L.orbm_bow_search.argtypes = [C.c_int, C.c_int, P(BowView), P(BowView), P(TriangParams), C.c_float, C.c_int,
@@ -364,6 +368,47 @@ def compute_stereo_matches(left, right, kps_l, desc_l, kps_r, desc_r, bf, fx):
            lib.orbx_compute_stereo_matches(left._h, right._h, kl.ctypes.data, _u8(dl), nl, kr.ctypes.data, _u8(dr), nr,
                                            bf, fx, f32(ur), f32(dp), C.byref(ng)))
     return ur[:nl].copy(), dp[:nl].copy(), ng.value
+
+
+def ingest_batch_device(src, rgb=False, map_x=None, map_y=None, out=None, stream=None):
+    """Tracking::GrabImage* colour conversion after the examples' cv::remap rectification, on a device
+    batch.  src: uint8 tensor (B, H, W) or (B, H, W, C); map_x / map_y: float32 (nmaps, H', W') or None.
+    Returns the gray (B, H', W') uint8 tensor (the layout orbx_extract_batch_device reads)."""
+    import torch
+    B, rows, cols = src.shape[:3]
+    ch = 1 if src.dim() == 3 else src.shape[3]
+    if map_x is not None:
+        nmaps, drows, dcols = map_x.shape
+    else:
+        nmaps, drows, dcols = 1, rows, cols
+    if out is None:
+        out = torch.empty((B, drows, dcols), dtype=torch.uint8, device=src.device)
+    s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    _check("orbx_ingest_batch_device",
+           lib.orbx_ingest_batch_device(_ptr(src), B, rows, cols, ch, int(bool(rgb)), src.stride(1), src.stride(0),
+                                        _ptr(map_x) if map_x is not None else None,
+                                        _ptr(map_y) if map_y is not None else None, nmaps, drows, dcols, _ptr(out),
+                                        out.stride(1), out.stride(0), C.c_void_p(s)))
+    return out
+
+
+def depth_batch_device(src, factor, out=None, stream=None):
+    """GrabImageRGBD's imDepth.convertTo(CV_32F, mDepthMapFactor), applied under the reference's own
+    condition (factor != 1 or a non-float depth map); src: (B, H, W) uint16-as-int16 or float32 tensor."""
+    import torch
+    B, rows, cols = src.shape
+    isf = src.dtype == torch.float32
+    if isf and abs(factor - 1.0) <= 1e-5:
+        return src
+    if out is None:
+        out = torch.empty((B, rows, cols), dtype=torch.float32, device=src.device)
+    esz = src.element_size()
+    s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    _check("orbx_depth_batch_device",
+           lib.orbx_depth_batch_device(_ptr(src), 1 if isf else 0, B, rows, cols, src.stride(1) * esz,
+                                       src.stride(0) * esz, factor, _ptr(out), out.stride(1) * 4, out.stride(0) * 4,
+                                       C.c_void_p(s)))
+    return out
 
 
 def keypoints_from_device(kps_i32, counts):
