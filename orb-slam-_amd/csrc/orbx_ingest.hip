@@ -23,37 +23,69 @@ __device__ __forceinline__ int ig_round_x86(float v)   // cvRound (cvtss2si): Na
     return (v >= -2147483648.0f && v < 2147483648.0f) ? __float2int_rn(v) : (-2147483647 - 1);
 }
 
+// the two horizontal taps (sx, sx+1) of one source row, all channels: one aligned 8- or 12-byte load
+// and a funnel shift when the window lies inside the row, byte loads with the border value 0 otherwise
 template <int CH>
-__device__ __forceinline__ uint32_t ig_pixel(const uint8_t* __restrict__ S, int rows, int cols, size_t sstep,
-                                             const float* __restrict__ mx, const float* __restrict__ my, size_t mo,
-                                             int y, int x, int w0, int w2)
+__device__ __forceinline__ void ig_taps(const uint8_t* __restrict__ row, int sx, int cols, bool rowin, int t0[3],
+                                        int t1[3])
 {
-    int val[CH > 1 ? 3 : 1];
-    if (mx) {
-        const int sx32 = ig_round_x86(mx[mo] * 32.0f);
-        const int sy32 = ig_round_x86(my[mo] * 32.0f);
-        const int fx = sx32 & 31, fy = sy32 & 31;
-        const int sx = min(max(sx32 >> 5, -32768), 32767), sy = min(max(sy32 >> 5, -32768), 32767);
-        const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
-        const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
-        const bool x0 = (unsigned)sx < (unsigned)cols, x1 = (unsigned)(sx + 1) < (unsigned)cols;
-        const bool y0 = (unsigned)sy < (unsigned)rows, y1 = (unsigned)(sy + 1) < (unsigned)rows;
-        const uint8_t* r0 = S + (size_t)(y0 ? sy : 0) * sstep;
-        const uint8_t* r1 = S + (size_t)(y1 ? sy + 1 : 0) * sstep;
-        const int c0 = (x0 ? sx : 0) * CH, c1 = (x1 ? sx + 1 : 0) * CH;
+    constexpr int C3 = CH > 1 ? 3 : 1;
 #pragma unroll
-        for (int k = 0; k < (CH > 1 ? 3 : 1); ++k) {
-            const int v00 = x0 && y0 ? r0[c0 + k] : 0, v01 = x1 && y0 ? r0[c1 + k] : 0;
-            const int v10 = x0 && y1 ? r1[c0 + k] : 0, v11 = x1 && y1 ? r1[c1 + k] : 0;
-            val[k] = (v00 * w00 + v01 * w01 + v10 * w10 + v11 * w11 + (1 << 14)) >> 15;
+    for (int k = 0; k < C3; ++k) t0[k] = t1[k] = 0;
+    if (!rowin) return;
+    const uintptr_t a = (uintptr_t)(row + (ptrdiff_t)sx * CH), a4 = a & ~(uintptr_t)3;
+    constexpr int kWords = CH == 1 ? 2 : 3;   // bytes [sh/8, sh/8 + 2*CH) of the aligned window
+    if (sx >= 0 && sx + 1 < cols && a4 >= (uintptr_t)row && a4 + 4 * kWords <= (uintptr_t)(row + (size_t)cols * CH)) {
+        const int sh = (int)(a - a4) * 8;
+        unsigned long long v;
+        if (kWords == 2) {
+            const uint2 w = *reinterpret_cast<const uint2*>(a4);
+            v = ((unsigned long long)w.y << 32 | w.x) >> sh;
+        } else {
+            const uint3 w = *reinterpret_cast<const uint3*>(a4);
+            const unsigned long long lo = (unsigned long long)w.y << 32 | w.x;
+            v = sh ? (lo >> sh) | ((unsigned long long)w.z << (64 - sh)) : lo;
         }
-    } else {
-        const uint8_t* p = S + (size_t)y * sstep + (size_t)x * CH;
 #pragma unroll
-        for (int k = 0; k < (CH > 1 ? 3 : 1); ++k) val[k] = p[k];
+        for (int k = 0; k < C3; ++k) {
+            t0[k] = (int)((v >> (8 * k)) & 255);
+            t1[k] = (int)((v >> (8 * (k + CH))) & 255);
+        }
+        return;
     }
-    if (CH == 1) return (uint32_t)val[0];
-    return (uint32_t)((val[0] * w0 + val[1] * 9617 + val[2 < CH ? 2 : 0] * w2 + (1 << 13)) >> 14);
+    const bool x0 = (unsigned)sx < (unsigned)cols, x1 = (unsigned)(sx + 1) < (unsigned)cols;
+#pragma unroll
+    for (int k = 0; k < C3; ++k) {
+        if (x0) t0[k] = row[(size_t)sx * CH + k];
+        if (x1) t1[k] = row[(size_t)(sx + 1) * CH + k];
+    }
+}
+
+template <int CH>
+__device__ __forceinline__ uint32_t ig_gray(const int v[3], int w0, int w2)
+{
+    if (CH == 1) return (uint32_t)v[0];
+    return (uint32_t)((v[0] * w0 + v[1] * 9617 + v[2 < CH ? 2 : 0] * w2 + (1 << 13)) >> 14);
+}
+
+template <int CH>
+__device__ __forceinline__ uint32_t ig_remap_pixel(const uint8_t* __restrict__ S, int rows, int cols, size_t sstep,
+                                                   float mxv, float myv, int w0, int w2)
+{
+    constexpr int C3 = CH > 1 ? 3 : 1;
+    const int sx32 = ig_round_x86(mxv * 32.0f);
+    const int sy32 = ig_round_x86(myv * 32.0f);
+    const int fx = sx32 & 31, fy = sy32 & 31;
+    const int sx = min(max(sx32 >> 5, -32768), 32767), sy = min(max(sy32 >> 5, -32768), 32767);
+    const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
+    const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
+    const bool y0 = (unsigned)sy < (unsigned)rows, y1 = (unsigned)(sy + 1) < (unsigned)rows;
+    int a0[3], a1[3], b0[3], b1[3], val[3];
+    ig_taps<CH>(S + (size_t)(y0 ? sy : 0) * sstep, sx, cols, y0, a0, a1);
+    ig_taps<CH>(S + (size_t)(y1 ? sy + 1 : 0) * sstep, sx, cols, y1, b0, b1);
+#pragma unroll
+    for (int k = 0; k < C3; ++k) val[k] = (a0[k] * w00 + a1[k] * w01 + b0[k] * w10 + b1[k] * w11 + (1 << 14)) >> 15;
+    return ig_gray<CH>(val, w0, w2);
 }
 
 template <int CH>
@@ -62,19 +94,44 @@ __global__ __launch_bounds__(256) void k_ingest(const uint8_t* __restrict__ src,
                                                 const float* __restrict__ my, int nmaps, int drows, int dcols,
                                                 uint8_t* __restrict__ dst, size_t dstep, size_t dfs, int gpr)
 {
+    constexpr int C3 = CH > 1 ? 3 : 1;
     const int f = blockIdx.y;
     const int g = blockIdx.x * 256 + threadIdx.x;
     const int y = g / gpr, x0 = (g - y * gpr) * 4;
     if (y >= drows) return;
     const uint8_t* S = src + (size_t)f * sfs;
-    const size_t mbase = (size_t)(f % nmaps) * drows * dcols + (size_t)y * dcols;
     const int w0 = rgb ? 4899 : 1868, w2 = rgb ? 1868 : 4899;   // RGB2Gray<uchar> coefficient order
     uint8_t* D = dst + (size_t)f * dfs + (size_t)y * dstep;
     const int n = min(4, dcols - x0);
     uint32_t packed = 0;
+    if (mx) {
+        const size_t mo = (size_t)(f % nmaps) * drows * dcols + (size_t)y * dcols + x0;
+        float4 vx, vy;
+        if (n == 4 && (((uintptr_t)(mx + mo) | (uintptr_t)(my + mo)) & 15) == 0) {
+            vx = *reinterpret_cast<const float4*>(mx + mo);
+            vy = *reinterpret_cast<const float4*>(my + mo);
+        } else {
+            vx.x = mx[mo]; vy.x = my[mo];
+            vx.y = n > 1 ? mx[mo + 1] : 0.f; vy.y = n > 1 ? my[mo + 1] : 0.f;
+            vx.z = n > 2 ? mx[mo + 2] : 0.f; vy.z = n > 2 ? my[mo + 2] : 0.f;
+            vx.w = n > 3 ? mx[mo + 3] : 0.f; vy.w = n > 3 ? my[mo + 3] : 0.f;
+        }
+        const float xs[4] = {vx.x, vx.y, vx.z, vx.w}, ys[4] = {vy.x, vy.y, vy.z, vy.w};
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (k < n) packed |= ig_pixel<CH>(S, rows, cols, sstep, mx, my, mbase + x0 + k, y, x0 + k, w0, w2) << (8 * k);
+        for (int k = 0; k < 4; ++k)
+            if (k < n) packed |= ig_remap_pixel<CH>(S, rows, cols, sstep, xs[k], ys[k], w0, w2) << (8 * k);
+    } else {
+        const uint8_t* p = S + (size_t)y * sstep + (size_t)x0 * CH;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < n) {
+                int v[3];
+#pragma unroll
+                for (int c = 0; c < C3; ++c) v[c] = p[k * CH + c];
+                packed |= ig_gray<CH>(v, w0, w2) << (8 * k);
+            }
+        }
+    }
     if (n == 4 && ((uintptr_t)(D + x0) & 3) == 0) {
         *reinterpret_cast<uint32_t*>(D + x0) = packed;
     } else {

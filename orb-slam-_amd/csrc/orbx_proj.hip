@@ -139,11 +139,49 @@ __device__ __forceinline__ int pj_candidate(const PjWindow& w, const orbm_proj_p
     return idx;
 }
 
-// J2 result per MapPoint: best / second candidate and the accept decision
+// The first kTop candidates of a window in (distance, visiting position) order -- the order in which
+// the reference's sequential strict-< scan ranks them -- packed as dist:9 | bin:5 | octave:4 | idx:13.
+// A claim made later in the call only removes candidates, so the replay takes the first unclaimed
+// entries of this list and scans the window again only when more than kTop were taken.
+constexpr int kTop = 8;
+struct TopK {
+    uint32_t e[kTop];
+    int n;   // candidates seen (saturating at 255)
+};
+
+__device__ __forceinline__ uint32_t top_entry(int dist, int bin, int oct, int idx)
+{
+    return (uint32_t)dist << 22 | (uint32_t)bin << 17 | (uint32_t)(oct & 15) << 13 | (uint32_t)idx;
+}
+__device__ __forceinline__ int top_idx(uint32_t e) { return (int)(e & 0x1FFF); }
+__device__ __forceinline__ int top_oct(uint32_t e) { return (int)((e >> 13) & 15); }
+__device__ __forceinline__ int top_bin(uint32_t e) { return (int)((e >> 17) & 31); }
+__device__ __forceinline__ int top_dist(uint32_t e) { return (int)(e >> 22); }
+
+__device__ __forceinline__ void top_insert(TopK& t, uint32_t entry)
+{
+    const uint32_t dnew = entry >> 22;
+    uint32_t carry = entry;
+    bool shifting = false;   // stable: after the entries of equal distance, then everything moves down
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) {
+        const bool take = shifting || k >= t.n || (t.e[k] >> 22) > dnew;
+        if (take) {
+            const uint32_t x = t.e[k];
+            t.e[k] = carry;
+            carry = x;
+            shifting = true;
+        }
+    }
+    t.n = min(t.n + 1, 255);
+}
+
+// J2 result per MapPoint: the top-kTop list and the accept decision of its first two entries
 struct PjResult {
-    int best, second;   // feature indices (-1 none)
-    int accept;         // bestDist <= TH_HIGH and the same-level ratio test passed
-    int pad;
+    uint32_t e[kTop];
+    int n;        // candidates in the window (not claimed on entry), saturating
+    int accept;   // bestDist <= TH_HIGH and the same-level ratio test passed
+    int pad[2];
 };
 
 __device__ __forceinline__ bool pj_accept(int bestDist, int bestLevel, int bestDist2, int bestLevel2, float nnratio)
@@ -164,7 +202,8 @@ __global__ __launch_bounds__(256) void k_pj_points(const orbx_keypoint* __restri
     const int f = blockIdx.y, m = blockIdx.x * 256 + threadIdx.x;
     if (m >= min(npts[f], pcap)) return;
     const size_t mo = (size_t)f * pcap + m;
-    PjResult R{-1, -1, 0, 0};
+    TopK T{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0};
+    int accept = 0;
     const orbm_proj_point M = pts[mo];
     if (M.flags & 1) {
         const uint32_t* keys = gkeys + (size_t)f * cap;
@@ -175,30 +214,24 @@ __global__ __launch_bounds__(256) void k_pj_points(const orbx_keypoint* __restri
             const uint8_t* C = claimed + (size_t)f * cap;
             const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
             const uint4 q0 = qd[0], q1 = qd[1];
-            int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1, bestIdx2 = -1;
             for (int p = w.lo; p < w.hi; ++p) {   // src/ORBmatcher.cc:78-113, in visiting order
                 const int idx = pj_candidate(w, M, keys, p, K, U);
                 if (idx < 0 || C[idx]) continue;
                 const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
-                const int dist = pj_ham(q0, q1, d[0], d[1]);
-                if (dist < bestDist) {
-                    bestDist2 = bestDist;
-                    bestDist = dist;
-                    bestLevel2 = bestLevel;
-                    bestLevel = K[idx].octave;
-                    bestIdx2 = bestIdx;
-                    bestIdx = idx;
-                } else if (dist < bestDist2) {
-                    bestLevel2 = K[idx].octave;
-                    bestDist2 = dist;
-                    bestIdx2 = idx;
-                }
+                top_insert(T, top_entry(pj_ham(q0, q1, d[0], d[1]), 0, K[idx].octave, idx));
             }
-            R.best = bestIdx;
-            R.second = bestIdx2;
-            R.accept = bestIdx >= 0 && pj_accept(bestDist, bestLevel, bestDist2, bestLevel2, P.nnratio);
+            // the scan's best / second are the first two entries (multiset top two, first wins ties)
+            if (T.n > 0)
+                accept = pj_accept(top_dist(T.e[0]), top_oct(T.e[0]), T.n > 1 ? top_dist(T.e[1]) : 256,
+                                   T.n > 1 ? top_oct(T.e[1]) : -1, P.nnratio);
         }
     }
+    PjResult R;
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) R.e[k] = T.e[k];
+    R.n = T.n;
+    R.accept = accept;
+    R.pad[0] = R.pad[1] = 0;
     res[mo] = R;
 }
 
@@ -223,10 +256,14 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
                                                    const int* __restrict__ gn, const PjResult* __restrict__ res,
                                                    int* __restrict__ match, int* __restrict__ nmatches)
 {
+    // the assignments live in LDS during the replay: a global store inside the serial loop would
+    // hold every later iteration's vmcnt wait until the store is acknowledged
+    extern __shared__ int s_mo[];
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(counts[f], cap), np = min(npts[f], pcap);
     int* Mo = match + (size_t)f * cap;
-    for (int i = lane; i < n; i += 64) Mo[i] = -1;
+    for (int i = lane; i < n; i += 64) s_mo[i] = -1;
+    __syncthreads();
     unsigned long long bits[kPjBitWords] = {0ull, 0ull};   // features claimed during this call
     const uint32_t* keys = gkeys + (size_t)f * cap;
     const orbx_keypoint* K = kps + (size_t)f * cap;
@@ -243,20 +280,49 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
     int count = 0;
     for (int base = 0; base < np; base += 64) {
         const int mm = base + lane;
-        PjResult R{-1, -1, 0, 0};
+        PjResult R{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0, 0, {0, 0}};
         int obs = 0;
         if (mm < np) {
             R = res[(size_t)f * pcap + mm];
             obs = (pts[(size_t)f * pcap + mm].flags & 2) ? 1 : 0;
         }
-        const int cnt = min(64, np - base);
-        for (int j = 0; j < cnt; ++j) {
-            int best = __builtin_amdgcn_readlane(R.best, j);
-            const int second = __builtin_amdgcn_readlane(R.second, j);
+        unsigned long long live = __ballot(R.n > 0);   // no candidate on entry: nothing to replay
+        while (live) {
+            const int j = __builtin_ctzll(live);
+            live &= live - 1;
+            uint32_t e[kTop];
+#pragma unroll
+            for (int k = 0; k < kTop; ++k) e[k] = (uint32_t)__builtin_amdgcn_readlane((int)R.e[k], j);
+            const int nc = __builtin_amdgcn_readlane(R.n, j);
+            int best = top_idx(e[0]);
+            const int second = nc > 1 ? top_idx(e[1]) : -1;
             int accept = __builtin_amdgcn_readlane(R.accept, j);
             const int o = __builtin_amdgcn_readlane(obs, j);
-            if (best < 0) continue;
+            bool rescan = false;
             if (claimed_now(best) || (second >= 0 && claimed_now(second))) {
+                // the first two unclaimed entries of the list, unless the list runs out
+                int k1 = -1, k2 = -1;
+#pragma unroll
+                for (int k = 0; k < kTop; ++k) {
+                    if (k < nc && k2 < 0 && !claimed_now(top_idx(e[k]))) {
+                        if (k1 < 0) k1 = k; else k2 = k;
+                    }
+                }
+                if (k2 < 0 && nc > kTop) {
+                    rescan = true;
+                } else {
+                    uint32_t e1 = 0, e2 = 0;
+#pragma unroll
+                    for (int k = 0; k < kTop; ++k) {
+                        if (k == k1) e1 = e[k];
+                        if (k == k2) e2 = e[k];
+                    }
+                    best = k1 >= 0 ? top_idx(e1) : -1;
+                    accept = k1 >= 0 && pj_accept(top_dist(e1), top_oct(e1), k2 >= 0 ? top_dist(e2) : 256,
+                                                  k2 >= 0 ? top_oct(e2) : -1, P.nnratio);
+                }
+            }
+            if (rescan) {
                 // search again against the current claims: best = first min of (dist, position),
                 // second = first min of the rest (the sequential scan's result)
                 const int m = base + j;
@@ -308,7 +374,7 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
                 }
             }
             if (best >= 0 && accept) {
-                if (lane == 0) Mo[best] = base + j;   // F.mvpMapPoints[bestIdx] = pMP (last writer)
+                if (lane == 0) s_mo[best] = base + j;   // F.mvpMapPoints[bestIdx] = pMP (last writer)
                 ++count;
                 if (o) {
                     const int word = best >> 6;
@@ -317,6 +383,8 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
             }
         }
     }
+    __syncthreads();
+    for (int i = lane; i < n; i += 64) Mo[i] = s_mo[i];
     if (lane == 0) nmatches[f] = count;
 }
 
@@ -340,8 +408,9 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
                        P.grid_w_inv, P.grid_h_inv, gkeys, gn);
     hipLaunchKernelGGL(k_pj_points, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright, claimed,
                        cap, pts, pdesc, npts, pcap, P, gkeys, gn, res);
-    hipLaunchKernelGGL(k_pj_resolve, dim3(nframes), dim3(64), 0, s, kps, desc, uright, claimed, counts, cap, pts,
-                       pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+    hipFuncSetAttribute((const void*)k_pj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * cap);
+    hipLaunchKernelGGL(k_pj_resolve, dim3(nframes), dim3(64), (size_t)4 * cap, s, kps, desc, uright, claimed, counts,
+                       cap, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
 }
 
 // =====================================================================================
@@ -534,8 +603,19 @@ __device__ __forceinline__ int ps_threshold(const orbm_pose_params& P)
     return MODE == ORBM_PROJ_LAST_FRAME ? 100 : (MODE == ORBM_PROJ_KEYFRAME ? P.orb_dist : 50);   // TH_HIGH / TH_LOW
 }
 
+__device__ __forceinline__ int ps_rot_bin(float a1, float a2)
+{
+    const float factor = 1.0f / 30;   // 1/HISTO_LENGTH
+    float rot = a1 - a2;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * factor);
+    if (bin == 30) bin = 0;
+    return bin;
+}
+
 struct PsResult {
-    int best, accept;
+    uint32_t e[kTop];   // top-kTop list (TopK), bins filled for the rotation-checked searches
+    int n, accept;
 };
 
 template <int MODE>
@@ -553,6 +633,7 @@ __global__ __launch_bounds__(256) void k_ps_points(const orbx_keypoint* __restri
     if (m >= min(npts[f], pcap)) return;
     const size_t mo = (size_t)f * pcap + m;
     int bestIdx = -1, accept = 0;
+    TopK T{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0};
     const orbm_map_point M = pts[mo];
     if (M.flags & 1) {
         const PsCam c = ps_camera(MODE, pose + (size_t)f * 24, P);
@@ -564,36 +645,38 @@ __global__ __launch_bounds__(256) void k_ps_points(const orbx_keypoint* __restri
             const uint8_t* C = claimed + (size_t)f * cap;
             const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
             const uint4 q0 = qd[0], q1 = qd[1];
+            const bool bins = kSearch && (MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME) && P.check_ori;
             int bestDist = 256;
             for (int p = w.lo; p < w.hi; ++p) {
                 const int idx = ps_candidate<MODE>(w, keys, p, K, U, P);
                 if (idx < 0 || (kSearch && C[idx])) continue;
                 const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
                 const int dist = pj_ham(q0, q1, d[0], d[1]);
-                if (dist < bestDist) {
+                if (kSearch) {
+                    top_insert(T, top_entry(dist, bins ? ps_rot_bin(M.angle, K[idx].angle) : 0, 0, idx));
+                } else if (dist < bestDist) {
                     bestDist = dist;
                     bestIdx = idx;
                 }
+            }
+            if (kSearch) {
+                bestIdx = T.n > 0 ? top_idx(T.e[0]) : -1;
+                bestDist = T.n > 0 ? top_dist(T.e[0]) : 256;
             }
             accept = bestIdx >= 0 && bestDist <= ps_threshold<MODE>(P);
         }
     }
     if (kSearch) {
-        res[mo] = PsResult{bestIdx, accept};
+        PsResult R;
+#pragma unroll
+        for (int k = 0; k < kTop; ++k) R.e[k] = T.e[k];
+        R.n = T.n;
+        R.accept = accept;
+        res[mo] = R;
     } else {
         match[mo] = accept ? bestIdx : -1;
         if (accept) atomicAdd(&nmatches[f], 1);
     }
-}
-
-__device__ __forceinline__ int ps_rot_bin(float a1, float a2)
-{
-    const float factor = 1.0f / 30;   // 1/HISTO_LENGTH
-    float rot = a1 - a2;
-    if (rot < 0.0f) rot += 360.0f;
-    int bin = (int)roundf(rot * factor);
-    if (bin == 30) bin = 0;
-    return bin;
 }
 
 template <int MODE>
@@ -608,11 +691,18 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
                                                    int* __restrict__ ent, int* __restrict__ match,
                                                    int* __restrict__ nmatches)
 {
+    // assignments and, per feature, the rotation bins of the matches that assigned it, in LDS (a
+    // global store inside the serial loop would hold every later vmcnt wait for its acknowledgement)
+    extern __shared__ int s_mo[];
+    uint32_t* s_bins = reinterpret_cast<uint32_t*>(s_mo + cap);
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(counts[f], cap), np = min(npts[f], pcap);
     int* Mo = match + (size_t)f * cap;
-    for (int i = lane; i < n; i += 64) Mo[i] = -1;
-    __threadfence();
+    for (int i = lane; i < n; i += 64) {
+        s_mo[i] = -1;
+        s_bins[i] = 0u;
+    }
+    __syncthreads();
     unsigned long long bits[kPjBitWords] = {0ull, 0ull};   // features claimed during this call
     const uint32_t* keys = gkeys + (size_t)f * cap;
     const orbx_keypoint* K = kps + (size_t)f * cap;
@@ -621,7 +711,6 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
     const int ng = gn[f];
     const PsCam cam = ps_camera(MODE, pose + (size_t)f * 24, P);
     const bool rot = P.check_ori && (MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME);
-    int* E = ent + (size_t)f * pcap;
     auto claimed_now = [&](int idx) -> bool {   // wave-uniform idx
         const int word = idx >> 6, w = word & 63, h = word >> 6;
         const unsigned long long b =
@@ -629,24 +718,49 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
             ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits[h] >> 32), w) << 32);
         return (b >> (idx & 63)) & 1ull;
     };
-    int count = 0, nent = 0, hist = 0;   // lane b holds rotHist[b].size()
+    int count = 0, hist = 0;   // lane b holds rotHist[b].size()
     for (int base = 0; base < np; base += 64) {
         const int mm = base + lane;
-        PsResult R{-1, 0};
+        PsResult R{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0, 0};
         int obs = 0;
-        float ang = 0.0f;
+        float ang = 0.0f;   // for a search again
         if (mm < np) {
             R = res[(size_t)f * pcap + mm];
             const orbm_map_point& Mp = pts[(size_t)f * pcap + mm];
             obs = MODE != ORBM_PROJ_LAST_FRAME || (Mp.flags & 2);
             ang = Mp.angle;
         }
-        const int cnt = min(64, np - base);
-        for (int j = 0; j < cnt; ++j) {
-            int best = __builtin_amdgcn_readlane(R.best, j);
-            int accept = __builtin_amdgcn_readlane(R.accept, j);
-            if (best < 0) continue;   // no candidate on entry: claims only remove candidates
-            if (claimed_now(best)) {
+        // only accepted J2 results can produce a match: a claim removes candidates, so a search
+        // again finds a distance >= the J2 one, which the threshold still rejects
+        unsigned long long live = __ballot(R.n > 0 && R.accept);
+        while (live) {
+            const int j = __builtin_ctzll(live);
+            live &= live - 1;
+            uint32_t e[kTop];
+#pragma unroll
+            for (int k = 0; k < kTop; ++k) e[k] = (uint32_t)__builtin_amdgcn_readlane((int)R.e[k], j);
+            const int nc = __builtin_amdgcn_readlane(R.n, j);
+            int best = top_idx(e[0]), bin = top_bin(e[0]);
+            int accept = 1;
+            bool rescan = false;
+            if (claimed_now(best)) {   // the first unclaimed entry of the list, unless it runs out
+                int k1 = -1;
+#pragma unroll
+                for (int k = 1; k < kTop; ++k)
+                    if (k < nc && k1 < 0 && !claimed_now(top_idx(e[k]))) k1 = k;
+                if (k1 < 0 && nc > kTop) {
+                    rescan = true;
+                } else {
+                    uint32_t e1 = 0;
+#pragma unroll
+                    for (int k = 1; k < kTop; ++k)
+                        if (k == k1) e1 = e[k];
+                    best = k1 >= 0 ? top_idx(e1) : -1;
+                    bin = top_bin(e1);
+                    accept = k1 >= 0 && top_dist(e1) <= ps_threshold<MODE>(P);
+                }
+            }
+            if (rescan) {
                 const int m = base + j;
                 const size_t mo = (size_t)f * pcap + m;
                 const orbm_map_point Mp = pts[mo];
@@ -680,25 +794,27 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
                 }
                 best = b1 == ~0ull ? -1 : (int)(b1 & 0xFFFF);
                 accept = best >= 0 && (int)(b1 >> 32) <= ps_threshold<MODE>(P);
+                if (accept && rot) {
+                    const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), j));
+                    bin = ps_rot_bin(a1, K[best].angle);
+                }
             }
             if (best < 0 || !accept) continue;
-            if (lane == 0) Mo[best] = base + j;   // mvpMapPoints[bestIdx] = pMP
+            if (lane == 0) {
+                s_mo[best] = base + j;   // mvpMapPoints[bestIdx] = pMP
+                if (rot) s_bins[best] |= 1u << bin;
+            }
             ++count;
             if (__builtin_amdgcn_readlane(obs, j)) {
                 const int word = best >> 6;
                 if (lane == (word & 63)) bits[word >> 6] |= 1ull << (best & 63);
             }
-            if (rot) {
-                const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), j));
-                const int bin = ps_rot_bin(a1, K[best].angle);
-                if (lane == 0) E[nent] = (best << 8) | bin;
-                ++nent;
-                hist += lane == bin;
-            }
+            if (rot) hist += lane == bin;
         }
     }
+    __syncthreads();
+    uint32_t drop = 0u;   // the bins outside the three maxima
     if (rot) {   // ComputeThreeMaxima (:1679-1723) and the NULL-ing of the other bins
-        __threadfence();
         int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;
         for (int i = 0; i < 30; ++i) {
             const int s = __builtin_amdgcn_readlane(hist, i);
@@ -708,18 +824,18 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
         }
         if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
-        int removed = 0;
-        for (int e = lane; e < nent; e += 64) {
-            const int v = E[e], bin = v & 255;
-            if (bin != ind1 && bin != ind2 && bin != ind3) {
-                Mo[v >> 8] = -2;
-                ++removed;
-            }
-        }
+        drop = 0x3FFFFFFFu;
+        if (ind1 >= 0) drop &= ~(1u << ind1);
+        if (ind2 >= 0) drop &= ~(1u << ind2);
+        if (ind3 >= 0) drop &= ~(1u << ind3);
+        // every match in a dropped bin is undone (nmatches--), and its feature set to NULL
+        const int removed_here = (lane < 30 && ((drop >> lane) & 1u)) ? hist : 0;
+        int removed = removed_here;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) removed += __shfl_xor(removed, o);
         count -= removed;
     }
+    for (int i = lane; i < n; i += 64) Mo[i] = (s_bins[i] & drop) ? -2 : s_mo[i];
     if (lane == 0) nmatches[f] = count;
 }
 
@@ -738,9 +854,11 @@ static void ps_launch(const orbx_keypoint* kps, const uint8_t* desc, const float
     if (MODE >= ORBM_FUSE) hipMemsetAsync(nmatches, 0, sizeof(int) * (size_t)nframes, s);
     hipLaunchKernelGGL(k_ps_points<MODE>, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright,
                        claimed, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
-    if (MODE <= ORBM_PROJ_SIM3)
-        hipLaunchKernelGGL(k_ps_resolve<MODE>, dim3(nframes), dim3(64), 0, s, kps, desc, uright, claimed, counts, cap,
-                           pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, ent, match, nmatches);
+    if (MODE <= ORBM_PROJ_SIM3) {
+        hipFuncSetAttribute((const void*)k_ps_resolve<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * cap);
+        hipLaunchKernelGGL(k_ps_resolve<MODE>, dim3(nframes), dim3(64), (size_t)8 * cap, s, kps, desc, uright, claimed,
+                           counts, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, ent, match, nmatches);
+    }
 }
 
 void launch_pose_search(int mode, const orbx_keypoint* kps, const uint8_t* desc, const float* uright,

@@ -383,12 +383,11 @@ def ingest_batch_device(src, rgb=False, map_x=None, map_y=None, out=None, stream
         nmaps, drows, dcols = 1, rows, cols
     if out is None:
         out = torch.empty((B, drows, dcols), dtype=torch.uint8, device=src.device)
-    s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
     _check("orbx_ingest_batch_device",
            lib.orbx_ingest_batch_device(_ptr(src), B, rows, cols, ch, int(bool(rgb)), src.stride(1), src.stride(0),
                                         _ptr(map_x) if map_x is not None else None,
                                         _ptr(map_y) if map_y is not None else None, nmaps, drows, dcols, _ptr(out),
-                                        out.stride(1), out.stride(0), C.c_void_p(s)))
+                                        out.stride(1), out.stride(0), _stream(stream)))
     return out
 
 
@@ -403,11 +402,10 @@ def depth_batch_device(src, factor, out=None, stream=None):
     if out is None:
         out = torch.empty((B, rows, cols), dtype=torch.float32, device=src.device)
     esz = src.element_size()
-    s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
     _check("orbx_depth_batch_device",
            lib.orbx_depth_batch_device(_ptr(src), 1 if isf else 0, B, rows, cols, src.stride(1) * esz,
                                        src.stride(0) * esz, factor, _ptr(out), out.stride(1) * 4, out.stride(0) * 4,
-                                       C.c_void_p(s)))
+                                       _stream(stream)))
     return out
 
 
@@ -502,6 +500,27 @@ class ORBmatcher:
                                        pp.ctypes.data, _u8(pd), len(pp), C.byref(prm),
                                        out.ctypes.data_as(C.POINTER(C.c_int)), C.byref(nm)))
         return nm.value, out[:nout].copy()
+
+    def project_search_batch_device(self, mode, kps, desc, uright, claimed, counts, pose, pts, pdesc, npts, params,
+                                    match=None, nmatches=None, stream=None):
+        """Batched device form of project_search: kps (B, cap, 7) int32, desc (B, cap, 32) uint8, uright
+        (B, cap) float32, claimed (B, cap) uint8, counts (B,), pose (B, 24) float32, pts (B, pcap, 12)
+        int32 view of MAP_POINT_DTYPE, pdesc (B, pcap, 32), npts (B,).  Returns (match, nmatches)."""
+        import torch
+        B, cap = kps.shape[0], kps.shape[1]
+        pcap = pts.shape[1]
+        nout = cap if mode <= PROJ_SIM3 else pcap
+        if match is None:
+            match = torch.empty((B, nout), dtype=torch.int32, device=kps.device)
+        if nmatches is None:
+            nmatches = torch.empty((B,), dtype=torch.int32, device=kps.device)
+        prm = PoseParams.from_buffer_copy(params)
+        prm.check_ori = int(self.mbCheckOrientation)
+        _check("orbm_project_search_device",
+               lib.orbm_project_search_device(mode, _ptr(kps), _ptr(desc), _ptr(uright), _ptr(claimed), _ptr(counts),
+                                              B, cap, _ptr(pose), _ptr(pts), _ptr(pdesc), _ptr(npts), pcap,
+                                              C.byref(prm), _ptr(match), _ptr(nmatches), _stream(stream)))
+        return match, nmatches
 
     def SearchByProjectionLastFrame(self, cur, last_pts, last_pdesc, Tcw, Tlw, params, th, bMono, device=0):
         """SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono) (src/ORBmatcher.cc:1396-1538).

@@ -218,3 +218,59 @@ class Vocabulary:
             for i in range(1, self.nnodes):
                 f.write("%d %d %s %r\n" % (self.parent[i], self.is_leaf[i], " ".join(str(int(x)) for x in self.desc[i]),
                                           float(self.weight[i])))
+
+
+# ---- MapPoints for the projection searches (SearchByProjection / Fuse inputs) ----
+
+MAP_POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                            ("max_dist", "<f4"), ("min_dist", "<f4"), ("angle", "<f4"), ("octave", "<i4"),
+                            ("flags", "<i4"), ("pad", "<i4")])
+
+
+def _rotation(w: np.ndarray) -> np.ndarray:
+    th = float(np.linalg.norm(w))
+    if th < 1e-12:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def pose_scene(seed: int, kps: np.ndarray, desc: np.ndarray, n_mp: int, K=(718.856, 718.856, 607.19, 185.22),
+               bf: float = 386.14, scale_factor: float = 1.2, nlevels: int = 8):
+    """MapPoints seen by a frame with keypoints `kps` (a structured KEYPOINT array, e.g. an extraction
+    result) and descriptors `desc`: each MapPoint re-projects near a keypoint (1.5 px noise) at a
+    per-keypoint depth, with a distance range whose predicted level is the keypoint's octave (or the
+    next), a normal towards the camera, the keypoint's angle (20% random) and a descriptor 8% away
+    from the keypoint's.  Returns (pose 3x4 float32 Tcw, map points, their descriptors, uRight)."""
+    rng = np.random.default_rng(seed)
+    n = len(kps)
+    depth = rng.uniform(2.0, 40.0, n)
+    uright = np.where(rng.random(n) < 0.4, kps["x"] - bf / depth, -1).astype(np.float32)
+    R = _rotation(rng.normal(0, 0.1, 3))
+    t = rng.normal(0, 0.5, 3)
+    tgt = rng.integers(0, n, n_mp)
+    u = kps["x"][tgt] + rng.normal(0, 1.5, n_mp)
+    v = kps["y"][tgt] + rng.normal(0, 1.5, n_mp)
+    d = depth[tgt] * (1 + rng.normal(0, 0.01, n_mp))
+    Xc = np.stack([(u - K[2]) / K[0] * d, (v - K[3]) / K[1] * d, d], 1)
+    Xw = (Xc - t) @ R
+    Ow = -R.T @ t
+    dist = np.linalg.norm(Xw - Ow, axis=1)
+    lvl = np.clip(kps["octave"][tgt] + rng.integers(0, 2, n_mp), 0, nlevels - 1)
+    max_dist = dist * scale_factor ** (lvl - rng.uniform(0.05, 0.95, n_mp))
+    pts = np.zeros(n_mp, MAP_POINT_DTYPE)
+    pts["x"], pts["y"], pts["z"] = Xw[:, 0], Xw[:, 1], Xw[:, 2]
+    nrm = (Xw - Ow) / dist[:, None] + rng.normal(0, 0.2, (n_mp, 3))
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    pts["nx"], pts["ny"], pts["nz"] = nrm[:, 0], nrm[:, 1], nrm[:, 2]
+    pts["max_dist"] = max_dist
+    pts["min_dist"] = max_dist / scale_factor ** (nlevels - 1)
+    ang = (kps["angle"][tgt] + rng.normal(0, 3, n_mp)) % 360
+    pts["angle"] = np.where(rng.random(n_mp) < 0.2, rng.uniform(0, 360, n_mp), ang)
+    pts["octave"] = lvl
+    pts["flags"] = (rng.random(n_mp) < 0.95).astype(np.int32) | ((rng.random(n_mp) < 0.8).astype(np.int32) << 1)
+    bits = np.unpackbits(desc[tgt], axis=1) ^ (rng.random((n_mp, 256)) < 0.08)
+    pdesc = np.packbits(bits, axis=1)
+    Tcw = np.hstack([R, t[:, None]]).astype(np.float32)
+    return Tcw, pts, pdesc, uright

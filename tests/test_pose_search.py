@@ -656,3 +656,37 @@ def test_gpu_project_search_batch(orbref, cuda, mode):
         wn, wm = run_oracle(mode, sc, pp)
         assert int(nm[b]) == wn
         assert np.array_equal(match[b, :len(wm)].cpu().numpy(), wm)
+
+
+def _chain(orbref):
+    """Fourteen MapPoints at one 3D point with one descriptor; twelve features around its projection at
+    growing Hamming distance: each MapPoint (Observations() > 0) takes the next feature."""
+    kps = _tiny(orbref, [(100.0 + i, 100.0) for i in range(12)])
+    desc = np.zeros((12, 32), np.uint8)
+    for i in range(12):
+        desc[i, :i] = 0xFF
+    pts = np.concatenate([_point_at(orbref, 105.5, 100, 10)] * 14)
+    pose = np.concatenate([np.hstack([np.eye(3), np.zeros((3, 1))]).ravel()] * 2).astype(np.float32)
+    return kps, desc, np.full(12, -1, np.float32), np.zeros(12, np.uint8), pose, pts, np.zeros((14, 32), np.uint8)
+
+
+def test_claim_chain(orbref):
+    kps, desc, ur, cl, pose, pts, pd = _chain(orbref)
+    pp = params(th=7.0, mono=1, check_ori=0)
+    n, m = orbref.project_search(0, kps, desc, ur, cl, pose, pts, pd, pp)
+    assert n == 12 and list(m) == list(range(12))
+    pn, pm = run_py("last_frame", (kps, desc, ur, cl, pose, pose[:12].reshape(3, 4), pts, pd), pp)
+    assert pn == n and pm == list(m)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gpu_claim_chain(orbref, cuda, mode):
+    """The replay runs out of its candidate list and scans the window again."""
+    import orbx
+    kps, desc, ur, cl, pose, pts, pd = _chain(orbref)
+    pp = params(th=7.0, mono=1, check_ori=0, orb_dist=100)
+    n, m = orbx.ORBmatcher(0.9, False).project_search(mode, kps, desc, ur, cl, pose, pts, pd,
+                                                        orbx.PoseParams.from_buffer_copy(pp))
+    wn, wm = orbref.project_search(mode, kps, desc, ur, cl, pose, pts, pd, pp)
+    assert n == wn == 12 and np.array_equal(m, wm)

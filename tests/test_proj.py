@@ -187,3 +187,36 @@ def test_gpu_search_by_projection_batch(orbref, cuda):
         wn, wm = orbref.search_by_projection(k, d, u, c, g, SCALE, p, pd, 3.0, 0.8)
         assert int(nm[b]) == wn
         assert np.array_equal(match[b, :len(k)].cpu().numpy(), wm)
+
+
+def _chain_scene(orbref):
+    """Fourteen MapPoints at one spot with one descriptor, twelve features around it at Hamming
+    distances 0, 3, 6, ...: each MapPoint takes the next feature, so the later ones find more
+    than the first eight candidates of their window claimed."""
+    kps = np.zeros(12, orbref.KEYPOINT_DTYPE)
+    kps["x"], kps["y"] = 100.0 + np.arange(12), 100.0
+    desc = np.zeros((12, 32), np.uint8)
+    for i in range(12):
+        desc[i, :i] = 0xFF                                  # distance 8*i
+    pts = np.zeros(14, orbref.PROJ_DTYPE)
+    pts["proj_x"], pts["proj_y"], pts["view_cos"], pts["flags"] = 105.5, 100.0, 1.0, 3
+    pdesc = np.zeros((14, 32), np.uint8)
+    grid = (0.0, 0.0, np.float32(64) / 640, np.float32(48) / 480)
+    return kps, desc, np.full(12, -1, np.float32), np.zeros(12, np.uint8), grid, pts, pdesc
+
+
+def test_claim_chain(orbref):
+    kps, desc, ur, cl, grid, pts, pdesc = _chain_scene(orbref)
+    n, m = orbref.search_by_projection(kps, desc, ur, cl, grid, SCALE, pts, pdesc, 3.0, 0.99)
+    assert n == 12 and list(m) == list(range(12))
+    pn, pm = py_search(kps, desc, ur, cl, grid, SCALE, pts, pdesc, 3.0, 0.99)
+    assert pn == n and np.array_equal(pm, m)
+
+
+@pytest.mark.gpu
+def test_gpu_claim_chain(orbref, cuda):
+    """The replay runs out of its candidate list and scans the window again."""
+    import orbx
+    kps, desc, ur, cl, grid, pts, pdesc = _chain_scene(orbref)
+    n, m = orbx.ORBmatcher(0.99).SearchByProjection(kps, desc, ur, cl, grid, SCALE, pts, pdesc, 3.0)
+    assert n == 12 and list(m) == list(range(12))
