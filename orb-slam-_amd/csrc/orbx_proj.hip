@@ -5,13 +5,14 @@
 // J1 k_pj_grid     one workgroup per frame: (cell, feature) keys of AssignFeaturesToGrid
 //                  sorted in LDS, so a window's columns are one key range and the keys
 //                  run in GetFeaturesInArea's visiting order (ix, then iy, then insertion)
-// J2 k_pj_points   one lane per MapPoint: the reference's sequential best / second scan
-//                  over its window, against the frame's claims on entry
-// J3 k_pj_resolve  one wave per frame replays the MapPoints in order: a MapPoint whose
-//                  best or second candidate was claimed earlier in this call is searched
-//                  again (wave-parallel) against the current claims; the others keep
-//                  their J2 result (a claim on any other candidate changes nothing).
-//                  Claims live in a per-lane register bitmap.
+// J2 k_pj_points   one lane per MapPoint: the reference's sequential scan over its window,
+//                  against the frame's claims on entry, kept as the first kTop candidates in
+//                  (distance, visiting position) order -- best and second are the first two
+// J3 k_pj_resolve  one wave per frame replays the MapPoints in order, 64 at a time
+//                  (replay_chunks): each takes the first unclaimed entries of its list; the
+//                  lanes before the first collision with an earlier lane's claim commit
+//                  together; a MapPoint whose list ran out searches its window again.
+//                  Assignments and claims live in LDS.
 #include <hip/hip_runtime.h>
 
 #include "orbx_kernels.hpp"
@@ -176,13 +177,13 @@ __device__ __forceinline__ void top_insert(TopK& t, uint32_t entry)
     t.n = min(t.n + 1, 255);
 }
 
-// J2 result per MapPoint: the top-kTop list and the accept decision of its first two entries
-struct PjResult {
+// J2 result per MapPoint: the top-kTop list and the accept decision of its first entries
+struct TopResult {
     uint32_t e[kTop];
     int n;        // candidates in the window (not claimed on entry), saturating
-    int accept;   // bestDist <= TH_HIGH and the same-level ratio test passed
-    int pad[2];
+    int accept;   // the reference's accept test on the J2 best (and second)
 };
+using PjResult = TopResult;
 
 __device__ __forceinline__ bool pj_accept(int bestDist, int bestLevel, int bestDist2, int bestLevel2, float nnratio)
 {
@@ -231,7 +232,6 @@ __global__ __launch_bounds__(256) void k_pj_points(const orbx_keypoint* __restri
     for (int k = 0; k < kTop; ++k) R.e[k] = T.e[k];
     R.n = T.n;
     R.accept = accept;
-    R.pad[0] = R.pad[1] = 0;
     res[mo] = R;
 }
 
@@ -245,7 +245,131 @@ __device__ __forceinline__ unsigned long long pj_wave_min_u64(unsigned long long
     return v;
 }
 
-constexpr int kPjBitWords = 2;   // per-lane u64 claim words: 64 lanes x 2 x 64 = 8192 features
+// ---- chunk-parallel, in-order replay of the reference's greedy loop (both searches) ----
+// A claim made earlier in the call only removes candidates, so each MapPoint's result is a function
+// of its J2 list and of the claims of the MapPoints before it.  A chunk of 64 MapPoints settles in
+// rounds: every pending lane takes the first unclaimed entries of its list; the first lane whose
+// choice collides with a claim of an earlier pending lane, or whose list ran out, stops the round;
+// the lanes before it are final and commit together (last writer = the largest MapPoint index,
+// claims, rotation bins); the next round starts at that lane, which now sees every claim before it.
+// A lane whose list ran out searches its window again, wave-parallel, against the claims.
+struct ReplayLds {
+    int* mo;          // [cap] MapPoint assigned to the feature (last writer), -1
+    uint32_t* bins;   // [cap] rotation bins of the matches that assigned the feature
+    int* first;       // [cap] smallest pending lane claiming the feature in this round (64 = none)
+    uint8_t* taken;   // [cap] claimed earlier in this call
+    int* hist;        // [32] rotHist sizes
+};
+
+__device__ __forceinline__ ReplayLds replay_lds(int cap)
+{
+    extern __shared__ int s_replay[];
+    ReplayLds S;
+    S.mo = s_replay;
+    S.bins = reinterpret_cast<uint32_t*>(s_replay + cap);
+    S.first = s_replay + 2 * cap;
+    S.hist = s_replay + 3 * cap;
+    S.taken = reinterpret_cast<uint8_t*>(s_replay + 3 * cap + 32);
+    return S;
+}
+
+inline size_t replay_lds_bytes(int cap) { return (size_t)13 * cap + 128; }
+
+struct ReplayPick {
+    int g, accept, bin;
+};
+
+template <bool kSecond, bool kRot, class ObsFn, class AcceptFn, class RescanFn>
+__device__ __forceinline__ int replay_chunks(int n, int np, const TopResult* __restrict__ R, const ReplayLds& S,
+                                             ObsFn obs_of, AcceptFn accept_of, RescanFn rescan)
+{
+    const int lane = threadIdx.x;
+    for (int i = lane; i < n; i += 64) {
+        S.mo[i] = -1;
+        S.bins[i] = 0u;
+        S.first[i] = 64;
+        S.taken[i] = 0;
+    }
+    if (lane < 32) S.hist[lane] = 0;
+    __syncthreads();
+    int count = 0;
+    for (int base = 0; base < np; base += 64) {
+        const int m = base + lane;
+        TopResult r{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0, 0};
+        int obs = 0;
+        if (m < np) {
+            r = R[m];
+            obs = obs_of(m);
+        }
+        // no candidate, or (single-best searches) a J2 best over the threshold: final, no match
+        bool pending = r.n > 0 && (kSecond || r.accept);
+        unsigned long long pend = __ballot(pending);
+        while (pend) {
+            int k1 = -1, k2 = -1;
+            uint32_t c1 = 0u, c2 = 0u;
+            bool out_of_list = false;
+            if (pending) {
+                const int lim = min(r.n, kTop);
+#pragma unroll
+                for (int k = 0; k < kTop; ++k) {
+                    if (k < lim && (kSecond ? k2 < 0 : k1 < 0) && !S.taken[top_idx(r.e[k])]) {
+                        if (k1 < 0) {
+                            k1 = k;
+                            c1 = r.e[k];
+                        } else {
+                            k2 = k;
+                            c2 = r.e[k];
+                        }
+                    }
+                }
+                out_of_list = (kSecond ? k2 < 0 : k1 < 0) && r.n > kTop;
+            }
+            const bool acc = pending && !out_of_list && k1 >= 0 && accept_of(c1, k2 >= 0, c2);
+            const bool claim = acc && obs;
+            if (claim) atomicMin(&S.first[top_idx(c1)], lane);
+            __syncthreads();
+            bool stop = pending && out_of_list;
+            if (pending && !out_of_list && k1 >= 0)
+                stop = S.first[top_idx(c1)] < lane || (kSecond && k2 >= 0 && S.first[top_idx(c2)] < lane);
+            __syncthreads();
+            if (claim) S.first[top_idx(c1)] = 64;
+            const unsigned long long stops = __ballot(stop);
+            const int j0 = stops ? __builtin_ctzll(stops) : 64;
+            const bool commit = pending && lane < j0;
+            if (commit && acc) {
+                const int g = top_idx(c1);
+                atomicMax(&S.mo[g], m);   // F.mvpMapPoints[bestIdx] = pMP, in MapPoint order
+                if (kRot) {
+                    atomicOr(&S.bins[g], 1u << top_bin(c1));
+                    atomicAdd(&S.hist[top_bin(c1)], 1);
+                }
+                if (obs) S.taken[g] = 1;
+            }
+            count += __popcll(__ballot(commit && acc));
+            if (commit) pending = false;
+            __syncthreads();
+            if (j0 < 64 && __builtin_amdgcn_readlane((int)out_of_list, j0)) {   // wave-uniform
+                const ReplayPick pk = rescan(base + j0, S.taken);
+                if (pk.accept) {
+                    if (lane == 0) {
+                        atomicMax(&S.mo[pk.g], base + j0);
+                        if (kRot) {
+                            atomicOr(&S.bins[pk.g], 1u << pk.bin);
+                            atomicAdd(&S.hist[pk.bin], 1);
+                        }
+                        if (__builtin_amdgcn_readlane(obs, j0)) S.taken[pk.g] = 1;
+                    }
+                    ++count;
+                }
+                if (lane == j0) pending = false;
+                __syncthreads();
+            }
+            pend = __ballot(pending);
+        }
+    }
+    __syncthreads();
+    return count;
+}
 
 __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restrict__ kps,
                                                    const uint8_t* __restrict__ desc, const float* __restrict__ uright,
@@ -256,135 +380,59 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
                                                    const int* __restrict__ gn, const PjResult* __restrict__ res,
                                                    int* __restrict__ match, int* __restrict__ nmatches)
 {
-    // the assignments live in LDS during the replay: a global store inside the serial loop would
-    // hold every later iteration's vmcnt wait until the store is acknowledged
-    extern __shared__ int s_mo[];
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(counts[f], cap), np = min(npts[f], pcap);
-    int* Mo = match + (size_t)f * cap;
-    for (int i = lane; i < n; i += 64) s_mo[i] = -1;
-    __syncthreads();
-    unsigned long long bits[kPjBitWords] = {0ull, 0ull};   // features claimed during this call
+    const ReplayLds S = replay_lds(cap);
     const uint32_t* keys = gkeys + (size_t)f * cap;
     const orbx_keypoint* K = kps + (size_t)f * cap;
     const float* U = uright + (size_t)f * cap;
     const uint8_t* C = claimed + (size_t)f * cap;
+    const orbm_proj_point* Pf = pts + (size_t)f * pcap;
     const int ng = gn[f];
-    auto claimed_now = [&](int idx) -> bool {   // wave-uniform idx
-        const int word = idx >> 6, w = word & 63, h = word >> 6;
-        const unsigned long long b =
-            (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits[h], w) |
-            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits[h] >> 32), w) << 32);
-        return (b >> (idx & 63)) & 1ull;
+    auto obs_of = [&](int m) { return (Pf[m].flags & 2) ? 1 : 0; };
+    auto accept_of = [&](uint32_t c1, bool has2, uint32_t c2) {
+        return pj_accept(top_dist(c1), top_oct(c1), has2 ? top_dist(c2) : 256, has2 ? top_oct(c2) : -1, P.nnratio);
     };
-    int count = 0;
-    for (int base = 0; base < np; base += 64) {
-        const int mm = base + lane;
-        PjResult R{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0, 0, {0, 0}};
-        int obs = 0;
-        if (mm < np) {
-            R = res[(size_t)f * pcap + mm];
-            obs = (pts[(size_t)f * pcap + mm].flags & 2) ? 1 : 0;
-        }
-        unsigned long long live = __ballot(R.n > 0);   // no candidate on entry: nothing to replay
-        while (live) {
-            const int j = __builtin_ctzll(live);
-            live &= live - 1;
-            uint32_t e[kTop];
-#pragma unroll
-            for (int k = 0; k < kTop; ++k) e[k] = (uint32_t)__builtin_amdgcn_readlane((int)R.e[k], j);
-            const int nc = __builtin_amdgcn_readlane(R.n, j);
-            int best = top_idx(e[0]);
-            const int second = nc > 1 ? top_idx(e[1]) : -1;
-            int accept = __builtin_amdgcn_readlane(R.accept, j);
-            const int o = __builtin_amdgcn_readlane(obs, j);
-            bool rescan = false;
-            if (claimed_now(best) || (second >= 0 && claimed_now(second))) {
-                // the first two unclaimed entries of the list, unless the list runs out
-                int k1 = -1, k2 = -1;
-#pragma unroll
-                for (int k = 0; k < kTop; ++k) {
-                    if (k < nc && k2 < 0 && !claimed_now(top_idx(e[k]))) {
-                        if (k1 < 0) k1 = k; else k2 = k;
-                    }
-                }
-                if (k2 < 0 && nc > kTop) {
-                    rescan = true;
-                } else {
-                    uint32_t e1 = 0, e2 = 0;
-#pragma unroll
-                    for (int k = 0; k < kTop; ++k) {
-                        if (k == k1) e1 = e[k];
-                        if (k == k2) e2 = e[k];
-                    }
-                    best = k1 >= 0 ? top_idx(e1) : -1;
-                    accept = k1 >= 0 && pj_accept(top_dist(e1), top_oct(e1), k2 >= 0 ? top_dist(e2) : 256,
-                                                  k2 >= 0 ? top_oct(e2) : -1, P.nnratio);
+    // search again against the current claims: best = first min of (dist, position), second = first
+    // min of the rest (the sequential scan's result)
+    auto rescan = [&](int m, const uint8_t* taken) {
+        const orbm_proj_point Mp = Pf[m];
+        const PjWindow w = pj_window(Mp, P, keys, ng);
+        const uint4* qd = reinterpret_cast<const uint4*>(pdesc + ((size_t)f * pcap + m) * 32);
+        const uint4 q0 = qd[0], q1 = qd[1];
+        unsigned long long b1 = ~0ull, b2 = ~0ull;
+        for (int p0 = w.lo; p0 < w.hi; p0 += 64) {
+            const int p = p0 + lane;
+            unsigned long long key = ~0ull;
+            if (p < w.hi) {
+                const int idx = pj_candidate(w, Mp, keys, p, K, U);
+                if (idx >= 0 && !C[idx] && !taken[idx]) {
+                    const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
+                    key = ((unsigned long long)pj_ham(q0, q1, d[0], d[1]) << 32) | ((unsigned long long)p << 16) |
+                          (unsigned)idx;
                 }
             }
-            if (rescan) {
-                // search again against the current claims: best = first min of (dist, position),
-                // second = first min of the rest (the sequential scan's result)
-                const int m = base + j;
-                const size_t mo = (size_t)f * pcap + m;
-                const orbm_proj_point Mp = pts[mo];
-                const PjWindow w = pj_window(Mp, P, keys, ng);
-                const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
-                const uint4 q0 = qd[0], q1 = qd[1];
-                // candidates in position order, 64 at a time; claims made during this call are
-                // tested one candidate lane at a time (claimed_now needs a uniform index)
-                unsigned long long b1 = ~0ull, b2 = ~0ull;
-                for (int p0 = w.lo; p0 < w.hi; p0 += 64) {
-                    const int p = p0 + lane;
-                    unsigned long long key = ~0ull;
-                    int idx = -1;
-                    if (p < w.hi) {
-                        idx = pj_candidate(w, Mp, keys, p, K, U);
-                        if (idx >= 0 && !C[idx]) {
-                            const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
-                            const int dist = pj_ham(q0, q1, d[0], d[1]);
-                            key = ((unsigned long long)dist << 32) | ((unsigned long long)p << 16) | (unsigned)idx;
-                        }
-                    }
-                    unsigned long long live = __ballot(key != ~0ull);
-                    while (live) {   // claims made in this call: test each candidate lane in turn
-                        const int l = __builtin_ctzll(live);
-                        live &= live - 1;
-                        const int cidx = __builtin_amdgcn_readlane(idx, l);
-                        if (claimed_now(cidx) && lane == l) key = ~0ull;
-                    }
-                    const unsigned long long c1 = pj_wave_min_u64(key);
-                    const unsigned long long c2 = pj_wave_min_u64(key == c1 ? ~0ull : key);
-                    // merge into the running (b1, b2): the multiset top two by (dist, position)
-                    if (c1 < b1) {
-                        b2 = min(b1, c2);
-                        b1 = c1;
-                    } else {
-                        b2 = min(b2, c1);
-                    }
-                }
-                best = b1 == ~0ull ? -1 : (int)(b1 & 0xFFFF);
-                accept = 0;
-                if (best >= 0) {
-                    const int bd = (int)(b1 >> 32);
-                    const int bl = K[best].octave;
-                    const int bd2 = b2 == ~0ull ? 256 : (int)(b2 >> 32);
-                    const int bl2 = b2 == ~0ull ? -1 : K[(int)(b2 & 0xFFFF)].octave;
-                    accept = pj_accept(bd, bl, bd2, bl2, P.nnratio);
-                }
-            }
-            if (best >= 0 && accept) {
-                if (lane == 0) s_mo[best] = base + j;   // F.mvpMapPoints[bestIdx] = pMP (last writer)
-                ++count;
-                if (o) {
-                    const int word = best >> 6;
-                    if (lane == (word & 63)) bits[word >> 6] |= 1ull << (best & 63);
-                }
+            const unsigned long long c1 = pj_wave_min_u64(key);
+            const unsigned long long c2 = pj_wave_min_u64(key == c1 ? ~0ull : key);
+            if (c1 < b1) {   // merge: the multiset top two by (dist, position)
+                b2 = min(b1, c2);
+                b1 = c1;
+            } else {
+                b2 = min(b2, c1);
             }
         }
-    }
-    __syncthreads();
-    for (int i = lane; i < n; i += 64) Mo[i] = s_mo[i];
+        ReplayPick pk{-1, 0, 0};
+        if (b1 != ~0ull) {
+            pk.g = (int)(b1 & 0xFFFF);
+            const int bd2 = b2 == ~0ull ? 256 : (int)(b2 >> 32);
+            const int bl2 = b2 == ~0ull ? -1 : K[(int)(b2 & 0xFFFF)].octave;
+            pk.accept = pj_accept((int)(b1 >> 32), K[pk.g].octave, bd2, bl2, P.nnratio);
+        }
+        return pk;
+    };
+    const int count = replay_chunks<true, false>(n, np, res + (size_t)f * pcap, S, obs_of, accept_of, rescan);
+    int* Mo = match + (size_t)f * cap;
+    for (int i = lane; i < n; i += 64) Mo[i] = S.mo[i];
     if (lane == 0) nmatches[f] = count;
 }
 
@@ -408,9 +456,10 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
                        P.grid_w_inv, P.grid_h_inv, gkeys, gn);
     hipLaunchKernelGGL(k_pj_points, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright, claimed,
                        cap, pts, pdesc, npts, pcap, P, gkeys, gn, res);
-    hipFuncSetAttribute((const void*)k_pj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * cap);
-    hipLaunchKernelGGL(k_pj_resolve, dim3(nframes), dim3(64), (size_t)4 * cap, s, kps, desc, uright, claimed, counts,
-                       cap, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+    hipFuncSetAttribute((const void*)k_pj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)replay_lds_bytes(cap));
+    hipLaunchKernelGGL(k_pj_resolve, dim3(nframes), dim3(64), replay_lds_bytes(cap), s, kps, desc, uright, claimed,
+                       counts, cap, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
 }
 
 // =====================================================================================
@@ -422,9 +471,9 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
 // J2 k_ps_points   one lane per MapPoint: project with the frame pose, scan the window in
 //                  GetFeaturesInArea order against the claims on entry (first minimum).
 //                  The Fuse overloads claim nothing during the search: they finish here.
-// J3 k_ps_resolve  one wave per frame replays the three searches in MapPoint order; a
-//                  MapPoint whose best candidate was taken earlier in the call searches
-//                  again against the current claims; then the rotation histogram.
+// J3 k_ps_resolve  one wave per frame replays the three searches in MapPoint order with
+//                  replay_chunks (above), then the rotation histogram from per-feature bin
+//                  masks in LDS.
 // Float arithmetic is oracle/orbref.c proj_* operation for operation (no contraction in this
 // file; the reference's GCC -march=native FMAs are explicit).
 // =====================================================================================
@@ -613,10 +662,7 @@ __device__ __forceinline__ int ps_rot_bin(float a1, float a2)
     return bin;
 }
 
-struct PsResult {
-    uint32_t e[kTop];   // top-kTop list (TopK), bins filled for the rotation-checked searches
-    int n, accept;
-};
+using PsResult = TopResult;   // bins filled for the rotation-checked searches
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_ps_points(const orbx_keypoint* __restrict__ kps,
@@ -688,139 +734,65 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
                                                    const uint8_t* __restrict__ pdesc, const int* __restrict__ npts,
                                                    int pcap, orbm_pose_params P, const uint32_t* __restrict__ gkeys,
                                                    const int* __restrict__ gn, const PsResult* __restrict__ res,
-                                                   int* __restrict__ ent, int* __restrict__ match,
-                                                   int* __restrict__ nmatches)
+                                                   int* __restrict__ match, int* __restrict__ nmatches)
 {
-    // assignments and, per feature, the rotation bins of the matches that assigned it, in LDS (a
-    // global store inside the serial loop would hold every later vmcnt wait for its acknowledgement)
-    extern __shared__ int s_mo[];
-    uint32_t* s_bins = reinterpret_cast<uint32_t*>(s_mo + cap);
+    constexpr bool kRotMode = MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME;
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(counts[f], cap), np = min(npts[f], pcap);
-    int* Mo = match + (size_t)f * cap;
-    for (int i = lane; i < n; i += 64) {
-        s_mo[i] = -1;
-        s_bins[i] = 0u;
-    }
-    __syncthreads();
-    unsigned long long bits[kPjBitWords] = {0ull, 0ull};   // features claimed during this call
+    const ReplayLds S = replay_lds(cap);
     const uint32_t* keys = gkeys + (size_t)f * cap;
     const orbx_keypoint* K = kps + (size_t)f * cap;
     const float* U = uright + (size_t)f * cap;
     const uint8_t* C = claimed + (size_t)f * cap;
+    const orbm_map_point* Pf = pts + (size_t)f * pcap;
     const int ng = gn[f];
     const PsCam cam = ps_camera(MODE, pose + (size_t)f * 24, P);
-    const bool rot = P.check_ori && (MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME);
-    auto claimed_now = [&](int idx) -> bool {   // wave-uniform idx
-        const int word = idx >> 6, w = word & 63, h = word >> 6;
-        const unsigned long long b =
-            (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits[h], w) |
-            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits[h] >> 32), w) << 32);
-        return (b >> (idx & 63)) & 1ull;
+    const bool rot = kRotMode && P.check_ori;
+    const int thr = ps_threshold<MODE>(P);
+    // LAST_FRAME claims a feature only for a MapPoint with Observations() > 0 (:1471-1473); the
+    // other searches skip every feature already assigned (:1609-1610, :375-376)
+    auto obs_of = [&](int m) { return MODE != ORBM_PROJ_LAST_FRAME || (Pf[m].flags & 2) ? 1 : 0; };
+    auto accept_of = [&](uint32_t c1, bool, uint32_t) { return top_dist(c1) <= thr; };
+    auto rescan = [&](int m, const uint8_t* taken) {
+        const orbm_map_point Mp = Pf[m];
+        PsWin w;
+        ps_project<MODE>(cam, Mp, P, w);   // true and non-empty: J2 found candidates in it
+        ps_window(w, P, keys, ng);
+        const uint4* qd = reinterpret_cast<const uint4*>(pdesc + ((size_t)f * pcap + m) * 32);
+        const uint4 q0 = qd[0], q1 = qd[1];
+        unsigned long long b1 = ~0ull;
+        for (int p0 = w.lo; p0 < w.hi; p0 += 64) {
+            const int p = p0 + lane;
+            unsigned long long key = ~0ull;
+            if (p < w.hi) {
+                const int idx = ps_candidate<MODE>(w, keys, p, K, U, P);
+                if (idx >= 0 && !C[idx] && !taken[idx]) {
+                    const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
+                    key = ((unsigned long long)pj_ham(q0, q1, d[0], d[1]) << 32) | ((unsigned long long)p << 16) |
+                          (unsigned)idx;
+                }
+            }
+            const unsigned long long c1 = pj_wave_min_u64(key);
+            b1 = c1 < b1 ? c1 : b1;
+        }
+        ReplayPick pk{-1, 0, 0};
+        if (b1 != ~0ull) {
+            pk.g = (int)(b1 & 0xFFFF);
+            pk.accept = (int)(b1 >> 32) <= thr;
+            if (rot) pk.bin = ps_rot_bin(Mp.angle, K[pk.g].angle);
+        }
+        return pk;
     };
-    int count = 0, hist = 0;   // lane b holds rotHist[b].size()
-    for (int base = 0; base < np; base += 64) {
-        const int mm = base + lane;
-        PsResult R{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0, 0};
-        int obs = 0;
-        float ang = 0.0f;   // for a search again
-        if (mm < np) {
-            R = res[(size_t)f * pcap + mm];
-            const orbm_map_point& Mp = pts[(size_t)f * pcap + mm];
-            obs = MODE != ORBM_PROJ_LAST_FRAME || (Mp.flags & 2);
-            ang = Mp.angle;
-        }
-        // only accepted J2 results can produce a match: a claim removes candidates, so a search
-        // again finds a distance >= the J2 one, which the threshold still rejects
-        unsigned long long live = __ballot(R.n > 0 && R.accept);
-        while (live) {
-            const int j = __builtin_ctzll(live);
-            live &= live - 1;
-            uint32_t e[kTop];
-#pragma unroll
-            for (int k = 0; k < kTop; ++k) e[k] = (uint32_t)__builtin_amdgcn_readlane((int)R.e[k], j);
-            const int nc = __builtin_amdgcn_readlane(R.n, j);
-            int best = top_idx(e[0]), bin = top_bin(e[0]);
-            int accept = 1;
-            bool rescan = false;
-            if (claimed_now(best)) {   // the first unclaimed entry of the list, unless it runs out
-                int k1 = -1;
-#pragma unroll
-                for (int k = 1; k < kTop; ++k)
-                    if (k < nc && k1 < 0 && !claimed_now(top_idx(e[k]))) k1 = k;
-                if (k1 < 0 && nc > kTop) {
-                    rescan = true;
-                } else {
-                    uint32_t e1 = 0;
-#pragma unroll
-                    for (int k = 1; k < kTop; ++k)
-                        if (k == k1) e1 = e[k];
-                    best = k1 >= 0 ? top_idx(e1) : -1;
-                    bin = top_bin(e1);
-                    accept = k1 >= 0 && top_dist(e1) <= ps_threshold<MODE>(P);
-                }
-            }
-            if (rescan) {
-                const int m = base + j;
-                const size_t mo = (size_t)f * pcap + m;
-                const orbm_map_point Mp = pts[mo];
-                PsWin w;
-                ps_project<MODE>(cam, Mp, P, w);   // true and non-empty: J2 found `best` in it
-                ps_window(w, P, keys, ng);
-                const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
-                const uint4 q0 = qd[0], q1 = qd[1];
-                unsigned long long b1 = ~0ull;
-                for (int p0 = w.lo; p0 < w.hi; p0 += 64) {
-                    const int p = p0 + lane;
-                    unsigned long long key = ~0ull;
-                    int idx = -1;
-                    if (p < w.hi) {
-                        idx = ps_candidate<MODE>(w, keys, p, K, U, P);
-                        if (idx >= 0 && !C[idx]) {
-                            const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
-                            const int dist = pj_ham(q0, q1, d[0], d[1]);
-                            key = ((unsigned long long)dist << 32) | ((unsigned long long)p << 16) | (unsigned)idx;
-                        }
-                    }
-                    unsigned long long live = __ballot(key != ~0ull);
-                    while (live) {
-                        const int l = __builtin_ctzll(live);
-                        live &= live - 1;
-                        const int cidx = __builtin_amdgcn_readlane(idx, l);
-                        if (claimed_now(cidx) && lane == l) key = ~0ull;
-                    }
-                    const unsigned long long c1 = pj_wave_min_u64(key);
-                    b1 = c1 < b1 ? c1 : b1;
-                }
-                best = b1 == ~0ull ? -1 : (int)(b1 & 0xFFFF);
-                accept = best >= 0 && (int)(b1 >> 32) <= ps_threshold<MODE>(P);
-                if (accept && rot) {
-                    const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), j));
-                    bin = ps_rot_bin(a1, K[best].angle);
-                }
-            }
-            if (best < 0 || !accept) continue;
-            if (lane == 0) {
-                s_mo[best] = base + j;   // mvpMapPoints[bestIdx] = pMP
-                if (rot) s_bins[best] |= 1u << bin;
-            }
-            ++count;
-            if (__builtin_amdgcn_readlane(obs, j)) {
-                const int word = best >> 6;
-                if (lane == (word & 63)) bits[word >> 6] |= 1ull << (best & 63);
-            }
-            if (rot) hist += lane == bin;
-        }
-    }
-    __syncthreads();
+    int count = rot ? replay_chunks<false, true>(n, np, res + (size_t)f * pcap, S, obs_of, accept_of, rescan)
+                    : replay_chunks<false, false>(n, np, res + (size_t)f * pcap, S, obs_of, accept_of, rescan);
     uint32_t drop = 0u;   // the bins outside the three maxima
-    if (rot) {   // ComputeThreeMaxima (:1679-1723) and the NULL-ing of the other bins
+    if (rot) {            // ComputeThreeMaxima (:1679-1723); every match in another bin is undone
         int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;
         for (int i = 0; i < 30; ++i) {
-            const int s = __builtin_amdgcn_readlane(hist, i);
-            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-            else if (s > max3) { max3 = s; ind3 = i; }
+            const int h = S.hist[i];
+            if (h > max1) { max3 = max2; max2 = max1; max1 = h; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (h > max2) { max3 = max2; max2 = h; ind3 = ind2; ind2 = i; }
+            else if (h > max3) { max3 = h; ind3 = i; }
         }
         if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
@@ -828,36 +800,34 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
         if (ind1 >= 0) drop &= ~(1u << ind1);
         if (ind2 >= 0) drop &= ~(1u << ind2);
         if (ind3 >= 0) drop &= ~(1u << ind3);
-        // every match in a dropped bin is undone (nmatches--), and its feature set to NULL
-        const int removed_here = (lane < 30 && ((drop >> lane) & 1u)) ? hist : 0;
-        int removed = removed_here;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) removed += __shfl_xor(removed, o);
-        count -= removed;
+        for (int i = 0; i < 30; ++i)
+            if ((drop >> i) & 1u) count -= S.hist[i];
     }
-    for (int i = lane; i < n; i += 64) Mo[i] = (s_bins[i] & drop) ? -2 : s_mo[i];
+    int* Mo = match + (size_t)f * cap;
+    for (int i = lane; i < n; i += 64) Mo[i] = (S.bins[i] & drop) ? -2 : S.mo[i];   // NULL-ed by the filter
     if (lane == 0) nmatches[f] = count;
 }
 
 size_t pose_scratch_bytes(int nframes, int cap, int pcap)
 {
-    return (size_t)nframes * cap * 4 + (size_t)nframes * 4 + (size_t)nframes * pcap * (sizeof(PsResult) + 4) + 256;
+    return (size_t)nframes * cap * 4 + (size_t)nframes * 4 + (size_t)nframes * pcap * sizeof(PsResult) + 256;
 }
 
 template <int MODE>
 static void ps_launch(const orbx_keypoint* kps, const uint8_t* desc, const float* uright, const uint8_t* claimed,
                       const int* counts, int nframes, int cap, const float* pose, const orbm_map_point* pts,
                       const uint8_t* pdesc, const int* npts, int pcap, const orbm_pose_params& P,
-                      const uint32_t* gkeys, const int* gn, PsResult* res, int* ent, int* match, int* nmatches,
+                      const uint32_t* gkeys, const int* gn, PsResult* res, int* match, int* nmatches,
                       hipStream_t s)
 {
     if (MODE >= ORBM_FUSE) hipMemsetAsync(nmatches, 0, sizeof(int) * (size_t)nframes, s);
     hipLaunchKernelGGL(k_ps_points<MODE>, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright,
                        claimed, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
     if (MODE <= ORBM_PROJ_SIM3) {
-        hipFuncSetAttribute((const void*)k_ps_resolve<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * cap);
-        hipLaunchKernelGGL(k_ps_resolve<MODE>, dim3(nframes), dim3(64), (size_t)8 * cap, s, kps, desc, uright, claimed,
-                           counts, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, ent, match, nmatches);
+        hipFuncSetAttribute((const void*)k_ps_resolve<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)replay_lds_bytes(cap));
+        hipLaunchKernelGGL(k_ps_resolve<MODE>, dim3(nframes), dim3(64), replay_lds_bytes(cap), s, kps, desc, uright,
+                           claimed, counts, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
     }
 }
 
@@ -869,7 +839,6 @@ void launch_pose_search(int mode, const orbx_keypoint* kps, const uint8_t* desc,
     uint32_t* gkeys = (uint32_t*)scratch;
     int* gn = (int*)(gkeys + (size_t)nframes * cap);
     PsResult* res = (PsResult*)(((uintptr_t)(gn + nframes) + 15) & ~(uintptr_t)15);
-    int* ent = (int*)(res + (size_t)nframes * pcap);
     int p2 = 1;
     while (p2 < cap) p2 <<= 1;
     hipFuncSetAttribute((const void*)k_pj_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * p2));
@@ -878,23 +847,23 @@ void launch_pose_search(int mode, const orbx_keypoint* kps, const uint8_t* desc,
     switch (mode) {
     case ORBM_PROJ_LAST_FRAME:
         ps_launch<ORBM_PROJ_LAST_FRAME>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap,
-                                        P, gkeys, gn, res, ent, match, nmatches, s);
+                                        P, gkeys, gn, res, match, nmatches, s);
         break;
     case ORBM_PROJ_KEYFRAME:
         ps_launch<ORBM_PROJ_KEYFRAME>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap,
-                                      P, gkeys, gn, res, ent, match, nmatches, s);
+                                      P, gkeys, gn, res, match, nmatches, s);
         break;
     case ORBM_PROJ_SIM3:
         ps_launch<ORBM_PROJ_SIM3>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap, P,
-                                  gkeys, gn, res, ent, match, nmatches, s);
+                                  gkeys, gn, res, match, nmatches, s);
         break;
     case ORBM_FUSE:
         ps_launch<ORBM_FUSE>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap, P, gkeys,
-                             gn, res, ent, match, nmatches, s);
+                             gn, res, match, nmatches, s);
         break;
     default:
         ps_launch<ORBM_FUSE_SIM3>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap, P,
-                                  gkeys, gn, res, ent, match, nmatches, s);
+                                  gkeys, gn, res, match, nmatches, s);
         break;
     }
 }
