@@ -926,6 +926,12 @@ constexpr int kRawSlots = kRawRows * kRawP / 4;
 constexpr int kTCols = 40, kTP = 22;                  // row-blurred, transposed: [col][row pairs], 22 dwords/col
 constexpr int kDescPerWave = 4;                       // keypoints per wave (lane state set up once per wave)
 
+// Horizontal-pass items (row pair rp << 8 | column group cg) that BRIEF can read: a sample
+// (18 + xx, 18 + yy) has |(x, y)| <= 18.39 before rounding (the pattern's largest radius), so a
+// column group needs only the row pairs its disc chord reaches, plus the 7-tap reach of
+// blur_at.  189 of the 22 x 10 items: three per lane, row-pair major so that the lanes of a
+// load read neighbouring raw dwords (distinct LDS banks).
+__constant__ uint16_t c_blur_items[192] = {2,3,4,5,6,257,258,259,260,261,262,263,513,514,515,516,517,518,519,768,769,770,771,772,773,774,775,776,1024,1025,1026,1027,1028,1029,1030,1031,1032,1280,1281,1282,1283,1284,1285,1286,1287,1288,1536,1537,1538,1539,1540,1541,1542,1543,1544,1545,1792,1793,1794,1795,1796,1797,1798,1799,1800,1801,2048,2049,2050,2051,2052,2053,2054,2055,2056,2057,2304,2305,2306,2307,2308,2309,2310,2311,2312,2313,2560,2561,2562,2563,2564,2565,2566,2567,2568,2569,2816,2817,2818,2819,2820,2821,2822,2823,2824,2825,3072,3073,3074,3075,3076,3077,3078,3079,3080,3081,3328,3329,3330,3331,3332,3333,3334,3335,3336,3337,3584,3585,3586,3587,3588,3589,3590,3591,3592,3593,3840,3841,3842,3843,3844,3845,3846,3847,3848,3849,4096,4097,4098,4099,4100,4101,4102,4103,4104,4352,4353,4354,4355,4356,4357,4358,4359,4360,4609,4610,4611,4612,4613,4614,4615,4616,4865,4866,4867,4868,4869,4870,4871,5122,5123,5124,5125,5126,5127,5379,5380,5381,5382,65535,65535,65535};
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
 __device__ __forceinline__ int reflect101(int p, int len)
@@ -995,19 +1001,30 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
     const int g0 = (bx * 4 + wave) * kDescPerWave;
 
     // ---- keypoint-independent lane state, set up once for the wave's keypoints ----
-    // IC_Angle: the lane owns disc column u = (lane & 31) - 15 (lanes 31, 63 idle) and the
-    // rows v = -15..0 (lanes 0..31) or v = 1..15 (lanes 32..63), 16 row steps k.  The
-    // disc |u| <= umax[|v|] is |v| <= vmax(|u|) (umax is non-increasing), i.e. a k range.
-    const int hu = lane & 31, half = lane >> 5;
-    const int u = hu - 15, au = u < 0 ? -u : u;
-    int vmax = -1;
-    if (hu < 31)
-        for (int v = 0; v < 16; ++v)
-            if (au <= c_umax[v]) vmax = v;
-    const int klo = half ? 0 : 15 - vmax, khi = half ? vmax - 1 : 15;   // empty when vmax < 0
-    const uint32_t kmask = klo > khi ? 0u : ((2u << khi) - 1u) & ~((1u << klo) - 1u);
-    const int voff = half ? 1 : -15;   // v = k + voff; raw row = 21 + v
-    const uint8_t* icb = raw + (half ? 22 : 6) * kRawP + 21 + u;
+    // IC_Angle: lane 2i + h owns disc row v = i - 15 (i < 31), half h: u = -15..0 or 1..15, as
+    // 4 realigned dwords of the raw row dotted (v_dot4_u32_u8) with per-lane weights that are
+    // zero outside |u| <= umax[|v|]: (u + 16) for m10 (minus 16 * sum I) and 1 for sum I.
+    const int icv = lane >> 1, ich = lane & 1;
+    const int vrow = icv - 15;
+    const int rmax = icv < 31 ? c_umax[vrow < 0 ? -vrow : vrow] : -1;
+    uint32_t W1[4], W0[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        W1[k] = 0u;
+        W0[k] = 0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int uu = (ich ? 1 : -15) + 4 * k + b;
+            if (uu <= (ich ? 15 : 0) && (uu < 0 ? -uu : uu) <= rmax) {
+                W1[k] |= (uint32_t)(uu + 16) << (8 * b);
+                W0[k] |= 1u << (8 * b);
+            }
+        }
+    }
+    const int ic_row = 21 + vrow, ic_col = ich ? 22 : 6;   // raw row, patch column of the first pixel
+    int bitem[3];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) bitem[it] = c_blur_items[lane + 64 * it];
     // rBRIEF: this lane's 8 tests (word wd = lane + 64 wd), pattern points as floats
     float ppx[8], ppy[8];
 #pragma unroll
@@ -1082,26 +1099,29 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this keypoint's DMA has landed
         wave_lds_sync();
 
-        // IC_Angle: m10 = sum u*I = u * (column sum), m01 = sum v*I = t + voff * (column sum).
-        // Rows 6+k and 22+k have the same shift (16*pitch = 0 mod 4), period 4 in k.
-        const uint8_t* icr[4];
+        // IC_Angle (src/ORBextractor.cc:84-128): integer moments over the disc, any order
+        const int icb0 = ic_row * kRawP + ((csb + ic_row * csp) & 3) + ic_col;
+        const uint32_t* icq = raw32 + (icb0 >> 2);
+        const uint32_t icsh = (uint32_t)(icb0 & 3);
+        const uint32_t q0 = icq[0], q1 = icq[1], q2 = icq[2], q3 = icq[3], q4 = icq[4];
+        const uint32_t iw[4] = {__builtin_amdgcn_alignbyte(q1, q0, icsh), __builtin_amdgcn_alignbyte(q2, q1, icsh),
+                                __builtin_amdgcn_alignbyte(q3, q2, icsh), __builtin_amdgcn_alignbyte(q4, q3, icsh)};
+        uint32_t s1 = 0u, s0 = 0u;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) icr[m] = icb + ((csb + (6 + m) * csp) & 3);
-        int csum = 0, t = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int val = icr[k & 3][k * kRawP] & ((int)(kmask << (31 - k)) >> 31);
-            csum += val;
-            t += k * val;
+        for (int k = 0; k < 4; ++k) {
+            s1 = __builtin_amdgcn_udot4(iw[k], W1[k], s1, false);
+            s0 = __builtin_amdgcn_udot4(iw[k], W0[k], s0, false);
         }
-        const int m10 = wave_sum(u * csum);
-        const int m01 = wave_sum(t + voff * csum);
+        const int m10 = wave_sum((int)s1 - 16 * (int)s0);
+        const int m01 = wave_sum(vrow * (int)s0);
 
         // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns
         const uint32_t K0 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
         const uint32_t K1 = 49u | (34u << 8) | (18u << 16);
-        for (int i = lane; i < 22 * 10; i += 64) {
-            const int rp = i / 10, cg = i - rp * 10;
+#pragma unroll
+        for (int it = 0; it < 3; ++it) {
+            if (bitem[it] == 0xFFFF) break;
+            const int rp = bitem[it] >> 8, cg = bitem[it] & 0xFF;
             uint32_t o[2][4];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
