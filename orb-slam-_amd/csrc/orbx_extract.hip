@@ -450,7 +450,6 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
 // reference uses heap addresses).
 // ---------------------------------------------------------------------------
 constexpr int QT_NT = 512;
-constexpr int QT_KPT = 24;
 constexpr int QT_NW = QT_NT / 64;
 constexpr uint16_t kNone = 0xFFFF;
 
@@ -557,7 +556,8 @@ size_t quadtree_smem_bytes(const Geometry& g) { return qt_layout(g.lcap, g.max_c
 // shared scalar slots
 enum { SH_N = 0, SH_L, SH_PHASE, SH_M, SH_DONE, SH_KK, SH_ERR, SH_S, SH_C, SH_NEWL };
 
-__global__ __launch_bounds__(QT_NT) void k_quadtree(const Geometry* __restrict__ G,
+template <int QT_KPT>
+__global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* __restrict__ G,
                                                    const Cell* __restrict__ cells,
                                                    const uint32_t* __restrict__ slots,
                                                    const int* __restrict__ cell_counts,
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(const Geometry* __restrict__
                                                    int* __restrict__ frame_counts, int* __restrict__ status)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int l = blockIdx.x, f = blockIdx.y;
+    const int l = level0 + blockIdx.x, f = blockIdx.y;
     const int tid = threadIdx.x;
     const LevelGeom& LG = G->lv[l];
     const int lcap = G->lcap;
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(const Geometry* __restrict__
     {
         int off = 0;
         for (int q = 0; q < l; ++q) {
-            const int extra = G->lv[q].slot_cap - QT_NT * QT_KPT;
+            const int extra = G->lv[q].slot_cap - QT_NT * qt_kpt(q);
             off += extra > 0 ? extra : 0;
         }
         fspill += off;
@@ -894,10 +894,19 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(const Geometry* __restrict__
 void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s)
 {
     const size_t smem = quadtree_smem_bytes(g);
-    hipFuncSetAttribute((const void*)k_quadtree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    dim3 grid(g.nlevels, batch);
-    hipLaunchKernelGGL(k_quadtree, grid, dim3(QT_NT), smem, s, b.geom, b.cells, b.slots, b.cell_counts,
-                       b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+    // register capacity per level (qt_kpt): level 0 holds most candidates; levels >= 2 hold a
+    // few hundred, and their small register file lets describe / FAST waves share the CU
+    hipFuncSetAttribute((const void*)k_quadtree<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipFuncSetAttribute((const void*)k_quadtree<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipFuncSetAttribute((const void*)k_quadtree<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL(k_quadtree<16>, dim3(1, batch), dim3(QT_NT), smem, s, 0, b.geom, b.cells, b.slots,
+                       b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+    if (g.nlevels > 1)
+        hipLaunchKernelGGL(k_quadtree<8>, dim3(1, batch), dim3(QT_NT), smem, s, 1, b.geom, b.cells, b.slots,
+                           b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+    if (g.nlevels > 2)
+        hipLaunchKernelGGL(k_quadtree<2>, dim3(g.nlevels - 2, batch), dim3(QT_NT), smem, s, 2, b.geom, b.cells,
+                           b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
 }
 
 // ---------------------------------------------------------------------------

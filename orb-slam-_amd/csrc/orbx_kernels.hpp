@@ -50,6 +50,8 @@ enum : int {
 };
 
 size_t quadtree_smem_bytes(const Geometry& g);
+// quadtree keypoints held in registers per thread (512 threads) at level l; the rest spill to global
+__host__ __device__ inline int qt_kpt(int l) { return l == 0 ? 16 : (l == 1 ? 8 : 2); }
 
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);

@@ -53,6 +53,7 @@ CONFIGS = [
     ("euroc", 752, 480, 1000, "gen"),
     ("small", 320, 240, 300, "gen"),
     ("kitti_init2x", 1241, 376, 4000, "kitti"),
+    ("hd1080", 1920, 1080, 4000, "gen"),   # config 5; quadtree levels 0 and 2+ overflow their registers
 ]
 
 
