@@ -46,7 +46,7 @@ __device__ __forceinline__ const uint8_t* level_base(const FramePtrs& P, const G
 // (11-bit coefficients, 22-bit vertical rounding) — SURVEY.md A.2.
 // Coefficient tables are built on the host exactly like OpenCV builds them.
 // ---------------------------------------------------------------------------
-constexpr int kPyrRows = 4;
+constexpr int kPyrRows = 8;
 
 __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
                                                        const int2* __restrict__ xtab,
@@ -82,30 +82,37 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
     __syncthreads();
     const uint8_t* S = (const uint8_t*)s_src;
     const int srow = nd * 4;
-    for (int j = threadIdx.x; j < dyn * ((D.w + 3) >> 2); j += 256) {
-        const int q = (D.w + 3) >> 2;
-        const int rr = j / q, dx0 = (j - rr * q) * 4;
-        const int dy = dy0 + rr;
-        const int2 yt = ytab[D.ytab_off + dy];
-        const uint8_t* r0 = S + ((yt.x & 0xFFFF) - sy0) * srow;
-        const uint8_t* r1 = S + ((int)((uint32_t)yt.x >> 16) - sy0) * srow;
-        const int b0 = yt.y & 0xFFFF, b1 = (int)((uint32_t)yt.y >> 16);
-        uint32_t packed = 0;
+    // a thread owns a group of 4 output columns: their coefficients are loaded once and
+    // reused for the block's rows
+    const int q = (D.w + 3) >> 2;
+    uint8_t* drow0 = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy0 * D.pitch;
+    for (int g = threadIdx.x; g < q; g += 256) {
+        const int dx0 = g * 4;
+        int x0[4], x1[4], a0[4], a1[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int dx = dx0 + k;
-            if (dx < D.w) {
-                const int2 xt = xtab[D.xtab_off + dx];
-                const int x0 = xt.x & 0xFFFF, x1 = (int)((uint32_t)xt.x >> 16);
-                const int a0 = xt.y & 0xFFFF, a1 = (int)((uint32_t)xt.y >> 16);
-                const int h0 = r0[x0] * a0 + r0[x1] * a1;
-                const int h1 = r1[x0] * a0 + r1[x1] * a1;
+            const int2 xt = xtab[D.xtab_off + min(dx0 + k, D.w - 1)];
+            x0[k] = xt.x & 0xFFFF;
+            x1[k] = (int)((uint32_t)xt.x >> 16);
+            a0[k] = xt.y & 0xFFFF;
+            a1[k] = (int)((uint32_t)xt.y >> 16);
+        }
+        for (int rr = 0; rr < dyn; ++rr) {
+            const int2 yt = ytab[D.ytab_off + dy0 + rr];
+            const uint8_t* r0 = S + ((yt.x & 0xFFFF) - sy0) * srow;
+            const uint8_t* r1 = S + ((int)((uint32_t)yt.x >> 16) - sy0) * srow;
+            const int b0 = yt.y & 0xFFFF, b1 = (int)((uint32_t)yt.y >> 16);
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int h0 = r0[x0[k]] * a0[k] + r0[x1[k]] * a1[k];
+                const int h1 = r1[x0[k]] * a0[k] + r1[x1[k]] * a1[k];
                 const int v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
                 packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
             }
+            // columns past the level width land in the row's pitch padding (pitch = align64(w))
+            *reinterpret_cast<uint32_t*>(drow0 + (size_t)rr * D.pitch + dx0) = packed;
         }
-        *reinterpret_cast<uint32_t*>(P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy * D.pitch + dx0) =
-            packed;
     }
 }
 
