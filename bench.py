@@ -227,8 +227,11 @@ def main():
         launches = {"pyramid": NLEVELS - 1}.get(dom, 1)
         t_launch = st[dom] / launches * 1e-3
         achieved = alg[dom] / launches / t_launch / 1e9
-        kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree",
+        kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree<16|8|2>",
                  "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
+        # stages made of several kernels: their per-launch counters add up
+        PARTS = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"],
+                 "quadtree": ["k_quadtree<16>", "k_quadtree<8>", "k_quadtree<2>"]}
         # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
         # same command (tools/collect_pmc.sh -> tools/pmc_summary.py); null when absent
         traffic = None
@@ -237,7 +240,7 @@ def main():
             try:
                 d = json.load(open(pmc))
                 if d.get("batch") == B:
-                    parts = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"]}.get(dom, [kname])
+                    parts = PARTS.get(dom, [kname])
                     traffic = int(sum(d["kernels"][k]["bytes_per_launch"] for k in parts))
             except Exception:
                 traffic = None
@@ -252,7 +255,7 @@ def main():
             try:
                 d = json.load(open(sq))
                 if d.get("batch") == B:
-                    parts = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"]}.get(dom, [kname])
+                    parts = PARTS.get(dom, [kname])
                     per = d["per_dispatch_averages"]
                     ins = sum(per[k]["SQ_INSTS_VALU"] for k in parts)
                     rate = ins / t_launch / 1e9
