@@ -460,8 +460,10 @@ constexpr int QT_NT = 512;
 constexpr int QT_NW = QT_NT / 64;
 constexpr uint16_t kNone = 0xFFFF;
 
+template <int QT_NT>
 __device__ uint32_t block_scan_excl(uint32_t* a, int n, uint32_t* wsum)
 {
+    constexpr int QT_NW = QT_NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int per = (n + QT_NT - 1) / QT_NT;
     const int b = tid * per, e = min(n, b + per);
@@ -496,6 +498,7 @@ __device__ uint32_t block_scan_excl(uint32_t* a, int n, uint32_t* wsum)
     return total;
 }
 
+template <int QT_NT>
 __device__ void block_bitonic_desc(uint32_t* k, int p2)
 {
     for (int size = 2; size <= p2; size <<= 1) {
@@ -563,7 +566,7 @@ size_t quadtree_smem_bytes(const Geometry& g) { return qt_layout(g.lcap, g.max_c
 // shared scalar slots
 enum { SH_N = 0, SH_L, SH_PHASE, SH_M, SH_DONE, SH_KK, SH_ERR, SH_S, SH_C, SH_NEWL };
 
-template <int QT_KPT>
+template <int QT_NT, int QT_KPT>
 __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* __restrict__ G,
                                                    const Cell* __restrict__ cells,
                                                    const uint32_t* __restrict__ slots,
@@ -602,7 +605,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
     const int ncl = LG.ncells, cb = LG.cell_begin;
     for (int c = tid; c < ncl; c += QT_NT) scan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
     __syncthreads();
-    const int n = (int)block_scan_excl(scan, ncl, wsum);
+    const int n = (int)block_scan_excl<QT_NT>(scan, ncl, wsum);
     const uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
     uint32_t* fspill = spill + (size_t)f * G->spill_per_frame + (LG.slot_begin > 0 ? 0 : 0);
     uint32_t* fspill_node = spill_node + (size_t)f * G->spill_per_frame;
@@ -610,7 +613,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
     {
         int off = 0;
         for (int q = 0; q < l; ++q) {
-            const int extra = G->lv[q].slot_cap - QT_NT * qt_kpt(q);
+            const int extra = G->lv[q].slot_cap - qt_regcap(q);
             off += extra > 0 ? extra : 0;
         }
         fspill += off;
@@ -705,7 +708,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
             // split set = nodes with more than one key, ranked in list order
             for (int p = tid; p < L; p += QT_NT) scan[p] = cntc[p] > 1 ? 1u : 0u;
             __syncthreads();
-            S = (int)block_scan_excl(scan, L, wsum);
+            S = (int)block_scan_excl<QT_NT>(scan, L, wsum);
             for (int p = tid; p < L; p += QT_NT) {
                 if (cntc[p] > 1) {
                     const int s = (int)scan[p];
@@ -724,7 +727,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
                 skey[k] = k < m ? ((cntc[vprev[k]] << 16) | (uint32_t)k) : 0u;
             for (int p = tid; p < L; p += QT_NT) srank[p] = kNone;
             __syncthreads();
-            block_bitonic_desc(skey, p2);
+            block_bitonic_desc<QT_NT>(skey, p2);
             for (int j = tid; j < m; j += QT_NT) {
                 const int p = vprev[skey[j] & 0xFFFF];
                 srank[p] = (uint16_t)j;
@@ -763,7 +766,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
             }
             if (tid == 0) sh[SH_KK] = S;
             __syncthreads();
-            block_scan_excl(scan, S, wsum);
+            block_scan_excl<QT_NT>(scan, S, wsum);
             for (int j = tid; j < S; j += QT_NT) {
                 int cs = 0;
                 for (int q = 0; q < 4; ++q) cs += ccnt[4 * j + q] > 0;
@@ -775,7 +778,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
             // non-split rank of every current node
             for (int p = tid; p < L; p += QT_NT) scan[p] = (srank[p] != kNone && srank[p] < kk) ? 1u : 0u;
             __syncthreads();
-            block_scan_excl(scan, L, wsum);
+            block_scan_excl<QT_NT>(scan, L, wsum);
             for (int p = tid; p < L; p += QT_NT) npos[p] = (uint16_t)(p - (int)scan[p]);
             __syncthreads();
         }
@@ -787,7 +790,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
             scan[s] = (uint32_t)cs;
         }
         __syncthreads();
-        const int Ctot = (int)block_scan_excl(scan, kk, wsum);
+        const int Ctot = (int)block_scan_excl<QT_NT>(scan, kk, wsum);
         const int newL = Ctot + (L - kk);
         if (newL > lcap) {
             if (tid == 0) {
@@ -835,7 +838,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
         // new expandable children in creation order (split rank, then n1..n4)
         for (int e = tid; e < 4 * kk; e += QT_NT) scan[e] = ccnt[e] > 1 ? 1u : 0u;
         __syncthreads();
-        const int nexp = (int)block_scan_excl(scan, 4 * kk, wsum);
+        const int nexp = (int)block_scan_excl<QT_NT>(scan, 4 * kk, wsum);
         for (int e = tid; e < 4 * kk; e += QT_NT)
             if (ccnt[e] > 1) vnew[scan[e]] = cpos[e];
         // relabel keypoints with their new list position
@@ -903,16 +906,17 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
     const size_t smem = quadtree_smem_bytes(g);
     // register capacity per level (qt_kpt): level 0 holds most candidates; levels >= 2 hold a
     // few hundred, and their small register file lets describe / FAST waves share the CU
-    hipFuncSetAttribute((const void*)k_quadtree<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipFuncSetAttribute((const void*)k_quadtree<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipFuncSetAttribute((const void*)k_quadtree<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(k_quadtree<16>, dim3(1, batch), dim3(QT_NT), smem, s, 0, b.geom, b.cells, b.slots,
+    hipFuncSetAttribute((const void*)k_quadtree<512, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipFuncSetAttribute((const void*)k_quadtree<512, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipFuncSetAttribute((const void*)k_quadtree<256, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    static_assert(512 * 16 == 8192 && 512 * 8 == 4096 && 256 * 4 == 1024, "qt_regcap");
+    hipLaunchKernelGGL((k_quadtree<512, 16>), dim3(1, batch), dim3(512), smem, s, 0, b.geom, b.cells, b.slots,
                        b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
     if (g.nlevels > 1)
-        hipLaunchKernelGGL(k_quadtree<8>, dim3(1, batch), dim3(QT_NT), smem, s, 1, b.geom, b.cells, b.slots,
+        hipLaunchKernelGGL((k_quadtree<512, 8>), dim3(1, batch), dim3(512), smem, s, 1, b.geom, b.cells, b.slots,
                            b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
     if (g.nlevels > 2)
-        hipLaunchKernelGGL(k_quadtree<2>, dim3(g.nlevels - 2, batch), dim3(QT_NT), smem, s, 2, b.geom, b.cells,
+        hipLaunchKernelGGL((k_quadtree<256, 4>), dim3(g.nlevels - 2, batch), dim3(256), smem, s, 2, b.geom, b.cells,
                            b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
 }
 

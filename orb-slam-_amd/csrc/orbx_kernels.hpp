@@ -50,8 +50,11 @@ enum : int {
 };
 
 size_t quadtree_smem_bytes(const Geometry& g);
-// quadtree keypoints held in registers per thread (512 threads) at level l; the rest spill to global
-__host__ __device__ inline int qt_kpt(int l) { return l == 0 ? 16 : (l == 1 ? 8 : 2); }
+// quadtree workgroup size and keypoints held in registers per thread at level l (the rest spill
+// to global): level 0 holds most candidates, levels >= 2 a few hundred
+__host__ __device__ inline int qt_nt(int l) { return l >= 2 ? 256 : 512; }
+__host__ __device__ inline int qt_kpt(int l) { return l == 0 ? 16 : (l == 1 ? 8 : 4); }
+__host__ __device__ inline int qt_regcap(int l) { return qt_nt(l) * qt_kpt(l); }
 
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
