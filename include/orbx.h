@@ -139,6 +139,22 @@ orbx_status orbm_allpairs_device(const uint8_t* d_q, int nq, const uint8_t* d_t,
                                  int* d_best_idx, int* d_best, int* d_second, uint16_t* d_full,
                                  void* stream);
 
+/* The inner loop every ORBmatcher search shares (SURVEY.md 8b orbm_best2_csr): query q's
+ * candidates are d_cand_idx[d_cand_ptr[q] .. d_cand_ptr[q+1]) in the caller's visiting order (a
+ * GetFeaturesInArea window, a FeatureVector node, ...).  tie_mode ORBM_TIE_FIRST keeps the first
+ * candidate at the minimum distance (strict <, e.g. src/ORBmatcher.cc:214-224, 489-505);
+ * ORBM_TIE_LAST the last one (dist > bestDist skip, SearchForTriangulation :806-823).  Outputs per
+ * query: the best target index (-1 when the list is empty), its distance and the multiset second
+ * distance (256 = none, the reference's initial value).  Candidate indices must lie in [0, nt).
+ * Asynchronous on `stream`. */
+enum { ORBM_TIE_FIRST = 0, ORBM_TIE_LAST = 1 };
+orbx_status orbm_best2_csr_device(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, const int* d_cand_ptr,
+                                  const int* d_cand_idx, int tie_mode, int* d_best_idx, int* d_best, int* d_second,
+                                  void* stream);
+/* Host arrays, on HIP device `device`; checks every candidate index.  Synchronous. */
+orbx_status orbm_best2_csr(int device, const uint8_t* q, int nq, const uint8_t* t, int nt, const int* cand_ptr,
+                           const int* cand_idx, int tie_mode, int* best_idx, int* best, int* second);
+
 /* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:417-588) for `npairs`
  * frame pairs (F1 = pair_a[p], F2 = pair_b[p]) of an `nframes` device batch produced by
  * orbx_extract_batch_device (kps/desc/counts, per-frame capacity `cap`).  Grid

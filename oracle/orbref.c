@@ -1738,3 +1738,27 @@ void orbref_depth_convert(const void* src, int depth_type, int rows, int cols, s
             ((float*)((uint8_t*)dst + (size_t)y * dst_step))[x] = v * factor + 0.0f;   /* cvtScale_, WT = float */
         }
 }
+
+/* ---- SURVEY.md 8b orbm_best2_csr: the shared best / second loop over a candidate list ---- */
+void orbref_best2_csr(const uint8_t* q, int nq, const uint8_t* t, const int* cand_ptr, const int* cand_idx,
+                      int tie_last, int* best_idx, int* best, int* second)
+{
+    for (int i = 0; i < nq; i++) {
+        int bestDist = 256, bestDist2 = 256, bestIdx = -1;
+        for (int c = cand_ptr[i]; c < cand_ptr[i + 1]; c++) {
+            const int j = cand_idx[c];
+            const int dist = orbref_descriptor_distance(q + 32 * (size_t)i, t + 32 * (size_t)j);
+            if (dist < bestDist) {                      /* e.g. src/ORBmatcher.cc:214-224 */
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestIdx = j;
+            } else {
+                if (tie_last && dist == bestDist) bestIdx = j;   /* :806-823 keeps the last <= */
+                if (dist < bestDist2) bestDist2 = dist;
+            }
+        }
+        best_idx[i] = bestIdx;
+        best[i] = bestDist;
+        second[i] = bestDist2;
+    }
+}

@@ -270,6 +270,13 @@ void orbref_ingest(const uint8_t* src, int rows, int cols, int channels, int rgb
 void orbref_depth_convert(const void* src, int depth_type, int rows, int cols, size_t src_step, float factor,
                           float* dst, size_t dst_step);
 
+/* The shared inner loop of the ORBmatcher searches over a CSR candidate list (SURVEY.md 8b
+ * orbm_best2_csr): tie_last 0 keeps the first candidate at the minimum (strict <), 1 the last
+ * (SearchForTriangulation's dist > bestDist skip, src/ORBmatcher.cc:806-823); second = the
+ * multiset second distance; 256 / -1 for an empty list. */
+void orbref_best2_csr(const uint8_t* q, int nq, const uint8_t* t, const int* cand_ptr, const int* cand_idx,
+                      int tie_last, int* best_idx, int* best, int* second);
+
 /* Config-5 brute force: per query best index (first min), best and second distance. */
 void orbref_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt,
                           int* best_idx, int* best_d, int* second_d);

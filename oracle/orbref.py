@@ -123,6 +123,8 @@ def lib():
         L.orbref_depth_convert.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_float, f32p,
                                            C.c_size_t]
         L.orbref_depth_convert.restype = None
+        L.orbref_best2_csr.argtypes = [u8p, C.c_int, u8p, i32p, i32p, C.c_int, i32p, i32p, i32p]
+        L.orbref_best2_csr.restype = None
         L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
         _lib = L
     return _lib
@@ -446,6 +448,17 @@ def depth_convert(src, factor):
     out = np.zeros((rows, cols), np.float32)
     lib().orbref_depth_convert(src.ctypes.data, dt, rows, cols, src.strides[0], factor, _f32(out), cols * 4)
     return out
+
+
+def best2_csr(q, t, ptr, idx, tie_last=False):
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t if len(t) else np.zeros((1, 32), np.uint8), np.uint8)
+    ptr = np.ascontiguousarray(ptr, np.int32)
+    idx = np.ascontiguousarray(idx if len(idx) else np.zeros(1, np.int32), np.int32)
+    nq = len(q)
+    bi, b1, b2 = (np.zeros(max(nq, 1), np.int32) for _ in range(3))
+    lib().orbref_best2_csr(_u8(q), nq, _u8(t), _i32(ptr), _i32(idx), int(bool(tie_last)), _i32(bi), _i32(b1), _i32(b2))
+    return bi[:nq].copy(), b1[:nq].copy(), b2[:nq].copy()
 
 
 def allpairs_top2(q: np.ndarray, t: np.ndarray):

@@ -1006,6 +1006,56 @@ orbx_status orbx_depth_batch_device(const void* d_src, int depth_type, int batch
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
+orbx_status orbm_best2_csr_device(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, const int* d_cand_ptr,
+                                  const int* d_cand_idx, int tie_mode, int* d_best_idx, int* d_best, int* d_second,
+                                  void* stream)
+{
+    if (nq < 0 || nt < 0 || (tie_mode != ORBM_TIE_FIRST && tie_mode != ORBM_TIE_LAST)) return ORBX_EINVAL;
+    if (nq == 0) return ORBX_OK;
+    if (!d_q || !d_cand_ptr || !d_best_idx || !d_best || !d_second || (nt > 0 && (!d_t || !d_cand_idx)))
+        return ORBX_EINVAL;
+    launch_best2_csr(d_q, nq, d_t, d_cand_ptr, d_cand_idx, tie_mode == ORBM_TIE_LAST, d_best_idx, d_best, d_second,
+                     (hipStream_t)stream);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+orbx_status orbm_best2_csr(int device, const uint8_t* q, int nq, const uint8_t* t, int nt, const int* cand_ptr,
+                           const int* cand_idx, int tie_mode, int* best_idx, int* best, int* second)
+{
+    if (nq < 0 || nt < 0 || (tie_mode != ORBM_TIE_FIRST && tie_mode != ORBM_TIE_LAST)) return ORBX_EINVAL;
+    if (nq == 0) return ORBX_OK;
+    if (!q || !cand_ptr || !best_idx || !best || !second) return ORBX_EINVAL;
+    const int ncand = cand_ptr[nq];
+    if (cand_ptr[0] != 0 || ncand < 0 || (ncand > 0 && (!cand_idx || !t))) return ORBX_EINVAL;
+    for (int i = 0; i < nq; ++i)
+        if (cand_ptr[i + 1] < cand_ptr[i]) return ORBX_EINVAL;
+    for (int c = 0; c < ncand; ++c)
+        if (cand_idx[c] < 0 || cand_idx[c] >= nt) return ORBX_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
+    hipSetDevice(device);
+    BowStage st;
+    const size_t oq = st.add(q, (size_t)32 * nq);
+    const size_t ot = st.add(t, (size_t)32 * nt);
+    const size_t op = st.add(cand_ptr, sizeof(int) * ((size_t)nq + 1));
+    const size_t oi = st.add(cand_idx, sizeof(int) * (size_t)ncand);
+    const size_t oo = st.add(nullptr, sizeof(int) * 3 * (size_t)nq);
+    uint8_t* d = nullptr;
+    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
+    orbx_status rc = ORBX_OK;
+    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
+    int* o = (int*)(d + oo);
+    if (rc == ORBX_OK)
+        rc = orbm_best2_csr_device(d + oq, nq, d + ot, nt, (const int*)(d + op), (const int*)(d + oi), tie_mode, o,
+                                   o + nq, o + 2 * nq, nullptr);
+    if (rc == ORBX_OK && (hipMemcpy(best_idx, o, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
+                          hipMemcpy(best, o + nq, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
+                          hipMemcpy(second, o + 2 * nq, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = ORBX_EDEVICE;
+    hipFree(d);
+    return rc;
+}
+
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b)
 {
     int d = 0;

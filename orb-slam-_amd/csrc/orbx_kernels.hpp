@@ -64,6 +64,8 @@ void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p
 
 void launch_allpairs_top2(const uint8_t* q, int nq, const uint8_t* t, int nt, int* bi, int* b1, int* b2,
                           int* part, int nsplit, hipStream_t s);
+void launch_best2_csr(const uint8_t* q, int nq, const uint8_t* t, const int* ptr, const int* idx, int tie_last,
+                      int* bi, int* b1, int* b2, hipStream_t s);
 void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, uint16_t* out, hipStream_t s);
 size_t search_init_scratch_bytes(int nframes, int npairs, int cap);
 void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int nframes, int cap,

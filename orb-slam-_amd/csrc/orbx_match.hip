@@ -148,6 +148,46 @@ __global__ __launch_bounds__(256) void k_allpairs_full(const ulonglong2* __restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// orbm_best2_csr: one lane per query walks its candidate list in order (the reference's
+// sequential loop); lists are a few to a few hundred entries.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_best2_csr(const uint4* __restrict__ q, int nq, const uint4* __restrict__ t,
+                                                   const int* __restrict__ ptr, const int* __restrict__ idx,
+                                                   int tie_last, int* __restrict__ bi, int* __restrict__ b1,
+                                                   int* __restrict__ b2)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= nq) return;
+    const uint4 q0 = q[2 * i], q1 = q[2 * i + 1];
+    int best = 256, second = 256, bidx = -1;
+    const int e = ptr[i + 1];
+    for (int c = ptr[i]; c < e; ++c) {
+        const int j = idx[c];
+        const uint4 t0 = t[2 * j], t1 = t[2 * j + 1];
+        const int d = __popc(q0.x ^ t0.x) + __popc(q0.y ^ t0.y) + __popc(q0.z ^ t0.z) + __popc(q0.w ^ t0.w) +
+                      __popc(q1.x ^ t1.x) + __popc(q1.y ^ t1.y) + __popc(q1.z ^ t1.z) + __popc(q1.w ^ t1.w);
+        if (d < best) {
+            second = best;
+            best = d;
+            bidx = j;
+        } else {
+            if (tie_last && d == best) bidx = j;   // the candidate replaces the best, the second is unchanged
+            if (d < second) second = d;
+        }
+    }
+    bi[i] = bidx;
+    b1[i] = best;
+    b2[i] = second;
+}
+
+void launch_best2_csr(const uint8_t* q, int nq, const uint8_t* t, const int* ptr, const int* idx, int tie_last,
+                      int* bi, int* b1, int* b2, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_best2_csr, dim3((nq + 255) / 256), dim3(256), 0, s, (const uint4*)q, nq, (const uint4*)t, ptr,
+                       idx, tie_last, bi, b1, b2);
+}
+
 void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, uint16_t* out, hipStream_t s)
 {
     dim3 grid((nt + 1023) / 1024, (nq + 63) / 64);

@@ -38,6 +38,7 @@ EXPORTED = [
     "orbm_bow_search_device", "orbm_bow_search",
     "orbm_search_by_projection_device", "orbm_search_by_projection",
     "orbm_project_search_device", "orbm_project_search", "orbx_ingest_batch_device", "orbx_depth_batch_device",
+    "orbm_best2_csr_device", "orbm_best2_csr",
     "orbv_load_text", "orbv_create", "orbv_destroy", "orbv_info", "orbv_transform", "orbv_transform_batch_device",
 ]
 BOW_KF_F, BOW_KF_KF, TRIANGULATION = 0, 1, 2
@@ -178,6 +179,8 @@ def _load():
                                            vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_size_t, C.c_size_t, vp]
     L.orbx_depth_batch_device.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_size_t, C.c_float,
                                           vp, C.c_size_t, C.c_size_t, vp]
+    L.orbm_best2_csr_device.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, vp, vp, vp, vp]
+    L.orbm_best2_csr.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, i32p, i32p, C.c_int, i32p, i32p, i32p]
     L.orbm_bow_search_device.argtypes = [C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, C.c_int, vp, C.c_int,
                                          vp, vp]
     L.orbm_bow_search.argtypes = [C.c_int, C.c_int, P(BowView), P(BowView), P(TriangParams), C.c_float, C.c_int,
@@ -407,6 +410,25 @@ def depth_batch_device(src, factor, out=None, stream=None):
                                        src.stride(0) * esz, factor, _ptr(out), out.stride(1) * 4, out.stride(0) * 4,
                                        _stream(stream)))
     return out
+
+
+TIE_FIRST, TIE_LAST = 0, 1
+
+
+def best2_csr(q, t, cand_ptr, cand_idx, tie_mode=TIE_FIRST, device=0):
+    """orbm_best2_csr on host arrays: per query (best target index, best distance, second distance)
+    over its candidate list, in the list's order."""
+    q = np.ascontiguousarray(q, np.uint8)
+    nt = len(t)
+    t = np.ascontiguousarray(t if nt else np.zeros((1, 32), np.uint8), np.uint8)
+    ptr = np.ascontiguousarray(cand_ptr, np.int32)
+    idx = np.ascontiguousarray(cand_idx if len(cand_idx) else np.zeros(1, np.int32), np.int32)
+    nq = len(q)
+    out = [np.zeros(max(nq, 1), np.int32) for _ in range(3)]
+    i32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+    _check("orbm_best2_csr", lib.orbm_best2_csr(device, _u8(q), nq, _u8(t), nt, i32(ptr), i32(idx), tie_mode,
+                                                i32(out[0]), i32(out[1]), i32(out[2])))
+    return tuple(o[:nq].copy() for o in out)
 
 
 def keypoints_from_device(kps_i32, counts):
