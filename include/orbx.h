@@ -155,6 +155,26 @@ orbx_status orbm_best2_csr_device(const uint8_t* d_q, int nq, const uint8_t* d_t
 orbx_status orbm_best2_csr(int device, const uint8_t* q, int nq, const uint8_t* t, int nt, const int* cand_ptr,
                            const int* cand_idx, int tie_mode, int* best_idx, int* best, int* second);
 
+/* The coarse stage of Frame::ComputeStereoMatches alone (SURVEY.md 8b orbm_stereo_band,
+ * src/Frame.cc:645-757), for callers that keep their own SAD refinement.  Per left keypoint: the right
+ * keypoints whose row band [floor(y - 2*scale[o]), ceil(y + 2*scale[o])] holds the left row (int)y,
+ * with octave within the left octave +- 1 and x in [xL - max_d, xL - min_d]; the first minimum of the
+ * Hamming distance in increasing right index.  Outputs best_idx (-1 when no candidate is below
+ * TH_HIGH = 100) and best_dist (100 then); the caller applies thOrbDist (:762).  Left keypoints with
+ * y < 0, (int)y >= rows or xL - min_d < 0 get -1 / 100.  scale = the extractor's scale factors
+ * (nlevels <= 32); right octaves must lie in [0, nlevels).  n_l, n_r <= 65535, and the row buckets
+ * (4 * rows + 11 * cap bytes) must fit one workgroup's LDS (ORBX_ENOSPC otherwise). */
+orbx_status orbm_stereo_band(int device, const orbx_keypoint* kps_l, const uint8_t* desc_l, int n_l,
+                             const orbx_keypoint* kps_r, const uint8_t* desc_r, int n_r, int rows, const float* scale,
+                             int nlevels, float min_d, float max_d, int* best_idx, int* best_dist);
+/* Batched: pairs (d_left[p], d_right[p]) of a device batch (kps / desc / counts / cap as
+ * orbx_extract_batch_device writes them); outputs d_best_idx[p*cap + i], d_best_dist[p*cap + i].
+ * `scale` is a host array.  Asynchronous on `stream`. */
+orbx_status orbm_stereo_band_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const int* d_counts, int cap,
+                                    const int* d_left, const int* d_right, int npairs, int rows, const float* scale,
+                                    int nlevels, float min_d, float max_d, int* d_best_idx, int* d_best_dist,
+                                    void* stream);
+
 /* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:417-588) for `npairs`
  * frame pairs (F1 = pair_a[p], F2 = pair_b[p]) of an `nframes` device batch produced by
  * orbx_extract_batch_device (kps/desc/counts, per-frame capacity `cap`).  Grid

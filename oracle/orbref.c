@@ -890,6 +890,65 @@ static int cmp_dist_idx(const void* a, const void* b)
     return x[1] < y[1] ? -1 : (x[1] > y[1]);
 }
 
+/* row table :645-673: vRowIndices[yi] lists iR in increasing order.  Rows outside
+ * [0, nRows) are UB in the reference (never reached for kps >= 19 px from the edge);
+ * they are dropped here.  rcnt[y]..rcnt[y+1] index ridx. */
+static void stereo_row_table(const orbref_keypoint* kR, int nR, const float* scale, int nRows, int** rcnt_out,
+                             int** ridx_out)
+{
+    int* rcnt = (int*)calloc((size_t)nRows + 1, sizeof(int));
+    for (int iR = 0; iR < nR; iR++) {
+        const float kpY = kR[iR].y;
+        const float r = 2.0f * scale[kR[iR].octave];
+        const int maxr = (int)ceilf(kpY + r);
+        const int minr = (int)floorf(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) rcnt[yi + 1]++;
+    }
+    for (int y = 0; y < nRows; y++) rcnt[y + 1] += rcnt[y];
+    int* ridx = (int*)malloc(sizeof(int) * ((size_t)rcnt[nRows] + 1));
+    int* rfill = (int*)calloc((size_t)nRows + 1, sizeof(int));
+    for (int iR = 0; iR < nR; iR++) {
+        const float kpY = kR[iR].y;
+        const float r = 2.0f * scale[kR[iR].octave];
+        const int maxr = (int)ceilf(kpY + r);
+        const int minr = (int)floorf(kpY - r);
+        for (int yi = minr; yi <= maxr; yi++)
+            if (yi >= 0 && yi < nRows) ridx[rcnt[yi] + rfill[yi]++] = iR;
+    }
+    free(rfill);
+    *rcnt_out = rcnt;
+    *ridx_out = ridx;
+}
+
+/* the coarse search of one left keypoint, :699-757: returns bestDist (TH_HIGH = 100 when no
+ * candidate beats it, or when the keypoint is skipped) and sets *bestIdxR (first min, increasing iR) */
+static int stereo_coarse(const orbref_keypoint* kpL, const uint8_t* dLi, const orbref_keypoint* kR, const uint8_t* dR,
+                         const int* rcnt, const int* ridx, int nRows, float minD, float maxD, int* bestIdxR)
+{
+    const int levelL = kpL->octave;
+    const float vL = kpL->y, uL = kpL->x;
+    if (vL < 0) return 100;                              /* (size_t) of a negative float: UB, never reached */
+    const size_t row = (size_t)vL;                       /* vRowIndices[vL], :699 */
+    if (row >= (size_t)nRows) return 100;
+    const int c0 = rcnt[row], c1 = rcnt[row + 1];
+    if (c0 == c1) return 100;                            /* :702-703 */
+    const float minU = uL - maxD, maxU = uL - minD;      /* :707-708 */
+    if (maxU < 0) return 100;
+    int bestDist = 100;                                  /* ORBmatcher::TH_HIGH */
+    for (int c = c0; c < c1; c++) {                      /* :723-757 */
+        const int iR = ridx[c];
+        const orbref_keypoint* kpR = &kR[iR];
+        if (kpR->octave < levelL - 1 || kpR->octave > levelL + 1) continue;
+        const float uR = kpR->x;
+        if (uR >= minU && uR <= maxU) {
+            const int dist = orbref_descriptor_distance(dLi, dR + 32 * (size_t)iR);
+            if (dist < bestDist) { bestDist = dist; *bestIdxR = iR; }
+        }
+    }
+    return bestDist;
+}
+
 int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, const uint8_t* pyrL,
                                   const uint8_t* pyrR, const orbref_keypoint* kL, const uint8_t* dL, int nL,
                                   const orbref_keypoint* kR, const uint8_t* dR, int nR, float bf, float fx,
@@ -901,29 +960,8 @@ int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, co
     const int thOrbDist = (100 + TH_LOW) / 2;                                                             /* :638 */
     const int nRows = rows;                                                                               /* :641 */
 
-    /* row table :645-673: vRowIndices[yi] lists iR in increasing order.  Rows outside
-     * [0, nRows) are UB in the reference (never reached for kps >= 19 px from the edge);
-     * they are dropped here. */
-    int* rcnt = (int*)calloc((size_t)nRows + 1, sizeof(int));
-    for (int iR = 0; iR < nR; iR++) {
-        const float kpY = kR[iR].y;
-        const float r = 2.0f * t.scale[kR[iR].octave];
-        const int maxr = (int)ceilf(kpY + r);
-        const int minr = (int)floorf(kpY - r);
-        for (int yi = minr; yi <= maxr; yi++)
-            if (yi >= 0 && yi < nRows) rcnt[yi + 1]++;
-    }
-    for (int y = 0; y < nRows; y++) rcnt[y + 1] += rcnt[y];
-    int* ridx = (int*)malloc(sizeof(int) * ((size_t)rcnt[nRows] + 1));
-    int* rfill = (int*)calloc((size_t)nRows + 1, sizeof(int));
-    for (int iR = 0; iR < nR; iR++) {
-        const float kpY = kR[iR].y;
-        const float r = 2.0f * t.scale[kR[iR].octave];
-        const int maxr = (int)ceilf(kpY + r);
-        const int minr = (int)floorf(kpY - r);
-        for (int yi = minr; yi <= maxr; yi++)
-            if (yi >= 0 && yi < nRows) ridx[rcnt[yi] + rfill[yi]++] = iR;
-    }
+    int *rcnt, *ridx;
+    stereo_row_table(kR, nR, t.scale, nRows, &rcnt, &ridx);
 
     /* :676-681.  The reference reads the member mb before Frame's constructor assigns
      * it (src/Frame.cc:108 vs :140); the intended value mb = mbf/fx is used. */
@@ -937,25 +975,9 @@ int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, co
     for (int iL = 0; iL < nL; iL++) {
         const orbref_keypoint* kpL = &kL[iL];
         const int levelL = kpL->octave;
-        const float vL = kpL->y, uL = kpL->x;
-        const size_t row = (size_t)vL;                       /* vRowIndices[vL], :699 */
-        if (row >= (size_t)nRows) continue;
-        const int c0 = rcnt[row], c1 = rcnt[row + 1];
-        if (c0 == c1) continue;                              /* :702-703 */
-        const float minU = uL - maxD, maxU = uL - minD;      /* :707-708 */
-        if (maxU < 0) continue;
-        int bestDist = 100;                                  /* ORBmatcher::TH_HIGH */
+        const float uL = kpL->x;
         int bestIdxR = 0;
-        for (int c = c0; c < c1; c++) {                      /* :723-757 */
-            const int iR = ridx[c];
-            const orbref_keypoint* kpR = &kR[iR];
-            if (kpR->octave < levelL - 1 || kpR->octave > levelL + 1) continue;
-            const float uR = kpR->x;
-            if (uR >= minU && uR <= maxU) {
-                const int dist = orbref_descriptor_distance(dL + 32 * (size_t)iL, dR + 32 * (size_t)iR);
-                if (dist < bestDist) { bestDist = dist; bestIdxR = iR; }
-            }
-        }
+        const int bestDist = stereo_coarse(kpL, dL + 32 * (size_t)iL, kR, dR, rcnt, ridx, nRows, minD, maxD, &bestIdxR);
         if (bestDist >= thOrbDist) continue;                 /* :762 */
 
         /* sub-pixel match by correlation, :764-853 */
@@ -1029,8 +1051,25 @@ int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, co
         }
     }
 #undef PADPX
-    free(rcnt); free(ridx); free(rfill); free(vDistIdx);
+    free(rcnt); free(ridx); free(vDistIdx);
     return good;
+}
+
+int orbref_stereo_band(const orbref_keypoint* kL, const uint8_t* dL, int nL, const orbref_keypoint* kR,
+                       const uint8_t* dR, int nR, int rows, const float* scale, float minD, float maxD,
+                       int* best_idx, int* best_dist)
+{
+    int *rcnt, *ridx;
+    stereo_row_table(kR, nR, scale, rows, &rcnt, &ridx);
+    for (int iL = 0; iL < nL; iL++) {
+        int bestIdxR = 0;
+        const int bestDist = stereo_coarse(&kL[iL], dL + 32 * (size_t)iL, kR, dR, rcnt, ridx, rows, minD, maxD,
+                                           &bestIdxR);
+        best_dist[iL] = bestDist;
+        best_idx[iL] = bestDist < 100 ? bestIdxR : -1;
+    }
+    free(rcnt); free(ridx);
+    return 0;
 }
 
 /* ---- a12 / a13: vocabulary-node candidate searches, src/ORBmatcher.cc ------

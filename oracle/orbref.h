@@ -142,6 +142,14 @@ int orbref_compute_stereo_matches(const orbref_params* p, int rows, int cols, co
                                   const orbref_keypoint* kR, const uint8_t* dR, int nR, float bf, float fx,
                                   float* uRight, float* depth, int* sad_out);
 
+/* The coarse stage of a15 alone (SURVEY.md 8b orbm_stereo_band, src/Frame.cc:645-757): per
+ * left keypoint the first-min Hamming right keypoint over its row band, octave +- 1 and
+ * x in [xL - maxD, xL - minD].  best_idx -1 / best_dist 100 (TH_HIGH) when nothing beats
+ * TH_HIGH or the keypoint is skipped (:699-708).  scale[octave] of the right keypoints. */
+int orbref_stereo_band(const orbref_keypoint* kL, const uint8_t* dL, int nL, const orbref_keypoint* kR,
+                       const uint8_t* dR, int nR, int rows, const float* scale, float minD, float maxD,
+                       int* best_idx, int* best_dist);
+
 /* DBoW2::FeatureVector as CSR: node ids ascending; the feature indices of node k are
  * idx[ptr[k] .. ptr[k+1]) in insertion order (Thirdparty/DBoW2/DBoW2/FeatureVector.cpp:31-47). */
 typedef struct {

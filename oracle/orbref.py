@@ -125,6 +125,8 @@ def lib():
         L.orbref_depth_convert.restype = None
         L.orbref_best2_csr.argtypes = [u8p, C.c_int, u8p, i32p, i32p, C.c_int, i32p, i32p, i32p]
         L.orbref_best2_csr.restype = None
+        L.orbref_stereo_band.argtypes = [C.c_void_p, u8p, C.c_int, C.c_void_p, u8p, C.c_int, C.c_int, f32p,
+                                         C.c_float, C.c_float, i32p, i32p]
         L.orbref_allpairs_top2.argtypes = [u8p, C.c_int, u8p, C.c_int, i32p, i32p, i32p]
         _lib = L
     return _lib
@@ -459,6 +461,19 @@ def best2_csr(q, t, ptr, idx, tie_last=False):
     bi, b1, b2 = (np.zeros(max(nq, 1), np.int32) for _ in range(3))
     lib().orbref_best2_csr(_u8(q), nq, _u8(t), _i32(ptr), _i32(idx), int(bool(tie_last)), _i32(bi), _i32(b1), _i32(b2))
     return bi[:nq].copy(), b1[:nq].copy(), b2[:nq].copy()
+
+
+def stereo_band(kl, dl, kr, dr, rows, scale, min_d, max_d):
+    """The coarse stage of ComputeStereoMatches alone: (best_idx, best_dist) per left keypoint."""
+    n, nr = len(kl), len(kr)
+    kl, kr = _kp(kl if n else np.zeros(1, KEYPOINT_DTYPE)), _kp(kr if nr else np.zeros(1, KEYPOINT_DTYPE))
+    dl = np.ascontiguousarray(dl if n else np.zeros((1, 32), np.uint8), np.uint8)
+    dr = np.ascontiguousarray(dr if nr else np.zeros((1, 32), np.uint8), np.uint8)
+    sc = np.ascontiguousarray(scale, np.float32)
+    bi, bd = np.zeros(max(n, 1), np.int32), np.zeros(max(n, 1), np.int32)
+    lib().orbref_stereo_band(kl.ctypes.data, _u8(dl), n, kr.ctypes.data, _u8(dr), nr, rows, _f32(sc), min_d, max_d,
+                             _i32(bi), _i32(bd))
+    return bi[:n].copy(), bd[:n].copy()
 
 
 def allpairs_top2(q: np.ndarray, t: np.ndarray):

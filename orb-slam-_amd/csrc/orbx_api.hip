@@ -1056,6 +1056,74 @@ orbx_status orbm_best2_csr(int device, const uint8_t* q, int nq, const uint8_t* 
     return rc;
 }
 
+orbx_status orbm_stereo_band_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const int* d_counts, int cap,
+                                    const int* d_left, const int* d_right, int npairs, int rows, const float* scale,
+                                    int nlevels, float min_d, float max_d, int* d_best_idx, int* d_best_dist,
+                                    void* stream)
+{
+    if (npairs < 0 || cap < 1 || cap > 65535 || rows < 1 || nlevels < 1 || nlevels > kStMaxLevels || !scale)
+        return ORBX_EINVAL;
+    if (npairs == 0) return ORBX_OK;
+    if (!d_kps || !d_desc || !d_counts || !d_left || !d_right || !d_best_idx || !d_best_dist) return ORBX_EINVAL;
+    if (stereo_band_smem(rows, cap) > 160 * 1024) return ORBX_ENOSPC;
+    StBandArgs a{};
+    float rmax = 0.f;
+    for (int l = 0; l < kStMaxLevels; ++l) {
+        a.scale[l] = scale[std::min(l, nlevels - 1)];
+        if (l < nlevels) rmax = std::max(rmax, 2.0f * scale[l]);
+    }
+    a.nlevels = nlevels;
+    a.rows = rows;
+    a.rband = (int)std::ceil(rmax);
+    a.minD = min_d;
+    a.maxD = max_d;
+    launch_stereo_band(a, d_kps, d_desc, d_counts, cap, d_left, d_right, npairs, d_best_idx, d_best_dist,
+                       (hipStream_t)stream);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+orbx_status orbm_stereo_band(int device, const orbx_keypoint* kps_l, const uint8_t* desc_l, int n_l,
+                             const orbx_keypoint* kps_r, const uint8_t* desc_r, int n_r, int rows, const float* scale,
+                             int nlevels, float min_d, float max_d, int* best_idx, int* best_dist)
+{
+    if (n_l < 0 || n_r < 0 || n_l > 65535 || n_r > 65535 || rows < 1 || nlevels < 1 || nlevels > kStMaxLevels ||
+        !scale)
+        return ORBX_EINVAL;
+    if (n_l == 0) return ORBX_OK;
+    if (!kps_l || !desc_l || !best_idx || !best_dist || (n_r > 0 && (!kps_r || !desc_r))) return ORBX_EINVAL;
+    for (int i = 0; i < n_r; ++i)
+        if (kps_r[i].octave < 0 || kps_r[i].octave >= nlevels) return ORBX_EINVAL;
+    const int cap = std::max(n_l, n_r);
+    if (stereo_band_smem(rows, cap) > 160 * 1024) return ORBX_ENOSPC;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
+    hipSetDevice(device);
+    BowStage st;
+    const size_t ok = st.add(nullptr, sizeof(orbx_keypoint) * 2 * (size_t)cap);
+    std::memcpy(st.host.data() + ok, kps_l, sizeof(orbx_keypoint) * (size_t)n_l);
+    if (n_r) std::memcpy(st.host.data() + ok + sizeof(orbx_keypoint) * (size_t)cap, kps_r, sizeof(orbx_keypoint) * n_r);
+    const size_t od = st.add(nullptr, (size_t)64 * cap);
+    std::memcpy(st.host.data() + od, desc_l, (size_t)32 * n_l);
+    if (n_r) std::memcpy(st.host.data() + od + (size_t)32 * cap, desc_r, (size_t)32 * n_r);
+    const int meta[4] = {n_l, n_r, 0, 1};   // counts[2], left frame, right frame
+    const size_t om = st.add(meta, sizeof(meta));
+    const size_t oo = st.add(nullptr, sizeof(int) * 2 * (size_t)cap);
+    uint8_t* d = nullptr;
+    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
+    orbx_status rc = ORBX_OK;
+    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
+    const int* m = (const int*)(d + om);
+    int* o = (int*)(d + oo);
+    if (rc == ORBX_OK)
+        rc = orbm_stereo_band_device((const orbx_keypoint*)(d + ok), d + od, m, cap, m + 2, m + 3, 1, rows, scale,
+                                     nlevels, min_d, max_d, o, o + cap, nullptr);
+    if (rc == ORBX_OK && (hipMemcpy(best_idx, o, sizeof(int) * (size_t)n_l, hipMemcpyDeviceToHost) != hipSuccess ||
+                          hipMemcpy(best_dist, o + cap, sizeof(int) * (size_t)n_l, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = ORBX_EDEVICE;
+    hipFree(d);
+    return rc;
+}
+
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b)
 {
     int d = 0;

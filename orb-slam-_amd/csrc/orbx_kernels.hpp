@@ -77,6 +77,15 @@ void launch_stereo(const Geometry& g, const Geometry* d_geom, const FramePtrs& P
                    const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int cap, const int* fl,
                    const int* fr, int npairs, float bf, float maxD, int rband, float* uright, float* depth, int* sad,
                    int* ngood, hipStream_t s);
+constexpr int kStMaxLevels = 32;
+struct StBandArgs {
+    float scale[kStMaxLevels];   // per-octave scale factor, padded with the last level's
+    int nlevels, rows, rband;
+    float minD, maxD;
+};
+size_t stereo_band_smem(int rows, int cap);
+void launch_stereo_band(const StBandArgs& a, const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int cap,
+                        const int* fl, const int* fr, int npairs, int* best_idx, int* best_dist, hipStream_t s);
 
 void launch_bow(int mode, const orbm_bow_view* v1, const orbm_bow_view* v2, const orbm_triang_params* tp,
                 int npairs, int max_nodes1, float nnratio, int check_ori, int* match, int* bins, int stride,

@@ -54,30 +54,11 @@ __host__ __device__ inline size_t stereo_lds_bytes(int rows, int cap)
     return (size_t)4 * (rows + 2) + (size_t)cap * (2 + 4 + 4 + 1) + 64;
 }
 
-__global__ __launch_bounds__(kStNT) void k_stereo_match(const Geometry* __restrict__ G, FramePtrs PL, FramePtrs PR,
-                                                        const orbx_keypoint* __restrict__ kps,
-                                                        const uint8_t* __restrict__ desc,
-                                                        const int* __restrict__ counts, int cap,
-                                                        const int* __restrict__ fleft, const int* __restrict__ fright,
-                                                        float bf, float maxD, int rband,
-                                                        float* __restrict__ uright, float* __restrict__ depth,
-                                                        int* __restrict__ sad)
+// right keypoints -> row buckets (vRowIndices, :645-673): keypoints grouped by floor(kpY), clamped
+// to [0, rows); off[b] ends as the end of bucket b (= the start of bucket b + 1)
+__device__ __forceinline__ void st_buckets(StereoLds& S, const orbx_keypoint* __restrict__ KR, int nR, int rows,
+                                           int tid)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_st[];
-    const int p = blockIdx.y, tid = threadIdx.x;
-    const int fl = fleft[p], fr = fright[p];
-    const int nL = min(counts[fl], cap), nR = min(counts[fr], cap);
-    const int rows = G->rows;
-    StereoLds S;
-    S.off = (int*)s_st;
-    S.rx = (float*)(s_st + (((size_t)4 * (rows + 2) + 15) & ~(size_t)15));
-    S.ry = S.rx + cap;
-    S.list = (uint16_t*)(S.ry + cap);
-    S.ro = (int8_t*)(S.list + cap);
-    const orbx_keypoint* KR = kps + (size_t)fr * cap;
-    const orbx_keypoint* KL = kps + (size_t)fl * cap;
-
-    // ---- right keypoints -> row buckets (vRowIndices, :645-673) ----------------
     for (int r = tid; r <= rows; r += kStNT) S.off[r] = 0;
     __syncthreads();
     for (int i = tid; i < nR; i += kStNT) {
@@ -110,8 +91,60 @@ __global__ __launch_bounds__(kStNT) void k_stereo_match(const Geometry* __restri
         S.list[slot] = (uint16_t)i;
     }
     __syncthreads();
-    // off[b] now holds the end of bucket b = the start of bucket b + 1
-    auto bstart = [&](int b) { return b == 0 ? 0 : S.off[b - 1]; };
+}
+
+// the coarse search of one left keypoint (:699-757): right keypoints whose band
+// [floor(kpY - r), ceil(kpY + r)], r = 2 * scale[octave], holds the left row, octave within
+// levelL +- 1, uR in [minU, maxU]; first min of Hamming in increasing iR = min of (dist << 16 | iR).
+// Returns (bestDist << 16 | bestIdxR), 100 << 16 when nothing beats TH_HIGH.
+template <class ScaleOf>
+__device__ __forceinline__ int st_coarse(const StereoLds& S, int rows, int rband, ScaleOf scale_of, int row, int levelL,
+                                         float minU, float maxU, const uint4& a0, const uint4& a1,
+                                         const uint8_t* __restrict__ descR)
+{
+    int bestKey = 100 << 16;   // (bestDist = TH_HIGH, bestIdxR = 0)
+    const int b0 = max(row - rband - 1, 0), b1 = min(row + rband + 1, rows - 1);
+    for (int j = b0 == 0 ? 0 : S.off[b0 - 1]; j < S.off[b1]; ++j) {
+        const int iR = S.list[j];
+        const float kpY = S.ry[iR];
+        const int oR = S.ro[iR];
+        const float r = 2.0f * scale_of(oR);   // :662
+        const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
+        if (row < minr || row > maxr) continue;
+        if (oR < levelL - 1 || oR > levelL + 1) continue;   // :729-730
+        const float uR = S.rx[iR];
+        if (uR >= minU && uR <= maxU) {
+            const uint4* dr = reinterpret_cast<const uint4*>(descR + (size_t)iR * 32);
+            bestKey = min(bestKey, (ham256(a0, a1, dr[0], dr[1]) << 16) | iR);
+        }
+    }
+    return bestKey;
+}
+
+__global__ __launch_bounds__(kStNT) void k_stereo_match(const Geometry* __restrict__ G, FramePtrs PL, FramePtrs PR,
+                                                        const orbx_keypoint* __restrict__ kps,
+                                                        const uint8_t* __restrict__ desc,
+                                                        const int* __restrict__ counts, int cap,
+                                                        const int* __restrict__ fleft, const int* __restrict__ fright,
+                                                        float bf, float maxD, int rband,
+                                                        float* __restrict__ uright, float* __restrict__ depth,
+                                                        int* __restrict__ sad)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_st[];
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int fl = fleft[p], fr = fright[p];
+    const int nL = min(counts[fl], cap), nR = min(counts[fr], cap);
+    const int rows = G->rows;
+    StereoLds S;
+    S.off = (int*)s_st;
+    S.rx = (float*)(s_st + (((size_t)4 * (rows + 2) + 15) & ~(size_t)15));
+    S.ry = S.rx + cap;
+    S.list = (uint16_t*)(S.ry + cap);
+    S.ro = (int8_t*)(S.list + cap);
+    const orbx_keypoint* KR = kps + (size_t)fr * cap;
+    const orbx_keypoint* KL = kps + (size_t)fl * cap;
+
+    st_buckets(S, KR, nR, rows, tid);
 
     const int iL = blockIdx.x * kStNT + tid;
     if (iL >= nL) return;
@@ -127,26 +160,11 @@ __global__ __launch_bounds__(kStNT) void k_stereo_match(const Geometry* __restri
     ok = ok && row < rows;
     const float minU = uL - maxD, maxU = uL - minD;   // :707-708
     ok = ok && !(maxU < 0);
-    int bestKey = 100 << 16;   // (bestDist = TH_HIGH, bestIdxR = 0); first min = smallest iR
+    int bestKey = 100 << 16;
     if (ok) {
         const uint4* dl = reinterpret_cast<const uint4*>(desc + ((size_t)fl * cap + iL) * 32);
-        const uint4 a0 = dl[0], a1 = dl[1];
-        const int b0 = max(row - rband - 1, 0), b1 = min(row + rband + 1, rows - 1);
-        for (int j = bstart(b0); j < S.off[b1]; ++j) {
-            const int iR = S.list[j];
-            const float kpY = S.ry[iR];
-            const float r = 2.0f * G->lv[S.ro[iR]].scale;   // :662
-            const int maxr = (int)ceilf(kpY + r), minr = (int)floorf(kpY - r);
-            if (row < minr || row > maxr) continue;
-            const int oR = S.ro[iR];
-            if (oR < levelL - 1 || oR > levelL + 1) continue;   // :729-730
-            const float uR = S.rx[iR];
-            if (uR >= minU && uR <= maxU) {
-                const uint4* dr = reinterpret_cast<const uint4*>(desc + ((size_t)fr * cap + iR) * 32);
-                const int key = (ham256(a0, a1, dr[0], dr[1]) << 16) | iR;
-                bestKey = min(bestKey, key);
-            }
-        }
+        bestKey = st_coarse(S, rows, rband, [&](int oR) { return G->lv[oR].scale; }, row, levelL, minU, maxU, dl[0],
+                            dl[1], desc + (size_t)fr * cap * 32);
     }
     const int bestDist = bestKey >> 16, bestIdxR = bestKey & 0xFFFF;
     if (ok && bestDist < 75) {   // thOrbDist = (TH_HIGH + TH_LOW) / 2, :762
@@ -311,7 +329,59 @@ __global__ __launch_bounds__(1024) void k_stereo_cut(const int* __restrict__ cou
     if (tid == 0) ngood[p] = s_good;
 }
 
+// S3 k_stereo_band: the coarse stage alone (orbm_stereo_band), for callers that keep their own SAD
+// stage.  Same buckets and search as S1; the scale table comes by value and is staged in LDS.
+__global__ __launch_bounds__(kStNT) void k_stereo_band(StBandArgs A, const orbx_keypoint* __restrict__ kps,
+                                                       const uint8_t* __restrict__ desc,
+                                                       const int* __restrict__ counts, int cap,
+                                                       const int* __restrict__ fleft, const int* __restrict__ fright,
+                                                       int* __restrict__ best_idx, int* __restrict__ best_dist)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_st[];
+    __shared__ float s_scale[kStMaxLevels];
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int fl = fleft[p], fr = fright[p];
+    const int nL = min(counts[fl], cap), nR = min(counts[fr], cap);
+    const int rows = A.rows;
+    if (tid < kStMaxLevels) s_scale[tid] = A.scale[tid];
+    StereoLds S;
+    S.off = (int*)s_st;
+    S.rx = (float*)(s_st + (((size_t)4 * (rows + 2) + 15) & ~(size_t)15));
+    S.ry = S.rx + cap;
+    S.list = (uint16_t*)(S.ry + cap);
+    S.ro = (int8_t*)(S.list + cap);
+    st_buckets(S, kps + (size_t)fr * cap, nR, rows, tid);   // its barriers also cover s_scale
+
+    const int iL = blockIdx.x * kStNT + tid;
+    if (iL >= nL) return;
+    const orbx_keypoint kpL = kps[(size_t)fl * cap + iL];
+    const int row = (int)kpL.y;   // vRowIndices[vL] (:699)
+    const float minU = kpL.x - A.maxD, maxU = kpL.x - A.minD;   // :707-708
+    int bestKey = 100 << 16;
+    if (kpL.y >= 0.0f && row < rows && !(maxU < 0)) {
+        const uint4* dl = reinterpret_cast<const uint4*>(desc + ((size_t)fl * cap + iL) * 32);
+        const int nlv = A.nlevels;
+        bestKey = st_coarse(S, rows, A.rband, [&](int oR) { return s_scale[min(max(oR, 0), nlv - 1)]; }, row,
+                            kpL.octave, minU, maxU, dl[0], dl[1], desc + (size_t)fr * cap * 32);
+    }
+    const size_t o = (size_t)p * cap + iL;
+    const int bd = bestKey >> 16;
+    best_dist[o] = bd;
+    best_idx[o] = bd < 100 ? (bestKey & 0xFFFF) : -1;
+}
+
 size_t stereo_match_smem(const Geometry& g, int cap) { return stereo_lds_bytes(g.rows, cap); }
+
+size_t stereo_band_smem(int rows, int cap) { return stereo_lds_bytes(rows, cap); }
+
+void launch_stereo_band(const StBandArgs& a, const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int cap,
+                        const int* fl, const int* fr, int npairs, int* best_idx, int* best_dist, hipStream_t s)
+{
+    const size_t sm = stereo_lds_bytes(a.rows, cap);
+    hipFuncSetAttribute((const void*)k_stereo_band, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL(k_stereo_band, dim3((cap + kStNT - 1) / kStNT, npairs), dim3(kStNT), sm, s, a, kps, desc,
+                       counts, cap, fl, fr, best_idx, best_dist);
+}
 
 void launch_stereo(const Geometry& g, const Geometry* d_geom, const FramePtrs& PL, const FramePtrs& PR,
                    const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int cap, const int* fl,

@@ -38,7 +38,7 @@ EXPORTED = [
     "orbm_bow_search_device", "orbm_bow_search",
     "orbm_search_by_projection_device", "orbm_search_by_projection",
     "orbm_project_search_device", "orbm_project_search", "orbx_ingest_batch_device", "orbx_depth_batch_device",
-    "orbm_best2_csr_device", "orbm_best2_csr",
+    "orbm_best2_csr_device", "orbm_best2_csr", "orbm_stereo_band", "orbm_stereo_band_device",
     "orbv_load_text", "orbv_create", "orbv_destroy", "orbv_info", "orbv_transform", "orbv_transform_batch_device",
 ]
 BOW_KF_F, BOW_KF_KF, TRIANGULATION = 0, 1, 2
@@ -181,6 +181,10 @@ def _load():
                                           vp, C.c_size_t, C.c_size_t, vp]
     L.orbm_best2_csr_device.argtypes = [vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, vp, vp, vp, vp]
     L.orbm_best2_csr.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, i32p, i32p, C.c_int, i32p, i32p, i32p]
+    L.orbm_stereo_band.argtypes = [C.c_int, vp, u8p, C.c_int, vp, u8p, C.c_int, C.c_int, f32p, C.c_int, C.c_float,
+                                   C.c_float, i32p, i32p]
+    L.orbm_stereo_band_device.argtypes = [vp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, f32p, C.c_int, C.c_float,
+                                          C.c_float, vp, vp, vp]
     L.orbm_bow_search_device.argtypes = [C.c_int, vp, vp, vp, C.c_int, C.c_int, C.c_float, C.c_int, vp, C.c_int,
                                          vp, vp]
     L.orbm_bow_search.argtypes = [C.c_int, C.c_int, P(BowView), P(BowView), P(TriangParams), C.c_float, C.c_int,
@@ -429,6 +433,41 @@ def best2_csr(q, t, cand_ptr, cand_idx, tie_mode=TIE_FIRST, device=0):
     _check("orbm_best2_csr", lib.orbm_best2_csr(device, _u8(q), nq, _u8(t), nt, i32(ptr), i32(idx), tie_mode,
                                                 i32(out[0]), i32(out[1]), i32(out[2])))
     return tuple(o[:nq].copy() for o in out)
+
+
+def stereo_band(kps_l, desc_l, kps_r, desc_r, rows, scale, min_d, max_d, device=0):
+    """orbm_stereo_band on host arrays, the coarse stage of ComputeStereoMatches (src/Frame.cc:645-757):
+    per left keypoint (best right index or -1, best distance or 100)."""
+    kl = np.ascontiguousarray(kps_l, KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kps_r, KEYPOINT_DTYPE)
+    nl, nr = len(kl), len(kr)
+    dl = np.ascontiguousarray(desc_l if nl else np.zeros((1, 32), np.uint8), np.uint8)
+    dr = np.ascontiguousarray(desc_r if nr else np.zeros((1, 32), np.uint8), np.uint8)
+    sc = np.ascontiguousarray(scale, np.float32)
+    bi, bd = np.zeros(max(nl, 1), np.int32), np.zeros(max(nl, 1), np.int32)
+    i32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+    _check("orbm_stereo_band",
+           lib.orbm_stereo_band(device, kl.ctypes.data, _u8(dl), nl, kr.ctypes.data, _u8(dr), nr, rows,
+                                sc.ctypes.data_as(C.POINTER(C.c_float)), len(sc), min_d, max_d, i32(bi), i32(bd)))
+    return bi[:nl].copy(), bd[:nl].copy()
+
+
+def stereo_band_batch_device(kps, desc, counts, left, right, rows, scale, min_d, max_d, stream=None):
+    """orbm_stereo_band_device over pairs (left[p], right[p]) of a device batch (kps int32 (F, cap, 7),
+    desc uint8 (F, cap, 32), counts int32 (F,)).  Returns (best_idx, best_dist), int32 (npairs, cap)."""
+    import torch
+    cap = kps.shape[1]
+    left = torch.as_tensor(left, dtype=torch.int32, device=kps.device).contiguous()
+    right = torch.as_tensor(right, dtype=torch.int32, device=kps.device).contiguous()
+    npairs = left.numel()
+    bi = torch.empty((npairs, cap), dtype=torch.int32, device=kps.device)
+    bd = torch.empty((npairs, cap), dtype=torch.int32, device=kps.device)
+    sc = np.ascontiguousarray(scale, np.float32)
+    _check("orbm_stereo_band_device",
+           lib.orbm_stereo_band_device(_ptr(kps), _ptr(desc), _ptr(counts), cap, _ptr(left), _ptr(right), npairs, rows,
+                                       sc.ctypes.data_as(C.POINTER(C.c_float)), len(sc), min_d, max_d, _ptr(bi),
+                                       _ptr(bd), _stream(stream)))
+    return bi, bd
 
 
 def keypoints_from_device(kps_i32, counts):

@@ -277,3 +277,129 @@ def test_gpu_stereo_edge_cases(orbref, cuda):
     exo(orbx_synth.gen_image(9, 400, 300))
     with pytest.raises(orbx.OrbxError):
         orbx.compute_stereo_matches(exl, exo, kl, dl, kl, dl, EUROC_BF, EUROC_FX)
+
+
+# ------------------------------------------- orbm_stereo_band (the coarse stage alone)
+
+
+def py_band(kL, dL, kR, dR, rows, scale, minD, maxD):
+    """src/Frame.cc:645-757 restated with Python lists: vRowIndices, then the first strict minimum."""
+    S = [F32(s) for s in scale]
+    rowidx = [[] for _ in range(rows)]
+    for iR in range(len(kR)):
+        y, r = F32(kR["y"][iR]), F32(2.0) * S[kR["octave"][iR]]
+        for yi in range(int(np.floor(F32(y - r))), int(np.ceil(F32(y + r))) + 1):
+            if 0 <= yi < rows:
+                rowidx[yi].append(iR)
+    ham = lambda a, b: int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+    bi, bd = np.full(len(kL), -1), np.full(len(kL), 100)
+    for iL in range(len(kL)):
+        vL, uL, lv = F32(kL["y"][iL]), F32(kL["x"][iL]), int(kL["octave"][iL])
+        if vL < 0 or int(vL) >= rows:
+            continue
+        minU, maxU = F32(uL - F32(maxD)), F32(uL - F32(minD))
+        if maxU < 0:
+            continue
+        best, idx = 100, -1
+        for iR in rowidx[int(vL)]:
+            o = int(kR["octave"][iR])
+            if lv - 1 <= o <= lv + 1 and minU <= F32(kR["x"][iR]) <= maxU:
+                d = ham(dL[iL], dR[iR])
+                if d < best:
+                    best, idx = d, iR
+        bi[iL], bd[iL] = idx, best
+    return bi, bd
+
+
+def band_case(seed, nl, nr, rows=240, cols=320, nlevels=8):
+    """Keypoints on and beyond the image rows, descriptors from 6 prototypes (many equal distances)."""
+    from orbref import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    proto = rng.integers(0, 256, (6, 32), dtype=np.uint8)
+
+    def side(n):
+        k = np.zeros(n, KEYPOINT_DTYPE)
+        k["x"] = rng.uniform(-2, cols, n)
+        k["y"] = rng.uniform(-3, rows + 3, n)
+        k["octave"] = rng.integers(0, nlevels, n)
+        bits = np.unpackbits(proto[rng.integers(0, 6, n)], axis=1) ^ (rng.random((n, 256)) < 0.03)
+        return k, np.packbits(bits, axis=1)
+    (kl, dl), (kr, dr) = side(nl), side(nr)
+    m = min(nl, nr) // 8
+    kr["y"][:m] = kl["y"][:m]                        # shared rows
+    dr[m: 2 * m] = dr[:m]                            # duplicate descriptors: ties broken by index
+    return kl, dl, kr, dr, [1.2 ** l for l in range(nlevels)]
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_band_oracle_matches_restatement(orbref, seed):
+    kl, dl, kr, dr, sc = band_case(seed, 400, 500)
+    maxD = EUROC_BF / (EUROC_BF / EUROC_FX)
+    got = orbref.stereo_band(kl, dl, kr, dr, 240, sc, 0.0, maxD)
+    want = py_band(kl, dl, kr, dr, 240, sc, 0.0, maxD)
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    assert (got[0] >= 0).sum() > 100 and (got[0] == -1).sum() > 10
+    # a narrow disparity range prunes candidates
+    narrow = orbref.stereo_band(kl, dl, kr, dr, 240, sc, 5.0, 40.0)
+    assert np.array_equal(narrow[1], py_band(kl, dl, kr, dr, 240, sc, 5.0, 40.0)[1])
+    assert (narrow[0] >= 0).sum() < (got[0] >= 0).sum()
+
+
+def test_band_agrees_with_full_stereo(orbref):
+    """Every pair the full ComputeStereoMatches keeps went through a coarse best below thOrbDist."""
+    L, R = _pair(3, 320, 240)
+    p = orbref.make_params(300, 1.2, 8, 20, 7)
+    a, b = orbref.extract(L, p), orbref.extract(R, p)
+    t = orbref.tables(p)
+    sc = [t.scale[l] for l in range(8)]
+    mb = np.float32(np.float32(EUROC_BF) / np.float32(EUROC_FX))
+    maxD = float(np.float32(np.float32(EUROC_BF) / mb))
+    bi, bd = orbref.stereo_band(a.keypoints, a.descriptors, b.keypoints, b.descriptors, 240, sc, 0.0, maxD)
+    ur, _, _, good = orbref.compute_stereo_matches(p, a, b, 240, 320, EUROC_BF, EUROC_FX)
+    assert good > 20 and np.all(bd[ur >= 0] < 75) and np.all(bi[ur >= 0] >= 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [2, 3])
+def test_gpu_stereo_band(orbref, cuda, seed):
+    import orbx
+    kl, dl, kr, dr, sc = band_case(seed, 3000, 2500, rows=480, cols=752)
+    for lo, hi in ((0.0, 110.0), (3.0, 30.0)):
+        got = orbx.stereo_band(kl, dl, kr, dr, 480, sc, lo, hi)
+        want = orbref.stereo_band(kl, dl, kr, dr, 480, sc, lo, hi)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    # empty sides
+    bi, bd = orbx.stereo_band(kl, dl, kr[:0], dr[:0], 480, sc, 0.0, 110.0)
+    assert np.all(bi == -1) and np.all(bd == 100)
+    assert len(orbx.stereo_band(kl[:0], dl[:0], kr, dr, 480, sc, 0.0, 110.0)[0]) == 0
+    bad = kr.copy()
+    bad["octave"][0] = 8
+    with pytest.raises(orbx.OrbxError):
+        orbx.stereo_band(kl, dl, bad, dr, 480, sc, 0.0, 110.0)
+
+
+@pytest.mark.gpu
+def test_gpu_stereo_band_batch(orbref, cuda):
+    import torch
+    import orbx
+    W, H, nfeat = 752, 480, 1000
+    pairs = [_pair(s, W, H) for s in (3, 4)]
+    frames = np.stack([im for pr in pairs for im in pr])
+    ex = orbx.ORBextractor(nfeat, 1.2, 8, 20, 7)
+    cap = ex.capacity(H, W)
+    kps = torch.empty((4, cap, 7), dtype=torch.int32, device=cuda)
+    desc = torch.empty((4, cap, 32), dtype=torch.uint8, device=cuda)
+    counts = torch.empty((4,), dtype=torch.int32, device=cuda)
+    ex.extract_batch_device(torch.from_numpy(frames).to(cuda), kps, desc, counts)
+    p = orbref.make_params(nfeat, 1.2, 8, 20, 7)
+    t = orbref.tables(p)
+    sc = [t.scale[l] for l in range(8)]
+    bi, bd = orbx.stereo_band_batch_device(kps, desc, counts, [0, 2], [1, 3], H, sc, 0.0, 110.0)
+    torch.cuda.synchronize()
+    c = counts.cpu().numpy()
+    for k, (L, R) in enumerate(pairs):
+        a, b = orbref.extract(L, p), orbref.extract(R, p)
+        wi, wd = orbref.stereo_band(a.keypoints, a.descriptors, b.keypoints, b.descriptors, H, sc, 0.0, 110.0)
+        n = c[2 * k]
+        assert n == len(a.keypoints)
+        assert np.array_equal(bi[k, :n].cpu().numpy(), wi) and np.array_equal(bd[k, :n].cpu().numpy(), wd)
