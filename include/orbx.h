@@ -138,6 +138,10 @@ enum { ORBM_TOP2 = 0, ORBM_FULL_U16 = 1 };
 orbx_status orbm_allpairs_device(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int mode,
                                  int* d_best_idx, int* d_best, int* d_second, uint16_t* d_full,
                                  void* stream);
+/* The same on host arrays (SURVEY.md 8b orbm_allpairs), on HIP device `device`; synchronous.
+ * nt == 0: TOP2 gives -1 / 256 / 256 per query. */
+orbx_status orbm_allpairs(int device, const uint8_t* q, int nq, const uint8_t* t, int nt, int mode, int* best_idx,
+                          int* best, int* second, uint16_t* full);
 
 /* The inner loop every ORBmatcher search shares (SURVEY.md 8b orbm_best2_csr): query q's
  * candidates are d_cand_idx[d_cand_ptr[q] .. d_cand_ptr[q+1]) in the caller's visiting order (a

@@ -1159,6 +1159,49 @@ orbx_status orbm_allpairs_device(const uint8_t* d_q, int nq, const uint8_t* d_t,
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
+orbx_status orbm_allpairs(int device, const uint8_t* q, int nq, const uint8_t* t, int nt, int mode, int* best_idx,
+                          int* best, int* second, uint16_t* full)
+{
+    if (nq < 0 || nt < 0 || (mode != ORBM_TOP2 && mode != ORBM_FULL_U16)) return ORBX_EINVAL;
+    if (nq == 0) return ORBX_OK;
+    if (!q || (nt > 0 && !t)) return ORBX_EINVAL;
+    if (mode == ORBM_TOP2 && (!best_idx || !best || !second)) return ORBX_EINVAL;
+    if (mode == ORBM_FULL_U16 && !full) return ORBX_EINVAL;
+    if (nt == 0) {
+        if (mode == ORBM_TOP2)
+            for (int i = 0; i < nq; ++i) {
+                best_idx[i] = -1;
+                best[i] = second[i] = 256;
+            }
+        return ORBX_OK;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
+    hipSetDevice(device);
+    BowStage st;
+    const size_t oq = st.add(q, (size_t)32 * nq);
+    const size_t ot = st.add(t, (size_t)32 * nt);
+    const size_t out_bytes = mode == ORBM_TOP2 ? sizeof(int) * 3 * (size_t)nq : sizeof(uint16_t) * (size_t)nq * nt;
+    uint8_t* d = nullptr;
+    if (hipMalloc((void**)&d, st.host.size() + out_bytes + 16) != hipSuccess) return ORBX_ENOMEM;
+    uint8_t* dout = d + ((st.host.size() + 15) & ~(size_t)15);
+    orbx_status rc = ORBX_OK;
+    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
+    int* o = (int*)dout;
+    if (rc == ORBX_OK)
+        rc = orbm_allpairs_device(d + oq, nq, d + ot, nt, mode, o, o + nq, o + 2 * nq, (uint16_t*)dout, nullptr);
+    if (rc == ORBX_OK && hipDeviceSynchronize() != hipSuccess) rc = ORBX_EDEVICE;
+    if (rc == ORBX_OK && mode == ORBM_TOP2 &&
+        (hipMemcpy(best_idx, o, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(best, o + nq, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(second, o + 2 * nq, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = ORBX_EDEVICE;
+    if (rc == ORBX_OK && mode == ORBM_FULL_U16 && hipMemcpy(full, dout, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = ORBX_EDEVICE;
+    hipFree(d);
+    return rc;
+}
+
 orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const int* d_counts,
                                           int nframes, int cap, const int* d_pair_a, const int* d_pair_b, int npairs,
                                           int rows, int cols, int window, float nnratio, int check_ori,

@@ -33,7 +33,7 @@ TOP2, FULL_U16 = 0, 1
 EXPORTED = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_capacity", "orbx_extract", "orbx_get_level",
     "orbx_extract_batch_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
-    "orbx_debug_pyramid", "orbx_debug_candidates", "orbm_descriptor_distance", "orbm_allpairs_device",
+    "orbx_debug_pyramid", "orbx_debug_candidates", "orbm_descriptor_distance", "orbm_allpairs_device", "orbm_allpairs",
     "orbm_search_init_batch_device", "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
     "orbm_bow_search_device", "orbm_bow_search",
     "orbm_search_by_projection_device", "orbm_search_by_projection",
@@ -153,6 +153,7 @@ def _load():
     L.orbx_debug_candidates.argtypes = [vp, C.c_int, C.c_int, i32p, C.c_int, i32p]
     L.orbm_descriptor_distance.argtypes = [u8p, u8p]
     L.orbm_allpairs_device.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]
+    L.orbm_allpairs.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, C.c_int, vp, vp, vp, vp]
     L.orbm_search_init_batch_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int,
                                                 C.c_int, C.c_float, C.c_int, vp, vp, vp]
     L.orbx_compute_stereo_matches.argtypes = [vp, vp, vp, u8p, C.c_int, vp, u8p, C.c_int, C.c_float, C.c_float,
@@ -839,3 +840,19 @@ class BowBatch:
                                         self.stride, _ptr(self.nmatches), _stream(stream))
         _check("orbm_bow_search_device", rc)
         return self.match, self.nmatches
+
+
+def allpairs_host(q, t, mode=TOP2, device=0):
+    """orbm_allpairs on host arrays: TOP2 -> (best_idx, best, second); FULL_U16 -> (nq, nt) uint16."""
+    q = np.ascontiguousarray(q, np.uint8)
+    nq, nt = len(q), len(t)
+    t = np.ascontiguousarray(t if nt else np.zeros((1, 32), np.uint8), np.uint8)
+    if mode == TOP2:
+        out = [np.zeros(max(nq, 1), np.int32) for _ in range(3)]
+        _check("orbm_allpairs", lib.orbm_allpairs(device, _u8(q), nq, _u8(t), nt, TOP2, out[0].ctypes.data,
+                                                  out[1].ctypes.data, out[2].ctypes.data, None))
+        return tuple(o[:nq].copy() for o in out)
+    full = np.zeros((max(nq, 1), max(nt, 1)), np.uint16)
+    _check("orbm_allpairs", lib.orbm_allpairs(device, _u8(q), nq, _u8(t), nt, FULL_U16, None, None, None,
+                                              full.ctypes.data))
+    return full[:nq, :nt].copy()

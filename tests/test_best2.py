@@ -77,3 +77,18 @@ def test_gpu_best2_csr_rejects_bad_index(cuda):
     idx[0] = 20
     with pytest.raises(orbx.OrbxError):
         orbx.best2_csr(q, t, ptr, idx)
+
+
+@pytest.mark.gpu
+def test_gpu_allpairs_host(orbref, cuda):
+    """orbm_allpairs (host arrays): TOP2 against the oracle, FULL_U16 against numpy popcounts."""
+    import orbx
+    q, t, _, _ = case(5, nq=700, nt=900)
+    bi, b1, b2 = orbx.allpairs_host(q, t, orbx.TOP2)
+    wi, w1, w2 = orbref.allpairs_top2(q, t)
+    assert np.array_equal(bi, wi) and np.array_equal(b1, w1) and np.array_equal(b2, w2)
+    full = orbx.allpairs_host(q[:50], t, orbx.FULL_U16)
+    want = np.unpackbits(q[:50, None, :] ^ t[None, :, :], axis=2).sum(axis=2)
+    assert np.array_equal(full.astype(np.int64), want)
+    bi, b1, b2 = orbx.allpairs_host(q[:5], t[:0], orbx.TOP2)
+    assert np.all(bi == -1) and np.all(b1 == 256) and np.all(b2 == 256)
