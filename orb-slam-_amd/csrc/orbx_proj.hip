@@ -37,49 +37,86 @@ __device__ __forceinline__ int pj_lower_bound(const uint32_t* a, int n, uint32_t
     return lo;
 }
 
+// J1 as a stable counting sort over the 3072 cells: per-cell counts by LDS atomics (the
+// arrival slot is unordered), an exclusive scan, a scatter, then each feature's stable rank
+// = the number of lower indices in its own cell segment (a few entries).  Keys are
+// cell << 16 | index in ascending order, i.e. (cell, insertion) order.
+constexpr int kPjCells = kPjCols * kPjRows;
+
+__host__ __device__ inline size_t pj_grid_smem(int cap) { return (size_t)4 * (kPjCells + 4) + (size_t)6 * cap + 16; }
+
 __global__ __launch_bounds__(256) void k_pj_grid(const orbx_keypoint* __restrict__ kps, const int* __restrict__ counts,
                                                  int cap, float min_x, float min_y, float grid_w_inv,
                                                  float grid_h_inv, uint32_t* __restrict__ gkeys, int* __restrict__ gn)
 {
-    extern __shared__ uint32_t s_keys[];
-    __shared__ int s_ng;
-    const int f = blockIdx.x, tid = threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_grid[];
+    __shared__ uint32_t s_wsum[4];
+    uint32_t* start = s_grid;                                   // [kPjCells + 1] counts, then offsets
+    uint16_t* code = (uint16_t*)(s_grid + kPjCells + 4);        // [cap] cell, 0xFFFF = outside the grid
+    uint16_t* pos = code + cap;                                 // [cap] arrival slot within the cell
+    uint16_t* tmp = pos + cap;                                  // [cap] features grouped by cell
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = min(counts[f], cap);
-    int p2 = 1;
-    while (p2 < n) p2 <<= 1;
-    if (tid == 0) s_ng = 0;
+    for (int c = tid; c <= kPjCells; c += 256) start[c] = 0u;
     __syncthreads();
     const orbx_keypoint* k = kps + (size_t)f * cap;
-    for (int i = tid; i < p2; i += 256) {
-        uint32_t key = 0xFFFFFFFFu;
-        if (i < n) {   // PosInGrid, src/Frame.cc:504-518
-            const int px = (int)roundf((k[i].x - min_x) * grid_w_inv);
-            const int py = (int)roundf((k[i].y - min_y) * grid_h_inv);
-            if (px >= 0 && px < kPjCols && py >= 0 && py < kPjRows) {
-                key = ((uint32_t)(px * kPjRows + py) << 16) | (uint32_t)i;
-                atomicAdd(&s_ng, 1);
-            }
+    for (int i = tid; i < n; i += 256) {   // PosInGrid, src/Frame.cc:504-518
+        const int px = (int)roundf((k[i].x - min_x) * grid_w_inv);
+        const int py = (int)roundf((k[i].y - min_y) * grid_h_inv);
+        uint16_t cc = 0xFFFF;
+        if (px >= 0 && px < kPjCols && py >= 0 && py < kPjRows) {
+            cc = (uint16_t)(px * kPjRows + py);
+            pos[i] = (uint16_t)atomicAdd(&start[cc], 1u);
         }
-        s_keys[i] = key;
+        code[i] = cc;
     }
     __syncthreads();
-    for (int size = 2; size <= p2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = tid; i < (p2 >> 1); i += 256) {
-                const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-                const bool asc = (lo & size) == 0;
-                const uint32_t a = s_keys[lo], b = s_keys[hi];
-                if ((a > b) == asc) {
-                    s_keys[lo] = b;
-                    s_keys[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
+    constexpr int kPer = kPjCells / 256;   // 12 consecutive cells per thread
+    uint32_t loc[kPer], sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        loc[j] = start[tid * kPer + j];
+        sum += loc[j];
     }
-    const int ng = s_ng;
-    for (int g = tid; g < ng; g += 256) gkeys[(size_t)f * cap + g] = s_keys[g];
-    if (tid == 0) gn[f] = ng;
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t base = incl - sum;
+    for (int w = 0; w < wave; ++w) base += s_wsum[w];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        start[tid * kPer + j] = base;
+        base += loc[j];
+    }
+    if (tid == 255) start[kPjCells] = base;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256)
+        if (code[i] != 0xFFFF) tmp[start[code[i]] + pos[i]] = (uint16_t)i;
+    __syncthreads();
+    uint32_t* out = gkeys + (size_t)f * cap;
+    for (int i = tid; i < n; i += 256) {
+        const int cc = code[i];
+        if (cc == 0xFFFF) continue;
+        const int s0 = (int)start[cc], s1 = (int)start[cc + 1];
+        int r = 0;
+        for (int j = s0; j < s1; ++j) r += tmp[j] < i;
+        out[s0 + r] = (uint32_t)cc << 16 | (uint32_t)i;
+    }
+    if (tid == 0) gn[f] = (int)start[kPjCells];
+}
+
+void launch_pj_grid(const orbx_keypoint* kps, const int* counts, int nframes, int cap, float min_x, float min_y,
+                    float grid_w_inv, float grid_h_inv, uint32_t* gkeys, int* gn, hipStream_t s)
+{
+    const size_t sm = pj_grid_smem(cap);
+    hipFuncSetAttribute((const void*)k_pj_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL(k_pj_grid, dim3(nframes), dim3(256), sm, s, kps, counts, cap, min_x, min_y, grid_w_inv,
+                       grid_h_inv, gkeys, gn);
 }
 
 // GetFeaturesInArea(x, y, r * scale[level], level - 1, level) window of one MapPoint
@@ -449,11 +486,7 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
     uint32_t* gkeys = (uint32_t*)scratch;
     int* gn = (int*)(gkeys + (size_t)nframes * cap);
     PjResult* res = (PjResult*)(((uintptr_t)(gn + nframes) + 15) & ~(uintptr_t)15);
-    int p2 = 1;
-    while (p2 < cap) p2 <<= 1;
-    hipFuncSetAttribute((const void*)k_pj_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * p2));
-    hipLaunchKernelGGL(k_pj_grid, dim3(nframes), dim3(256), (size_t)4 * p2, s, kps, counts, cap, P.min_x, P.min_y,
-                       P.grid_w_inv, P.grid_h_inv, gkeys, gn);
+    launch_pj_grid(kps, counts, nframes, cap, P.min_x, P.min_y, P.grid_w_inv, P.grid_h_inv, gkeys, gn, s);
     hipLaunchKernelGGL(k_pj_points, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright, claimed,
                        cap, pts, pdesc, npts, pcap, P, gkeys, gn, res);
     hipFuncSetAttribute((const void*)k_pj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -839,11 +872,7 @@ void launch_pose_search(int mode, const orbx_keypoint* kps, const uint8_t* desc,
     uint32_t* gkeys = (uint32_t*)scratch;
     int* gn = (int*)(gkeys + (size_t)nframes * cap);
     PsResult* res = (PsResult*)(((uintptr_t)(gn + nframes) + 15) & ~(uintptr_t)15);
-    int p2 = 1;
-    while (p2 < cap) p2 <<= 1;
-    hipFuncSetAttribute((const void*)k_pj_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * p2));
-    hipLaunchKernelGGL(k_pj_grid, dim3(nframes), dim3(256), (size_t)4 * p2, s, kps, counts, cap, P.min_x, P.min_y,
-                       P.grid_w_inv, P.grid_h_inv, gkeys, gn);
+    launch_pj_grid(kps, counts, nframes, cap, P.min_x, P.min_y, P.grid_w_inv, P.grid_h_inv, gkeys, gn, s);
     switch (mode) {
     case ORBM_PROJ_LAST_FRAME:
         ps_launch<ORBM_PROJ_LAST_FRAME>(kps, desc, uright, claimed, counts, nframes, cap, pose, pts, pdesc, npts, pcap,
