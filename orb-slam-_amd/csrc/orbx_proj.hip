@@ -214,6 +214,71 @@ __device__ __forceinline__ void top_insert(TopK& t, uint32_t entry)
     t.n = min(t.n + 1, 255);
 }
 
+// J2 / P1 give a MapPoint kSub adjacent lanes: sub-lane s scans window positions lo + s, lo + s +
+// kSub, ...  Each keeps its own first kTop as 64-bit keys dist:9 | position:16 | entry low 22 bits
+// (bin, octave, index), i.e. in (distance, visiting position) order, and the group merges its
+// lists by kTop rounds of a min over the group's heads.  Same list as one sequential scan.
+constexpr int kSub = 4;
+struct TopK64 {
+    unsigned long long e[kTop];
+    int n;   // candidates this sub-lane saw (saturating)
+};
+
+__device__ __forceinline__ unsigned long long top_key(uint32_t entry, int p)
+{
+    return (unsigned long long)(entry >> 22) << 38 | (unsigned long long)p << 22 | (entry & 0x3FFFFFu);
+}
+
+__device__ __forceinline__ void top64_insert(TopK64& t, unsigned long long key)
+{
+    unsigned long long carry = key;
+    bool shifting = false;   // positions only grow within a sub-lane: equal distances stay in visiting order
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) {
+        const bool take = shifting || k >= t.n || t.e[k] > key;
+        if (take) {
+            const unsigned long long x = t.e[k];
+            t.e[k] = carry;
+            carry = x;
+            shifting = true;
+        }
+    }
+    t.n = min(t.n + 1, 255);
+}
+
+__device__ __forceinline__ unsigned long long sub_min_u64(unsigned long long v)
+{
+#pragma unroll
+    for (int o = 1; o < kSub; o <<= 1) {
+        const unsigned long long y = __shfl_xor(v, o);
+        v = y < v ? y : v;
+    }
+    return v;
+}
+
+// every lane of the group returns the merged list (entries as top_entry packs them)
+__device__ __forceinline__ TopK top_merge(TopK64& t)
+{
+    int total = t.n;
+#pragma unroll
+    for (int o = 1; o < kSub; o <<= 1) total += __shfl_xor(total, o);
+    TopK out;
+    out.n = min(total, 255);
+    int have = min(t.n, kTop);
+#pragma unroll
+    for (int r = 0; r < kTop; ++r) {
+        const unsigned long long h = have > 0 ? t.e[0] : ~0ull;
+        const unsigned long long m = sub_min_u64(h);
+        if (have > 0 && h == m) {   // keys are unique (positions): only the owner pops
+#pragma unroll
+            for (int k = 0; k + 1 < kTop; ++k) t.e[k] = t.e[k + 1];
+            --have;
+        }
+        out.e[r] = m == ~0ull ? 0u : (uint32_t)((m >> 38) << 22 | (m & 0x3FFFFFu));
+    }
+    return out;
+}
+
 // J2 result per MapPoint: the top-kTop list and the accept decision of its first entries
 struct TopResult {
     uint32_t e[kTop];
@@ -237,33 +302,40 @@ __global__ __launch_bounds__(256) void k_pj_points(const orbx_keypoint* __restri
                                                    int pcap, orbm_proj_params P, const uint32_t* __restrict__ gkeys,
                                                    const int* __restrict__ gn, PjResult* __restrict__ res)
 {
-    const int f = blockIdx.y, m = blockIdx.x * 256 + threadIdx.x;
-    if (m >= min(npts[f], pcap)) return;
+    const int f = blockIdx.y, m = blockIdx.x * (256 / kSub) + threadIdx.x / kSub, sub = threadIdx.x % kSub;
+    if (m >= min(npts[f], pcap)) return;   // uniform over the kSub lanes of a MapPoint
     const size_t mo = (size_t)f * pcap + m;
-    TopK T{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0};
+    TopK64 T64;
+    T64.n = 0;
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) T64.e[k] = 0ull;
     int accept = 0;
     const orbm_proj_point M = pts[mo];
+    bool scanned = false;
     if (M.flags & 1) {
         const uint32_t* keys = gkeys + (size_t)f * cap;
         const PjWindow w = pj_window(M, P, keys, gn[f]);
         if (w.ok) {
+            scanned = true;
             const orbx_keypoint* K = kps + (size_t)f * cap;
             const float* U = uright + (size_t)f * cap;
             const uint8_t* C = claimed + (size_t)f * cap;
             const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
             const uint4 q0 = qd[0], q1 = qd[1];
-            for (int p = w.lo; p < w.hi; ++p) {   // src/ORBmatcher.cc:78-113, in visiting order
+            for (int p = w.lo + sub; p < w.hi; p += kSub) {   // src/ORBmatcher.cc:78-113, visiting order
                 const int idx = pj_candidate(w, M, keys, p, K, U);
                 if (idx < 0 || C[idx]) continue;
                 const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
-                top_insert(T, top_entry(pj_ham(q0, q1, d[0], d[1]), 0, K[idx].octave, idx));
+                top64_insert(T64, top_key(top_entry(pj_ham(q0, q1, d[0], d[1]), 0, K[idx].octave, idx), p));
             }
-            // the scan's best / second are the first two entries (multiset top two, first wins ties)
-            if (T.n > 0)
-                accept = pj_accept(top_dist(T.e[0]), top_oct(T.e[0]), T.n > 1 ? top_dist(T.e[1]) : 256,
-                                   T.n > 1 ? top_oct(T.e[1]) : -1, P.nnratio);
         }
     }
+    const TopK T = top_merge(T64);   // whole group: `scanned` is uniform over it
+    if (sub != 0) return;
+    // the scan's best / second are the first two entries (multiset top two, first wins ties)
+    if (scanned && T.n > 0)
+        accept = pj_accept(top_dist(T.e[0]), top_oct(T.e[0]), T.n > 1 ? top_dist(T.e[1]) : 256,
+                           T.n > 1 ? top_oct(T.e[1]) : -1, P.nnratio);
     PjResult R;
 #pragma unroll
     for (int k = 0; k < kTop; ++k) R.e[k] = T.e[k];
@@ -487,8 +559,8 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
     int* gn = (int*)(gkeys + (size_t)nframes * cap);
     PjResult* res = (PjResult*)(((uintptr_t)(gn + nframes) + 15) & ~(uintptr_t)15);
     launch_pj_grid(kps, counts, nframes, cap, P.min_x, P.min_y, P.grid_w_inv, P.grid_h_inv, gkeys, gn, s);
-    hipLaunchKernelGGL(k_pj_points, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright, claimed,
-                       cap, pts, pdesc, npts, pcap, P, gkeys, gn, res);
+    hipLaunchKernelGGL(k_pj_points, dim3((pcap + 256 / kSub - 1) / (256 / kSub), nframes), dim3(256), 0, s, kps, desc,
+                       uright, claimed, cap, pts, pdesc, npts, pcap, P, gkeys, gn, res);
     hipFuncSetAttribute((const void*)k_pj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)replay_lds_bytes(cap));
     hipLaunchKernelGGL(k_pj_resolve, dim3(nframes), dim3(64), replay_lds_bytes(cap), s, kps, desc, uright, claimed,
@@ -708,43 +780,60 @@ __global__ __launch_bounds__(256) void k_ps_points(const orbx_keypoint* __restri
                                                    int* __restrict__ match, int* __restrict__ nmatches)
 {
     constexpr bool kSearch = MODE <= ORBM_PROJ_SIM3;
-    const int f = blockIdx.y, m = blockIdx.x * 256 + threadIdx.x;
-    if (m >= min(npts[f], pcap)) return;
+    const int f = blockIdx.y, m = blockIdx.x * (256 / kSub) + threadIdx.x / kSub, sub = threadIdx.x % kSub;
+    if (m >= min(npts[f], pcap)) return;   // uniform over the kSub lanes of a MapPoint
     const size_t mo = (size_t)f * pcap + m;
     int bestIdx = -1, accept = 0;
-    TopK T{{0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, 0};
+    TopK64 T64;
+    T64.n = 0;
+#pragma unroll
+    for (int k = 0; k < kTop; ++k) T64.e[k] = 0ull;
+    unsigned long long best = ~0ull;   // Fuse: first minimum as (dist, position, index)
     const orbm_map_point M = pts[mo];
+    bool scanned = false;
     if (M.flags & 1) {
         const PsCam c = ps_camera(MODE, pose + (size_t)f * 24, P);
         const uint32_t* keys = gkeys + (size_t)f * cap;
         PsWin w;
         if (ps_project<MODE>(c, M, P, w) && ps_window(w, P, keys, gn[f])) {
+            scanned = true;
             const orbx_keypoint* K = kps + (size_t)f * cap;
             const float* U = uright + (size_t)f * cap;
             const uint8_t* C = claimed + (size_t)f * cap;
             const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
             const uint4 q0 = qd[0], q1 = qd[1];
             const bool bins = kSearch && (MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME) && P.check_ori;
-            int bestDist = 256;
-            for (int p = w.lo; p < w.hi; ++p) {
+            for (int p = w.lo + sub; p < w.hi; p += kSub) {
                 const int idx = ps_candidate<MODE>(w, keys, p, K, U, P);
                 if (idx < 0 || (kSearch && C[idx])) continue;
                 const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
                 const int dist = pj_ham(q0, q1, d[0], d[1]);
                 if (kSearch) {
-                    top_insert(T, top_entry(dist, bins ? ps_rot_bin(M.angle, K[idx].angle) : 0, 0, idx));
-                } else if (dist < bestDist) {
-                    bestDist = dist;
-                    bestIdx = idx;
+                    top64_insert(T64, top_key(top_entry(dist, bins ? ps_rot_bin(M.angle, K[idx].angle) : 0, 0, idx),
+                                              p));
+                } else {
+                    const unsigned long long key =
+                        (unsigned long long)dist << 32 | (unsigned long long)p << 16 | (unsigned)idx;
+                    best = key < best ? key : best;
                 }
             }
-            if (kSearch) {
-                bestIdx = T.n > 0 ? top_idx(T.e[0]) : -1;
-                bestDist = T.n > 0 ? top_dist(T.e[0]) : 256;
-            }
-            accept = bestIdx >= 0 && bestDist <= ps_threshold<MODE>(P);
         }
     }
+    TopK T;
+    if (kSearch) {
+        T = top_merge(T64);   // whole group: `scanned` is uniform over it
+        if (scanned && T.n > 0) {
+            bestIdx = top_idx(T.e[0]);
+            accept = top_dist(T.e[0]) <= ps_threshold<MODE>(P);
+        }
+    } else {
+        best = sub_min_u64(best);
+        if (best != ~0ull) {
+            bestIdx = (int)(best & 0xFFFF);
+            accept = (int)(best >> 32) <= ps_threshold<MODE>(P);
+        }
+    }
+    if (sub != 0) return;
     if (kSearch) {
         PsResult R;
 #pragma unroll
@@ -854,7 +943,8 @@ static void ps_launch(const orbx_keypoint* kps, const uint8_t* desc, const float
                       hipStream_t s)
 {
     if (MODE >= ORBM_FUSE) hipMemsetAsync(nmatches, 0, sizeof(int) * (size_t)nframes, s);
-    hipLaunchKernelGGL(k_ps_points<MODE>, dim3((pcap + 255) / 256, nframes), dim3(256), 0, s, kps, desc, uright,
+    hipLaunchKernelGGL(k_ps_points<MODE>, dim3((pcap + 256 / kSub - 1) / (256 / kSub), nframes), dim3(256), 0, s,
+                       kps, desc, uright,
                        claimed, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
     if (MODE <= ORBM_PROJ_SIM3) {
         hipFuncSetAttribute((const void*)k_ps_resolve<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
