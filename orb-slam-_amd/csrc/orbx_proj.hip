@@ -27,21 +27,14 @@ __device__ __forceinline__ int pj_ham(const uint4& a0, const uint4& a1, const ui
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-__device__ __forceinline__ int pj_lower_bound(const uint32_t* a, int n, uint32_t v)
-{
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (a[mid] < v) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
 // J1 as a stable counting sort over the 3072 cells: per-cell counts by LDS atomics (the
 // arrival slot is unordered), an exclusive scan, a scatter, then each feature's stable rank
 // = the number of lower indices in its own cell segment (a few entries).  Keys are
 // cell << 16 | index in ascending order, i.e. (cell, insertion) order.
 constexpr int kPjCells = kPjCols * kPjRows;
+
+// per frame: cap keys, then the kPjCells + 1 cell offsets (cell c = keys [off[c], off[c + 1]))
+__host__ __device__ inline size_t pj_grid_stride(int cap) { return (size_t)cap + kPjCells + 4; }
 
 __host__ __device__ inline size_t pj_grid_smem(int cap) { return (size_t)4 * (kPjCells + 4) + (size_t)6 * cap + 16; }
 
@@ -98,7 +91,8 @@ __global__ __launch_bounds__(256) void k_pj_grid(const orbx_keypoint* __restrict
     for (int i = tid; i < n; i += 256)
         if (code[i] != 0xFFFF) tmp[start[code[i]] + pos[i]] = (uint16_t)i;
     __syncthreads();
-    uint32_t* out = gkeys + (size_t)f * cap;
+    uint32_t* out = gkeys + (size_t)f * pj_grid_stride(cap);
+    for (int c = tid; c <= kPjCells; c += 256) out[cap + c] = start[c];   // cell -> first key position
     for (int i = tid; i < n; i += 256) {
         const int cc = code[i];
         if (cc == 0xFFFF) continue;
@@ -121,13 +115,13 @@ void launch_pj_grid(const orbx_keypoint* kps, const int* counts, int nframes, in
 
 // GetFeaturesInArea(x, y, r * scale[level], level - 1, level) window of one MapPoint
 struct PjWindow {
-    int lo, hi, cy0, cy1, minLevel, maxLevel;
+    int lo, hi, cx0, cx1, cy0, cy1, minLevel, maxLevel;
     float x, y, rr, rs;   // rr = window radius; rs = r * scale[level] for the stereo test
     bool ok;
 };
 
 __device__ __forceinline__ PjWindow pj_window(const orbm_proj_point& M, const orbm_proj_params& P,
-                                              const uint32_t* keys, int ng)
+                                              const uint32_t* keys, int cap)
 {
     PjWindow w;
     w.ok = false;
@@ -150,8 +144,10 @@ __device__ __forceinline__ PjWindow pj_window(const orbm_proj_point& M, const or
     if (w.cy0 >= kPjRows) return w;
     w.cy1 = min(kPjRows - 1, (int)ceilf((w.y - P.min_y + w.rr) * P.grid_h_inv));
     if (w.cy1 < 0) return w;
-    w.lo = pj_lower_bound(keys, ng, (uint32_t)(cx0 * kPjRows) << 16);
-    w.hi = pj_lower_bound(keys, ng, (uint32_t)((cx1 + 1) * kPjRows) << 16);
+    w.cx0 = cx0;
+    w.cx1 = cx1;
+    w.lo = (int)keys[cap + cx0 * kPjRows];
+    w.hi = (int)keys[cap + (cx1 + 1) * kPjRows];
     w.ok = true;
     return w;
 }
@@ -313,8 +309,8 @@ __global__ __launch_bounds__(256) void k_pj_points(const orbx_keypoint* __restri
     const orbm_proj_point M = pts[mo];
     bool scanned = false;
     if (M.flags & 1) {
-        const uint32_t* keys = gkeys + (size_t)f * cap;
-        const PjWindow w = pj_window(M, P, keys, gn[f]);
+        const uint32_t* keys = gkeys + (size_t)f * pj_grid_stride(cap);
+        const PjWindow w = pj_window(M, P, keys, cap);
         if (w.ok) {
             scanned = true;
             const orbx_keypoint* K = kps + (size_t)f * cap;
@@ -322,11 +318,14 @@ __global__ __launch_bounds__(256) void k_pj_points(const orbx_keypoint* __restri
             const uint8_t* C = claimed + (size_t)f * cap;
             const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
             const uint4 q0 = qd[0], q1 = qd[1];
-            for (int p = w.lo + sub; p < w.hi; p += kSub) {   // src/ORBmatcher.cc:78-113, visiting order
-                const int idx = pj_candidate(w, M, keys, p, K, U);
-                if (idx < 0 || C[idx]) continue;
-                const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
-                top64_insert(T64, top_key(top_entry(pj_ham(q0, q1, d[0], d[1]), 0, K[idx].octave, idx), p));
+            for (int cx = w.cx0; cx <= w.cx1; ++cx) {   // src/ORBmatcher.cc:78-113, visiting order
+                const int a = (int)keys[cap + cx * kPjRows + w.cy0], b = (int)keys[cap + cx * kPjRows + w.cy1 + 1];
+                for (int p = a + sub; p < b; p += kSub) {
+                    const int idx = pj_candidate(w, M, keys, p, K, U);
+                    if (idx < 0 || C[idx]) continue;
+                    const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
+                    top64_insert(T64, top_key(top_entry(pj_ham(q0, q1, d[0], d[1]), 0, K[idx].octave, idx), p));
+                }
             }
         }
     }
@@ -492,12 +491,11 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(counts[f], cap), np = min(npts[f], pcap);
     const ReplayLds S = replay_lds(cap);
-    const uint32_t* keys = gkeys + (size_t)f * cap;
+    const uint32_t* keys = gkeys + (size_t)f * pj_grid_stride(cap);
     const orbx_keypoint* K = kps + (size_t)f * cap;
     const float* U = uright + (size_t)f * cap;
     const uint8_t* C = claimed + (size_t)f * cap;
     const orbm_proj_point* Pf = pts + (size_t)f * pcap;
-    const int ng = gn[f];
     auto obs_of = [&](int m) { return (Pf[m].flags & 2) ? 1 : 0; };
     auto accept_of = [&](uint32_t c1, bool has2, uint32_t c2) {
         return pj_accept(top_dist(c1), top_oct(c1), has2 ? top_dist(c2) : 256, has2 ? top_oct(c2) : -1, P.nnratio);
@@ -506,7 +504,7 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
     // min of the rest (the sequential scan's result)
     auto rescan = [&](int m, const uint8_t* taken) {
         const orbm_proj_point Mp = Pf[m];
-        const PjWindow w = pj_window(Mp, P, keys, ng);
+        const PjWindow w = pj_window(Mp, P, keys, cap);
         const uint4* qd = reinterpret_cast<const uint4*>(pdesc + ((size_t)f * pcap + m) * 32);
         const uint4 q0 = qd[0], q1 = qd[1];
         unsigned long long b1 = ~0ull, b2 = ~0ull;
@@ -547,7 +545,7 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
 
 size_t proj_scratch_bytes(int nframes, int cap, int pcap)
 {
-    return (size_t)nframes * cap * 4 + (size_t)nframes * 4 + (size_t)nframes * pcap * sizeof(PjResult) + 256;
+    return (size_t)nframes * pj_grid_stride(cap) * 4 + (size_t)nframes * 4 + (size_t)nframes * pcap * sizeof(PjResult) + 256;
 }
 
 void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uright, const uint8_t* claimed,
@@ -556,7 +554,7 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
                  hipStream_t s)
 {
     uint32_t* gkeys = (uint32_t*)scratch;
-    int* gn = (int*)(gkeys + (size_t)nframes * cap);
+    int* gn = (int*)(gkeys + (size_t)nframes * pj_grid_stride(cap));
     PjResult* res = (PjResult*)(((uintptr_t)(gn + nframes) + 15) & ~(uintptr_t)15);
     launch_pj_grid(kps, counts, nframes, cap, P.min_x, P.min_y, P.grid_w_inv, P.grid_h_inv, gkeys, gn, s);
     hipLaunchKernelGGL(k_pj_points, dim3((pcap + 256 / kSub - 1) / (256 / kSub), nframes), dim3(256), 0, s, kps, desc,
@@ -628,7 +626,7 @@ __device__ __forceinline__ PsCam ps_camera(int mode, const float* __restrict__ p
 
 struct PsWin {
     float u, v, r, ur;
-    int minLevel, maxLevel, cy0, cy1, lo, hi;
+    int minLevel, maxLevel, cx0, cx1, cy0, cy1, lo, hi;
 };
 
 // MapPoint::PredictScale (src/MapPoint.cc:385-417)
@@ -702,7 +700,7 @@ __device__ __forceinline__ bool ps_project(const PsCam& c, const orbm_map_point&
     return true;
 }
 
-__device__ __forceinline__ bool ps_window(PsWin& w, const orbm_pose_params& P, const uint32_t* keys, int ng)
+__device__ __forceinline__ bool ps_window(PsWin& w, const orbm_pose_params& P, const uint32_t* keys, int cap)
 {
     const int cx0 = max(0, ps_x86_int(floorf((w.u - P.min_x - w.r) * P.grid_w_inv)));
     if (cx0 >= kPjCols) return false;
@@ -712,8 +710,10 @@ __device__ __forceinline__ bool ps_window(PsWin& w, const orbm_pose_params& P, c
     if (w.cy0 >= kPjRows) return false;
     w.cy1 = min(kPjRows - 1, ps_x86_int(ceilf((w.v - P.min_y + w.r) * P.grid_h_inv)));
     if (w.cy1 < 0) return false;
-    w.lo = pj_lower_bound(keys, ng, (uint32_t)(cx0 * kPjRows) << 16);
-    w.hi = pj_lower_bound(keys, ng, (uint32_t)((cx1 + 1) * kPjRows) << 16);
+    w.cx0 = cx0;
+    w.cx1 = cx1;
+    w.lo = (int)keys[cap + cx0 * kPjRows];
+    w.hi = (int)keys[cap + (cx1 + 1) * kPjRows];
     return true;
 }
 
@@ -793,9 +793,9 @@ __global__ __launch_bounds__(256) void k_ps_points(const orbx_keypoint* __restri
     bool scanned = false;
     if (M.flags & 1) {
         const PsCam c = ps_camera(MODE, pose + (size_t)f * 24, P);
-        const uint32_t* keys = gkeys + (size_t)f * cap;
+        const uint32_t* keys = gkeys + (size_t)f * pj_grid_stride(cap);
         PsWin w;
-        if (ps_project<MODE>(c, M, P, w) && ps_window(w, P, keys, gn[f])) {
+        if (ps_project<MODE>(c, M, P, w) && ps_window(w, P, keys, cap)) {
             scanned = true;
             const orbx_keypoint* K = kps + (size_t)f * cap;
             const float* U = uright + (size_t)f * cap;
@@ -803,18 +803,22 @@ __global__ __launch_bounds__(256) void k_ps_points(const orbx_keypoint* __restri
             const uint4* qd = reinterpret_cast<const uint4*>(pdesc + mo * 32);
             const uint4 q0 = qd[0], q1 = qd[1];
             const bool bins = kSearch && (MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME) && P.check_ori;
-            for (int p = w.lo + sub; p < w.hi; p += kSub) {
-                const int idx = ps_candidate<MODE>(w, keys, p, K, U, P);
-                if (idx < 0 || (kSearch && C[idx])) continue;
-                const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
-                const int dist = pj_ham(q0, q1, d[0], d[1]);
-                if (kSearch) {
-                    top64_insert(T64, top_key(top_entry(dist, bins ? ps_rot_bin(M.angle, K[idx].angle) : 0, 0, idx),
-                                              p));
-                } else {
-                    const unsigned long long key =
-                        (unsigned long long)dist << 32 | (unsigned long long)p << 16 | (unsigned)idx;
-                    best = key < best ? key : best;
+            for (int cx = w.cx0; cx <= w.cx1; ++cx) {   // GetFeaturesInArea order, rows cy0..cy1 only
+                const int a = (int)keys[cap + cx * kPjRows + w.cy0], b = (int)keys[cap + cx * kPjRows + w.cy1 + 1];
+                for (int p = a + sub; p < b; p += kSub) {
+                    const int idx = ps_candidate<MODE>(w, keys, p, K, U, P);
+                    if (idx < 0 || (kSearch && C[idx])) continue;
+                    const uint4* d = reinterpret_cast<const uint4*>(desc + ((size_t)f * cap + idx) * 32);
+                    const int dist = pj_ham(q0, q1, d[0], d[1]);
+                    if (kSearch) {
+                        top64_insert(T64, top_key(top_entry(dist, bins ? ps_rot_bin(M.angle, K[idx].angle) : 0, 0,
+                                                            idx),
+                                                  p));
+                    } else {
+                        const unsigned long long key =
+                            (unsigned long long)dist << 32 | (unsigned long long)p << 16 | (unsigned)idx;
+                        best = key < best ? key : best;
+                    }
                 }
             }
         }
@@ -862,12 +866,11 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(counts[f], cap), np = min(npts[f], pcap);
     const ReplayLds S = replay_lds(cap);
-    const uint32_t* keys = gkeys + (size_t)f * cap;
+    const uint32_t* keys = gkeys + (size_t)f * pj_grid_stride(cap);
     const orbx_keypoint* K = kps + (size_t)f * cap;
     const float* U = uright + (size_t)f * cap;
     const uint8_t* C = claimed + (size_t)f * cap;
     const orbm_map_point* Pf = pts + (size_t)f * pcap;
-    const int ng = gn[f];
     const PsCam cam = ps_camera(MODE, pose + (size_t)f * 24, P);
     const bool rot = kRotMode && P.check_ori;
     const int thr = ps_threshold<MODE>(P);
@@ -879,7 +882,7 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
         const orbm_map_point Mp = Pf[m];
         PsWin w;
         ps_project<MODE>(cam, Mp, P, w);   // true and non-empty: J2 found candidates in it
-        ps_window(w, P, keys, ng);
+        ps_window(w, P, keys, cap);
         const uint4* qd = reinterpret_cast<const uint4*>(pdesc + ((size_t)f * pcap + m) * 32);
         const uint4 q0 = qd[0], q1 = qd[1];
         unsigned long long b1 = ~0ull;
@@ -932,7 +935,7 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
 
 size_t pose_scratch_bytes(int nframes, int cap, int pcap)
 {
-    return (size_t)nframes * cap * 4 + (size_t)nframes * 4 + (size_t)nframes * pcap * sizeof(PsResult) + 256;
+    return (size_t)nframes * pj_grid_stride(cap) * 4 + (size_t)nframes * 4 + (size_t)nframes * pcap * sizeof(PsResult) + 256;
 }
 
 template <int MODE>
@@ -960,7 +963,7 @@ void launch_pose_search(int mode, const orbx_keypoint* kps, const uint8_t* desc,
                         const orbm_pose_params& P, void* scratch, int* match, int* nmatches, hipStream_t s)
 {
     uint32_t* gkeys = (uint32_t*)scratch;
-    int* gn = (int*)(gkeys + (size_t)nframes * cap);
+    int* gn = (int*)(gkeys + (size_t)nframes * pj_grid_stride(cap));
     PsResult* res = (PsResult*)(((uintptr_t)(gn + nframes) + 15) & ~(uintptr_t)15);
     launch_pj_grid(kps, counts, nframes, cap, P.min_x, P.min_y, P.grid_w_inv, P.grid_h_inv, gkeys, gn, s);
     switch (mode) {
