@@ -14,6 +14,8 @@
 // (32-fx)(32-fy)*32 ..., (sum + 2^14) >> 15; gray = (w0*c0 + 9617*c1 + w2*c2 + 2^13) >> 14.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "orbx_kernels.hpp"
 
 namespace orbx {
@@ -68,15 +70,51 @@ __device__ __forceinline__ uint32_t ig_gray(const int v[3], int w0, int w2)
     return (uint32_t)((v[0] * w0 + v[1] * 9617 + v[2 < CH ? 2 : 0] * w2 + (1 << 13)) >> 14);
 }
 
+// Interior pixels (all four taps inside, rows 4-byte aligned): one aligned 8/12-byte load per
+// source row, realigned by alignbyte; per channel the two taps of a row are gathered by one v_perm
+// and blended horizontally by one v_dot4_u32_u8 with (32 - fx, fx).  OpenCV's sum
+// (a0 (32-fx)(32-fy) 32 + ... + 2^14) >> 15 is 32 X with X = (32-fy) h_a + fy h_b, so it equals
+// (X + 512) >> 10 exactly.
 template <int CH>
 __device__ __forceinline__ uint32_t ig_remap_pixel(const uint8_t* __restrict__ S, int rows, int cols, size_t sstep,
-                                                   float mxv, float myv, int w0, int w2)
+                                                   int xlim, float mxv, float myv, int w0, int w2)
 {
     constexpr int C3 = CH > 1 ? 3 : 1;
     const int sx32 = ig_round_x86(mxv * 32.0f);
     const int sy32 = ig_round_x86(myv * 32.0f);
     const int fx = sx32 & 31, fy = sy32 & 31;
     const int sx = min(max(sx32 >> 5, -32768), 32767), sy = min(max(sy32 >> 5, -32768), 32767);
+    if ((unsigned)sx < (unsigned)xlim && (unsigned)sy < (unsigned)(rows - 1)) {   // xlim = 0: never
+        const uint8_t* pa = S + (size_t)sy * sstep + sx * CH;
+        const uint32_t sh = (uint32_t)((uintptr_t)pa & 3);
+        const uint8_t* a4 = pa - sh;
+        uint32_t la, ha, lb, hb;
+        if (CH == 1) {
+            const uint2 A = *reinterpret_cast<const uint2*>(a4);
+            const uint2 B = *reinterpret_cast<const uint2*>(a4 + sstep);
+            la = __builtin_amdgcn_alignbyte(A.y, A.x, sh);
+            lb = __builtin_amdgcn_alignbyte(B.y, B.x, sh);
+            ha = hb = 0u;
+        } else {
+            const uint3 A = *reinterpret_cast<const uint3*>(a4);
+            const uint3 B = *reinterpret_cast<const uint3*>(a4 + sstep);
+            la = __builtin_amdgcn_alignbyte(A.y, A.x, sh);
+            ha = __builtin_amdgcn_alignbyte(A.z, A.y, sh);
+            lb = __builtin_amdgcn_alignbyte(B.y, B.x, sh);
+            hb = __builtin_amdgcn_alignbyte(B.z, B.y, sh);
+        }
+        const uint32_t wx = (uint32_t)(32 - fx) | (uint32_t)fx << 8;
+        const uint32_t wy0 = (uint32_t)(32 - fy), wy1 = (uint32_t)fy;
+        int val[3];
+#pragma unroll
+        for (int k = 0; k < C3; ++k) {
+            const uint32_t sel = (uint32_t)k | (uint32_t)(k + CH) << 8 | 0x0C0C0000u;   // (tap x, tap x+1, 0, 0)
+            const uint32_t hA = __builtin_amdgcn_udot4(__builtin_amdgcn_perm(ha, la, sel), wx, 0u, false);
+            const uint32_t hB = __builtin_amdgcn_udot4(__builtin_amdgcn_perm(hb, lb, sel), wx, 0u, false);
+            val[k] = (int)((hA * wy0 + hB * wy1 + 512u) >> 10);
+        }
+        return ig_gray<CH>(val, w0, w2);
+    }
     const int w00 = (32 - fx) * (32 - fy) * 32, w01 = fx * (32 - fy) * 32;
     const int w10 = (32 - fx) * fy * 32, w11 = fx * fy * 32;
     const bool y0 = (unsigned)sy < (unsigned)rows, y1 = (unsigned)(sy + 1) < (unsigned)rows;
@@ -92,7 +130,8 @@ template <int CH>
 __global__ __launch_bounds__(256) void k_ingest(const uint8_t* __restrict__ src, int rows, int cols, int rgb,
                                                 size_t sstep, size_t sfs, const float* __restrict__ mx,
                                                 const float* __restrict__ my, int nmaps, int drows, int dcols,
-                                                uint8_t* __restrict__ dst, size_t dstep, size_t dfs, int gpr)
+                                                uint8_t* __restrict__ dst, size_t dstep, size_t dfs, int gpr,
+                                                int xlim)
 {
     constexpr int C3 = CH > 1 ? 3 : 1;
     const int f = blockIdx.y;
@@ -119,7 +158,7 @@ __global__ __launch_bounds__(256) void k_ingest(const uint8_t* __restrict__ src,
         const float xs[4] = {vx.x, vx.y, vx.z, vx.w}, ys[4] = {vy.x, vy.y, vy.z, vy.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            if (k < n) packed |= ig_remap_pixel<CH>(S, rows, cols, sstep, xs[k], ys[k], w0, w2) << (8 * k);
+            if (k < n) packed |= ig_remap_pixel<CH>(S, rows, cols, sstep, xlim, xs[k], ys[k], w0, w2) << (8 * k);
     } else {
         const uint8_t* p = S + (size_t)y * sstep + (size_t)x0 * CH;
 #pragma unroll
@@ -158,18 +197,23 @@ void launch_ingest(const uint8_t* src, int batch, int rows, int cols, int channe
 {
     const int gpr = (dcols + 3) / 4;
     const dim3 grid((unsigned)(((size_t)gpr * drows + 255) / 256), batch);
+    // interior fast path bound (ig_remap_pixel): x + 1 < cols and the aligned 8/12-byte window inside
+    // the row; it needs 4-byte aligned rows, otherwise every pixel takes the checked path
+    const int kw = channels == 1 ? 8 : 12;
+    int xlim = std::min(cols - 2, (cols * channels - kw) / channels) + 1;   // fast iff 0 <= x < xlim
+    if ((((uintptr_t)src | sstep | sfs) & 3) || cols * channels < kw || xlim < 0) xlim = 0;
     switch (channels) {
     case 1:
         hipLaunchKernelGGL(k_ingest<1>, grid, dim3(256), 0, s, src, rows, cols, rgb, sstep, sfs, mx, my, nmaps, drows,
-                           dcols, dst, dstep, dfs, gpr);
+                           dcols, dst, dstep, dfs, gpr, xlim);
         break;
     case 3:
         hipLaunchKernelGGL(k_ingest<3>, grid, dim3(256), 0, s, src, rows, cols, rgb, sstep, sfs, mx, my, nmaps, drows,
-                           dcols, dst, dstep, dfs, gpr);
+                           dcols, dst, dstep, dfs, gpr, xlim);
         break;
     default:
         hipLaunchKernelGGL(k_ingest<4>, grid, dim3(256), 0, s, src, rows, cols, rgb, sstep, sfs, mx, my, nmaps, drows,
-                           dcols, dst, dstep, dfs, gpr);
+                           dcols, dst, dstep, dfs, gpr, xlim);
         break;
     }
 }
