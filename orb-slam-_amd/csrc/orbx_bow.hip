@@ -15,6 +15,8 @@
 //                 (:1679-1723) and removal, nmatches.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "orbx_kernels.hpp"
 
 namespace orbx {
@@ -35,6 +37,21 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
     return v;
+}
+
+// the same over a fully active wave with DPP row reductions and four readlanes (no LDS round trips)
+__device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v)
+{
+    auto dpp_min = [](uint32_t x, auto ctrl) {
+        return min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, decltype(ctrl)::value, 0xF, 0xF, false));
+    };
+    v = dpp_min(v, std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]
+    v = dpp_min(v, std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]
+    v = dpp_min(v, std::integral_constant<int, 0x141>{});   // row_half_mirror
+    v = dpp_min(v, std::integral_constant<int, 0x140>{});   // row_mirror
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(r0, r1), min(r2, r3));
 }
 
 __device__ __forceinline__ int bow_rot_bin(float a1, float a2)
@@ -99,90 +116,138 @@ __global__ __launch_bounds__(256) void k_bow_nodes(int mode, const orbm_bow_view
     orbm_triang_params T;
     if (tri) T = TP[p];
 
-    for (int a = a0; a < a1; ++a) {
-        const int idx1 = A.fv_idx[a];
-        const bool mp1 = A.has_mp ? A.has_mp[idx1] != 0 : false;
-        bool stereo1 = false;
+    // The node's first 64 view2 features stay in registers for all of its view1 features, and the
+    // view1 features are loaded 64 at a time (lane j = feature j) and broadcast by readlane: the
+    // serial replay below touches global memory only for nodes with more than 64 view2 features.
+    int c_idx2 = 0;
+    bool c_mp2 = false, c_st2 = false;
+    uint4 c_e0 = make_uint4(0, 0, 0, 0), c_e1 = c_e0;
+    orbx_keypoint c_kp2{};
+    if (lane < nb) {
+        c_idx2 = B.fv_idx[b0 + lane];
+        c_mp2 = B.has_mp ? B.has_mp[c_idx2] != 0 : false;
+        const uint4* d2 = reinterpret_cast<const uint4*>(B.desc + (size_t)c_idx2 * 32);
+        c_e0 = d2[0];
+        c_e1 = d2[1];
         if (tri) {
-            if (mp1) continue;   // "If there is already a MapPoint skip" (:775-776)
-            stereo1 = A.u_right ? A.u_right[idx1] >= 0 : false;
-            if (T.only_stereo && !stereo1) continue;
-        } else if (!mp1) {
-            continue;            // !pMP || pMP->isBad()
+            c_st2 = B.u_right ? B.u_right[c_idx2] >= 0 : false;
+            c_kp2 = B.kps[c_idx2];
         }
-        const uint4* d1 = reinterpret_cast<const uint4*>(A.desc + (size_t)idx1 * 32);
-        const uint4 q0 = d1[0], q1 = d1[1];
-        const orbx_keypoint kp1 = A.kps[idx1];
-        uint32_t best = 0xFFFFFFFFu;   // greedy: (dist << 16 | pos) first min; triangulation: (dist, last pos)
-        int second = 256;              // this lane's second smallest distance (multiset)
-        for (int c = 0; c < nb; c += 64) {
-            const int pos = c + lane;
-            if (pos >= nb) break;
-            const int idx2 = B.fv_idx[b0 + pos];
-            const bool mp2 = B.has_mp ? B.has_mp[idx2] != 0 : false;
-            bool ok;
+    }
+    const int n1 = a1 - a0;
+    for (int abase = 0; abase < n1; abase += 64) {
+        int l_idx1 = 0, l_flags = 0;
+        uint4 l_q0 = make_uint4(0, 0, 0, 0), l_q1 = l_q0;
+        float l_x = 0.f, l_y = 0.f, l_ang = 0.f;
+        if (abase + lane < n1) {
+            l_idx1 = A.fv_idx[a0 + abase + lane];
+            const bool mp = A.has_mp ? A.has_mp[l_idx1] != 0 : false;
+            const bool st = tri && A.u_right ? A.u_right[l_idx1] >= 0 : false;
+            l_flags = (mp ? 1 : 0) | (st ? 2 : 0);
+            const uint4* d1 = reinterpret_cast<const uint4*>(A.desc + (size_t)l_idx1 * 32);
+            l_q0 = d1[0];
+            l_q1 = d1[1];
+            const orbx_keypoint kp = A.kps[l_idx1];
+            l_x = kp.x;
+            l_y = kp.y;
+            l_ang = kp.angle;
+        }
+        const int cnt = min(64, n1 - abase);
+        for (int j = 0; j < cnt; ++j) {
+            auto bc = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); };
+            auto bcf = [&](float v) { return __builtin_bit_cast(float, bc(__builtin_bit_cast(uint32_t, v))); };
+            const int idx1 = (int)bc((uint32_t)l_idx1);
+            const int flags1 = (int)bc((uint32_t)l_flags);
+            const bool mp1 = flags1 & 1;
+            bool stereo1 = false;
             if (tri) {
-                ok = !mp2;
-            } else {
-                ok = !((done[pos >> 5] >> (pos & 31)) & 1u);
-                if (mode == ORBM_BOW_KF_KF) ok = ok && mp2;
+                if (mp1) continue;   // "If there is already a MapPoint skip" (:775-776)
+                stereo1 = (flags1 & 2) != 0;
+                if (T.only_stereo && !stereo1) continue;
+            } else if (!mp1) {
+                continue;            // !pMP || pMP->isBad()
             }
-            if (!ok) continue;
-            const uint4* d2 = reinterpret_cast<const uint4*>(B.desc + (size_t)idx2 * 32);
-            const int dist = ham_u4(q0, q1, d2[0], d2[1]);
+            const uint4 q0 = make_uint4(bc(l_q0.x), bc(l_q0.y), bc(l_q0.z), bc(l_q0.w));
+            const uint4 q1 = make_uint4(bc(l_q1.x), bc(l_q1.y), bc(l_q1.z), bc(l_q1.w));
+            const float x1 = bcf(l_x), y1 = bcf(l_y), ang1 = bcf(l_ang);
+            uint32_t best = 0xFFFFFFFFu;   // greedy: (dist << 16 | pos) first min; triangulation: (dist, last pos)
+            int second = 256;              // this lane's second smallest distance (multiset)
+            for (int c = 0; c < nb; c += 64) {
+                const int pos = c + lane;
+                if (pos >= nb) break;
+                int idx2 = c_idx2;
+                bool mp2 = c_mp2;
+                uint4 e0 = c_e0, e1 = c_e1;
+                if (c > 0) {
+                    idx2 = B.fv_idx[b0 + pos];
+                    mp2 = B.has_mp ? B.has_mp[idx2] != 0 : false;
+                    const uint4* d2 = reinterpret_cast<const uint4*>(B.desc + (size_t)idx2 * 32);
+                    e0 = d2[0];
+                    e1 = d2[1];
+                }
+                bool ok;
+                if (tri) {
+                    ok = !mp2;
+                } else {
+                    ok = !((done[pos >> 5] >> (pos & 31)) & 1u);
+                    if (mode == ORBM_BOW_KF_KF) ok = ok && mp2;
+                }
+                if (!ok) continue;
+                const int dist = ham_u4(q0, q1, e0, e1);
+                if (tri) {
+                    const bool stereo2 = c > 0 ? (B.u_right ? B.u_right[idx2] >= 0 : false) : c_st2;
+                    if (T.only_stereo && !stereo2) continue;
+                    if (dist > kTH_LOW) continue;
+                    const orbx_keypoint kp2 = c > 0 ? B.kps[idx2] : c_kp2;
+                    if (!stereo1 && !stereo2) {   // :800-806
+                        const float distex = T.ex - kp2.x, distey = T.ey - kp2.y;
+                        if (__builtin_fmaf(distex, distex, distey * distey) < 100 * T.scale2[kp2.octave]) continue;
+                    }
+                    if (!bow_epipolar(x1, y1, kp2.x, kp2.y, kp2.octave, T)) continue;
+                    // the sequential `dist > bestDist -> skip, else take` keeps the LAST minimum
+                    best = min(best, ((uint32_t)dist << 16) | (uint32_t)(0xFFFF - pos));
+                } else {
+                    const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)pos;
+                    if (key < best) {
+                        second = min(second, (int)(best >> 16));
+                        best = key;
+                    } else {
+                        second = min(second, dist);
+                    }
+                }
+            }
+            const uint32_t wbest = wave_min_dpp(best);
+            if (wbest == 0xFFFFFFFFu) continue;
+            const int bdist = (int)(wbest >> 16);
             if (tri) {
-                const bool stereo2 = B.u_right ? B.u_right[idx2] >= 0 : false;
-                if (T.only_stereo && !stereo2) continue;
-                if (dist > kTH_LOW) continue;
-                const orbx_keypoint kp2 = B.kps[idx2];
-                if (!stereo1 && !stereo2) {   // :800-806
-                    const float distex = T.ex - kp2.x, distey = T.ey - kp2.y;
-                    if (__builtin_fmaf(distex, distex, distey * distey) < 100 * T.scale2[kp2.octave]) continue;
-                }
-                if (!bow_epipolar(kp1.x, kp1.y, kp2.x, kp2.y, kp2.octave, T)) continue;
-                // the sequential `dist > bestDist -> skip, else take` keeps the LAST minimum
-                best = min(best, ((uint32_t)dist << 16) | (uint32_t)(0xFFFF - pos));
-            } else {
-                const uint32_t key = ((uint32_t)dist << 16) | (uint32_t)pos;
-                if (key < best) {
-                    second = min(second, (int)(best >> 16));
-                    best = key;
-                } else {
-                    second = min(second, dist);
-                }
-            }
-        }
-        const uint32_t wbest = wave_min_u32(best);
-        if (wbest == 0xFFFFFFFFu) continue;
-        const int bdist = (int)(wbest >> 16);
-        if (tri) {
-            const int pos = 0xFFFF - (int)(wbest & 0xFFFF);
-            if (lane == 0) {
-                const int idx2 = B.fv_idx[b0 + pos];
-                M[idx1] = idx2;
-                if (check_ori) BN[idx1] = bow_rot_bin(kp1.angle, B.kps[idx2].angle);
-            }
-            continue;
-        }
-        // second best of the whole node = min(the winner lane's second, every other lane's best)
-        const int mine = best == wbest ? second : (int)min(best >> 16, 256u);
-        const int bsecond = (int)wave_min_u32((uint32_t)mine);
-        const bool accept = (mode == ORBM_BOW_KF_F ? bdist <= kTH_LOW : bdist < kTH_LOW) &&
-                            (float)bdist < nnratio * (float)bsecond;
-        if (accept) {
-            const int pos = (int)(wbest & 0xFFFF);
-            const int idx2 = B.fv_idx[b0 + pos];
-            if (lane == 0) {
-                done[pos >> 5] |= 1u << (pos & 31);
-                if (mode == ORBM_BOW_KF_F) {
-                    M[idx2] = idx1;
-                    if (check_ori) BN[idx2] = bow_rot_bin(kp1.angle, B.kps[idx2].angle);
-                } else {
+                const int pos = 0xFFFF - (int)(wbest & 0xFFFF);
+                if (lane == 0) {
+                    const int idx2 = B.fv_idx[b0 + pos];
                     M[idx1] = idx2;
-                    if (check_ori) BN[idx1] = bow_rot_bin(kp1.angle, B.kps[idx2].angle);
+                    if (check_ori) BN[idx1] = bow_rot_bin(ang1, B.kps[idx2].angle);
                 }
+                continue;
             }
-            bow_wave_sync();
+            // second best of the whole node = min(the winner lane's second, every other lane's best)
+            const int mine = best == wbest ? second : (int)min(best >> 16, 256u);
+            const int bsecond = (int)wave_min_dpp((uint32_t)mine);
+            const bool accept = (mode == ORBM_BOW_KF_F ? bdist <= kTH_LOW : bdist < kTH_LOW) &&
+                                (float)bdist < nnratio * (float)bsecond;
+            if (accept) {
+                const int pos = (int)(wbest & 0xFFFF);
+                if (lane == 0) {
+                    const int idx2 = B.fv_idx[b0 + pos];
+                    done[pos >> 5] |= 1u << (pos & 31);
+                    if (mode == ORBM_BOW_KF_F) {
+                        M[idx2] = idx1;
+                        if (check_ori) BN[idx2] = bow_rot_bin(ang1, B.kps[idx2].angle);
+                    } else {
+                        M[idx1] = idx2;
+                        if (check_ori) BN[idx1] = bow_rot_bin(ang1, B.kps[idx2].angle);
+                    }
+                }
+                bow_wave_sync();
+            }
         }
     }
 }
