@@ -149,7 +149,6 @@ __device__ __forceinline__ fh2 pmax2(fh2 a, fh2 b) { return __builtin_elementwis
 __device__ __forceinline__ fh2 pmin2(fh2 a, fh2 b) { return __builtin_elementwise_minimum(a, b); }
 __device__ __forceinline__ fh2 pmax3(fh2 a, fh2 b, fh2 c) { return pmax2(pmax2(a, b), c); }
 __device__ __forceinline__ fh2 pmin3(fh2 a, fh2 b, fh2 c) { return pmin2(pmin2(a, b), c); }
-__device__ __forceinline__ uint32_t fast_pack(uint32_t x) { return 0x64FF6400u + x - (x << 16); }
 
 // packed tile row pitch in dwords (pixels), a multiple of 4 for 16-byte LDS stores
 __host__ __device__ inline int fast_tile_pitch(int max_roi_w) { return (max_roi_w + 3) & ~3; }
@@ -264,11 +263,13 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch& F, uint32_t* til
     for (int u = 0; u < kFastLd; ++u) {
         if (F.dst[u] < 0) continue;
         const uint32_t w = __builtin_amdgcn_alignbyte(F.hi[u], F.lo[u], F.sh[u]);
+        // fast_pack(x) = (0x6400 | x, 0x64FF - x) = 0x64FF6400 ^ (x | x << 16) for a byte x:
+        // one v_perm (byte k of w into bytes 0 and 2, zeros elsewhere) and one xor per pixel
         uint4 q;
-        q.x = fast_pack(w & 0xFFu);
-        q.y = fast_pack((w >> 8) & 0xFFu);
-        q.z = fast_pack((w >> 16) & 0xFFu);
-        q.w = fast_pack(w >> 24);
+        q.x = __builtin_amdgcn_perm(0u, w, 0x0C000C00u) ^ 0x64FF6400u;
+        q.y = __builtin_amdgcn_perm(0u, w, 0x0C010C01u) ^ 0x64FF6400u;
+        q.z = __builtin_amdgcn_perm(0u, w, 0x0C020C02u) ^ 0x64FF6400u;
+        q.w = __builtin_amdgcn_perm(0u, w, 0x0C030C03u) ^ 0x64FF6400u;
         *(uint4*)(tile + F.dst[u]) = q;
     }
 }
