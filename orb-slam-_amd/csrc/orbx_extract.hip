@@ -240,18 +240,23 @@ struct FastCellSrc {
 
 __device__ __forceinline__ void fast_issue(const FastCellSrc& S, int i0, int lane, int tp, FastPrefetch& F)
 {
+    // 32-bit byte offsets from the wave-uniform aligned ROI origin: scalar base + vector offset
+    // addressing, no 64-bit address arithmetic per load
+    const __attribute__((address_space(1))) uint8_t* base =
+        (const __attribute__((address_space(1))) uint8_t*)((uintptr_t)S.src & ~(uintptr_t)3);
+    const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
 #pragma unroll
     for (int u = 0; u < kFastLd; ++u) {
         const int i = i0 + u * 64 + lane;
         F.dst[u] = -1;
         if (i < S.ntot) {
             const int r = (int)(((float)i + 0.5f) * S.inv_nd), k = i - __mul24(r, S.nd);
-            const uintptr_t a = (uintptr_t)(S.src + __mul24(r, S.pitch) + 4 * k);
+            const uint32_t o = s0 + (uint32_t)__mul24(r, S.pitch) + 4u * (uint32_t)k;
             const __attribute__((address_space(1))) uint32_t* ap =
-                (const __attribute__((address_space(1))) uint32_t*)(a & ~(uintptr_t)3);
+                (const __attribute__((address_space(1))) uint32_t*)(base + (o & ~3u));
             F.lo[u] = ap[0];
             F.hi[u] = ap[1];
-            F.sh[u] = (uint32_t)(a & 3);
+            F.sh[u] = o & 3u;
             F.dst[u] = __mul24(r, tp) + 4 * k;
         }
     }
@@ -282,7 +287,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     // per-wave LDS sized from the geometry's largest cell ROI
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
     const int kTileP = fast_tile_pitch(G->max_roi_w);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
     const int c0 = ((lb - f * gridDim.x) * 4 + wave) * kCellsPerWave;
@@ -1011,7 +1016,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][kRawSlots];
     __shared__ __attribute__((aligned(16))) uint32_t s_rowT[4][kTCols * kTP];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x, bx = lb - f * gridDim.x;
     const int L = G->nlevels;
