@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(int mode, const orbm_bow_view
                                                    int stride)
 {
     __shared__ uint32_t s_done[4][kBowWords];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // uniform
     const int p = blockIdx.y;
     const orbm_bow_view A = V1[p], B = V2[p];
     const int k = blockIdx.x * 4 + wave;

@@ -372,7 +372,7 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
                                                           int* __restrict__ qcnt, uint4* __restrict__ qtop)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave: uniform
     const int fa = pa[pair], fb = pb[pair];
     const int n10 = gn[2 * fa], ng = gn[2 * fb + 1];
     uint32_t* keys = (uint32_t*)smem;
