@@ -255,7 +255,8 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     g.lcap = lcap;
     g.pyr_bytes = (pyr + 255) & ~255LL;
     int spill = 0;
-    for (int l = 0; l < t.nlevels; ++l) spill += std::max(0, g.lv[l].slot_cap - qt_regcap(l));
+    g.qt_kpt0 = (long long)rows * cols > kQtBigArea ? 24 : 16;
+    for (int l = 0; l < t.nlevels; ++l) spill += std::max(0, g.lv[l].slot_cap - qt_regcap(g, l));
     g.spill_per_frame = std::max(spill, 1);
     if (lcap >= 65535 || quadtree_smem_bytes(g) > 160 * 1024) return ORBX_EINVAL;
 

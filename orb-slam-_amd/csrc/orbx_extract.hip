@@ -619,7 +619,7 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
     {
         int off = 0;
         for (int q = 0; q < l; ++q) {
-            const int extra = G->lv[q].slot_cap - qt_regcap(q);
+            const int extra = G->lv[q].slot_cap - qt_regcap(*G, q);
             off += extra > 0 ? extra : 0;
         }
         fspill += off;
@@ -913,11 +913,30 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
     // register capacity per level (qt_kpt): level 0 holds most candidates; levels >= 2 hold a
     // few hundred, and their small register file lets describe / FAST waves share the CU
     hipFuncSetAttribute((const void*)k_quadtree<512, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipFuncSetAttribute((const void*)k_quadtree<512, 24>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipFuncSetAttribute((const void*)k_quadtree<512, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipFuncSetAttribute((const void*)k_quadtree<256, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    static_assert(512 * 16 == 8192 && 512 * 8 == 4096 && 256 * 4 == 1024, "qt_regcap");
-    hipLaunchKernelGGL((k_quadtree<512, 16>), dim3(1, batch), dim3(512), smem, s, 0, b.geom, b.cells, b.slots,
-                       b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+    // Small batches (the per-frame host path): one launch of the level-0 kernel over every level, so
+    // the levels run concurrently instead of as three dependent launches (latency, not throughput).
+    // A level run with more register capacity than qt_regcap(g, l) spills less than its region holds.
+    if (batch <= kQtMergedMaxBatch) {
+        if (g.qt_kpt0 == 24)
+            hipLaunchKernelGGL((k_quadtree<512, 24>), dim3(g.nlevels, batch), dim3(512), smem, s, 0, b.geom, b.cells,
+                               b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts,
+                               b.status);
+        else
+            hipLaunchKernelGGL((k_quadtree<512, 16>), dim3(g.nlevels, batch), dim3(512), smem, s, 0, b.geom, b.cells,
+                               b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts,
+                               b.status);
+        return;
+    }
+    // the launched templates must match qt_regcap(g, l), which sizes the spill regions
+    if (g.qt_kpt0 == 24)
+        hipLaunchKernelGGL((k_quadtree<512, 24>), dim3(1, batch), dim3(512), smem, s, 0, b.geom, b.cells, b.slots,
+                           b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+    else
+        hipLaunchKernelGGL((k_quadtree<512, 16>), dim3(1, batch), dim3(512), smem, s, 0, b.geom, b.cells, b.slots,
+                           b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
     if (g.nlevels > 1)
         hipLaunchKernelGGL((k_quadtree<512, 8>), dim3(1, batch), dim3(512), smem, s, 1, b.geom, b.cells, b.slots,
                            b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);

@@ -52,6 +52,7 @@ struct Geometry {
     int max_cells_level;      // largest per-level cell count
     int max_roi_w, max_roi_h; // largest FAST cell ROI (sizes the per-wave LDS tiles)
     int lcap;                 // quadtree list capacity (max level cap + slack)
+    int qt_kpt0;              // level-0 quadtree keypoints per thread (16, or 24 for large frames)
     long long pyr_bytes;      // bytes per frame for levels 1..L-1
     int umax[16];
     LevelGeom lv[kMaxLevels];

@@ -52,9 +52,14 @@ enum : int {
 size_t quadtree_smem_bytes(const Geometry& g);
 // quadtree workgroup size and keypoints held in registers per thread at level l (the rest spill
 // to global): level 0 holds most candidates, levels >= 2 a few hundred
+// (level 0: 16 per thread, or 24 for frames above kQtBigArea pixels, whose level-0 candidates
+// would otherwise mostly spill; the 24-wide kernel's 178 VGPRs crowd co-running waves, so
+// smaller frames keep 16)
+constexpr long long kQtBigArea = 1000000;
+constexpr int kQtMergedMaxBatch = 8;   // batches up to this size run all levels in one launch
 __host__ __device__ inline int qt_nt(int l) { return l >= 2 ? 256 : 512; }
-__host__ __device__ inline int qt_kpt(int l) { return l == 0 ? 16 : (l == 1 ? 8 : 4); }
-__host__ __device__ inline int qt_regcap(int l) { return qt_nt(l) * qt_kpt(l); }
+__host__ __device__ inline int qt_kpt(const Geometry& g, int l) { return l == 0 ? g.qt_kpt0 : (l == 1 ? 8 : 4); }
+__host__ __device__ inline int qt_regcap(const Geometry& g, int l) { return qt_nt(l) * qt_kpt(g, l); }
 
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);

@@ -83,7 +83,7 @@ def config1(args):
 
 def config3(args):
     import orbref
-    W, H, NF, B = 752, 480, args.feat or 1000, args.batch or 32
+    W, H, NF, B = 752, 480, args.feat or 1000, args.batch or 96
     dev = torch.device("cuda", 0)
     pairs = [orbx_synth.stereo_pair(100 + i, W, H) for i in range(B)]
     frames = torch.from_numpy(np.stack([im for pr in pairs for im in pr])).to(dev)   # L0 R0 L1 R1 ...
@@ -142,7 +142,7 @@ def config3(args):
 def config5(args, world, rank, local):
     import orbref
     dev = torch.device("cuda", local)
-    W, H, NF, B = 1920, 1080, 4000, args.batch or 16
+    W, H, NF, B = 1920, 1080, 4000, args.batch or 128
     out = {"config": "config5_1920x1080_4000feat + 10k x 10k Hamming", "n_gpus": world}
     # extraction (frames sharded like config 4: every rank its own batch)
     frames = torch.from_numpy(np.stack([orbx_synth.gen_image(5 + 97 * rank + i, W, H) for i in range(B)])).to(dev)
