@@ -67,17 +67,24 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
     const int sy1 = (int)((uint32_t)ytab[D.ytab_off + dy0 + dyn - 1].x >> 16);
     const int nrows = sy1 - sy0 + 1;
     const int nd = (sw + 3) >> 2;                 // dwords per staged row
+    // 32-bit byte offsets from the block-uniform aligned base (scalar base + vector offset loads);
+    // the row split uses a float reciprocal: (i + 0.5) / nd sits 0.5 / nd from any integer and the
+    // float product errs by < (i + 1) / nd * 2^-23, so r is exact for i < 2^22 (here i < 13k)
+    const __attribute__((address_space(1))) uint8_t* base =
+        (const __attribute__((address_space(1))) uint8_t*)((uintptr_t)src & ~(uintptr_t)3);
+    const uint32_t o0 = (uint32_t)((uintptr_t)src & 3) + (uint32_t)sy0 * (uint32_t)spitch;
+    const float inv_nd = 1.0f / (float)nd;
     for (int i = threadIdx.x; i < nrows * nd; i += 256) {
-        const int r = i / nd, k = i - r * nd;
-        const uint8_t* p = src + (size_t)(sy0 + r) * spitch + 4 * k;
-        const uintptr_t a = (uintptr_t)p;
-        const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
+        const int r = (int)(((float)i + 0.5f) * inv_nd), k = i - __mul24(r, nd);
+        const uint32_t o = o0 + __umul24((uint32_t)r, (uint32_t)spitch) + 4u * (uint32_t)k;
+        const __attribute__((address_space(1))) uint32_t* ap =
+            (const __attribute__((address_space(1))) uint32_t*)(base + (o & ~3u));
         // the second dword is needed only if some of its bytes belong to the row; an aligned
         // dword that starts inside the row cannot run past the (4-byte aligned) buffer end
-        const int sh = (int)(a & 3);
-        const bool tail = sh == 0 || 4 * k + 4 - sh >= sw;
+        const uint32_t sh = o & 3u;
+        const bool tail = sh == 0 || 4 * k + 4 - (int)sh >= sw;
         const uint32_t lo = ap[0], hi = tail ? 0u : ap[1];
-        s_src[r * nd + k] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3));
+        s_src[r * nd + k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
     }
     __syncthreads();
     const uint8_t* S = (const uint8_t*)s_src;
@@ -88,27 +95,32 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
     uint8_t* drow0 = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy0 * D.pitch;
     for (int g = threadIdx.x; g < q; g += 256) {
         const int dx0 = g * 4;
-        int x0[4], x1[4], a0[4], a1[4];
+        // every product fits a 24 x 24 -> 32-bit multiply (v_mul_u32_u24, full rate; the compiler
+        // otherwise emits the quarter-rate v_mul_lo_u32 for h * b).  The two taps keep separate
+        // addresses: byte reads at x0 and x0 + 1 merge into an unaligned ds_read_u16, which
+        // measured 3.5x slower for the whole kernel.
+        int x0[4], x1[4];
+        uint32_t a0[4], a1[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int2 xt = xtab[D.xtab_off + min(dx0 + k, D.w - 1)];
             x0[k] = xt.x & 0xFFFF;
             x1[k] = (int)((uint32_t)xt.x >> 16);
-            a0[k] = xt.y & 0xFFFF;
-            a1[k] = (int)((uint32_t)xt.y >> 16);
+            a0[k] = (uint32_t)xt.y & 0xFFFFu;
+            a1[k] = (uint32_t)xt.y >> 16;
         }
         for (int rr = 0; rr < dyn; ++rr) {
             const int2 yt = ytab[D.ytab_off + dy0 + rr];
             const uint8_t* r0 = S + ((yt.x & 0xFFFF) - sy0) * srow;
             const uint8_t* r1 = S + ((int)((uint32_t)yt.x >> 16) - sy0) * srow;
-            const int b0 = yt.y & 0xFFFF, b1 = (int)((uint32_t)yt.y >> 16);
+            const uint32_t b0 = (uint32_t)yt.y & 0xFFFFu, b1 = (uint32_t)yt.y >> 16;
             uint32_t packed = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int h0 = r0[x0[k]] * a0[k] + r0[x1[k]] * a1[k];
-                const int h1 = r1[x0[k]] * a0[k] + r1[x1[k]] * a1[k];
-                const int v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-                packed |= (uint32_t)(v > 255 ? 255 : v) << (8 * k);
+                const uint32_t h0 = __umul24(r0[x0[k]], a0[k]) + __umul24(r0[x1[k]], a1[k]);
+                const uint32_t h1 = __umul24(r1[x0[k]], a0[k]) + __umul24(r1[x1[k]], a1[k]);
+                const uint32_t v = (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
+                packed |= min(v, 255u) << (8 * k);
             }
             // columns past the level width land in the row's pitch padding (pitch = align64(w))
             *reinterpret_cast<uint32_t*>(drow0 + (size_t)rr * D.pitch + dx0) = packed;
