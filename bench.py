@@ -259,14 +259,17 @@ def main():
     }
     def roofline(st):
         dom = max(st, key=lambda k: st[k])
-        launches = {"pyramid": NLEVELS - 1}.get(dom, 1)
+        # several launches of one kernel per stage: per-launch figures are stage / launches,
+        # like rocprofv3's per-kernel average (FAST: two LDS classes of cells on config 2,
+        # levels 0-3 and 4-7, orbx_extract.hip fast_groups)
+        launches = {"pyramid": NLEVELS - 1, "fast": 2}.get(dom, 1)
         t_launch = st[dom] / launches * 1e-3
         achieved = alg[dom] / launches / t_launch / 1e9
-        kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree<16|8|2>",
+        kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree<512,16|512,8|256,4>",
                  "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
         # stages made of several kernels: their per-launch counters add up
         PARTS = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"],
-                 "quadtree": ["k_quadtree<16>", "k_quadtree<8>", "k_quadtree<2>"]}
+                 "quadtree": ["k_quadtree<512, 16>", "k_quadtree<512, 8>", "k_quadtree<256, 4>"]}
         # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
         # same command (tools/collect_pmc.sh -> tools/pmc_summary.py); null when absent
         traffic = None

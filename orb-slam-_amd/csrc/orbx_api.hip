@@ -223,6 +223,8 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
                 if (c.roi_w > 66 || c.roi_h > 66) return ORBX_EINVAL;
                 g.max_roi_w = std::max(g.max_roi_w, (int)c.roi_w);
                 g.max_roi_h = std::max(g.max_roi_h, (int)c.roi_h);
+                L.roi_mw = std::max(L.roi_mw, (int)c.roi_w);
+                L.roi_mh = std::max(L.roi_mh, (int)c.roi_h);
                 const int dw = c.roi_w - 6, dh = c.roi_h - 6;
                 c.slot_base = slot;
                 c.slot_cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
@@ -249,6 +251,7 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         L.patch_size = (float)(int)(31 * t.scale[l]);   // :1013
     }
     g.ncells = (int)cells.size();
+    fast_groups(g);
     g.slots_per_frame = slot;
     g.out_per_frame = out;
     g.max_cells_level = maxcells;

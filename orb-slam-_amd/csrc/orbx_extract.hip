@@ -294,20 +294,21 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch& F, uint32_t* til
 __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                     const Cell* __restrict__ cells,
                                                     uint32_t* __restrict__ slots,
-                                                    int* __restrict__ cell_counts)
+                                                    int* __restrict__ cell_counts,
+                                                    int cb, int ce, int rw, int rh)
 {
-    // per-wave LDS sized from the geometry's largest cell ROI
+    // cells [cb, ce); per-wave LDS sized from the group's largest cell ROI (rw x rh)
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
-    const int kTileP = fast_tile_pitch(G->max_roi_w);
+    const int kTileP = fast_tile_pitch(rw);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
-    const int c0 = ((lb - f * gridDim.x) * 4 + wave) * kCellsPerWave;
-    const int c1 = min(c0 + kCellsPerWave, G->ncells);
+    const int c0 = cb + ((lb - f * gridDim.x) * 4 + wave) * kCellsPerWave;
+    const int c1 = min(c0 + kCellsPerWave, ce);
     if (c0 >= c1) return;   // wave-uniform; no block barriers below
-    uint32_t* tile = (uint32_t*)(s_fast + (size_t)wave * fast_wave_bytes(G->max_roi_w, G->max_roi_h));
-    uint8_t* map = (uint8_t*)(tile + (size_t)G->max_roi_h * kTileP);
-    uint16_t* list = (uint16_t*)(map + ((((size_t)(G->max_roi_h - 4) * (G->max_roi_w - 4)) + 3) & ~(size_t)3));
+    uint32_t* tile = (uint32_t*)(s_fast + (size_t)wave * fast_wave_bytes(rw, rh));
+    uint8_t* map = (uint8_t*)(tile + (size_t)rh * kTileP);
+    uint16_t* list = (uint16_t*)(map + ((((size_t)(rh - 4) * (rw - 4)) + 3) & ~(size_t)3));
     const int tq = min(G->ini_th, G->min_th);
 
     // ROI -> LDS: aligned dword loads (alignbyte realigns rows of any pitch; the ROI ends >= 16
@@ -454,13 +455,58 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     }
 }
 
+// LDS per CU on gfx950: the occupancy a FAST launch's per-wave tiles allow
+constexpr size_t kLdsPerCu = 160 * 1024;
+static int fast_blocks_per_cu(int w, int h) { return (int)(kLdsPerCu / (4 * fast_wave_bytes(w, h))); }
+
+void fast_groups(Geometry& g)
+{
+    // The longest prefix of levels whose largest ROI keeps level 0's occupancy is launch 0;
+    // the remaining levels (KITTI 1241x376: levels 4-7, ROIs up to 38x46 against 38x39) are
+    // launch 1.  Cells are stored level by level, so each launch is a contiguous range.
+    int w = g.lv[0].roi_mw, h = g.lv[0].roi_mh, split = g.nlevels;
+    const int occ0 = fast_blocks_per_cu(std::max(w, 8), std::max(h, 8));
+    for (int l = 1; l < g.nlevels; ++l) {
+        const int nw = std::max(w, g.lv[l].roi_mw), nh = std::max(h, g.lv[l].roi_mh);
+        if (fast_blocks_per_cu(nw, nh) < occ0) {
+            split = l;
+            break;
+        }
+        w = nw;
+        h = nh;
+    }
+    g.fast_cb[0] = 0;
+    g.fast_rw[0] = std::max(w, 8);
+    g.fast_rh[0] = std::max(h, 8);
+    if (split == g.nlevels) {
+        g.fast_groups = 1;
+        g.fast_cb[1] = g.ncells;
+        return;
+    }
+    int w1 = 8, h1 = 8;
+    for (int l = split; l < g.nlevels; ++l) {
+        w1 = std::max(w1, g.lv[l].roi_mw);
+        h1 = std::max(h1, g.lv[l].roi_mh);
+    }
+    g.fast_groups = 2;
+    g.fast_cb[1] = g.lv[split].cell_begin;
+    g.fast_cb[2] = g.ncells;
+    g.fast_rw[1] = w1;
+    g.fast_rh[1] = h1;
+}
+
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
     const int per_block = 4 * kCellsPerWave;
-    dim3 grid((g.ncells + per_block - 1) / per_block, batch);
-    const size_t smem = 4 * fast_wave_bytes(g.max_roi_w, g.max_roi_h);
-    hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts);
+    for (int i = 0; i < g.fast_groups; ++i) {
+        const int cb = g.fast_cb[i], ce = g.fast_cb[i + 1];
+        if (ce <= cb) continue;
+        dim3 grid((ce - cb + per_block - 1) / per_block, batch);
+        const size_t smem = 4 * fast_wave_bytes(g.fast_rw[i], g.fast_rh[i]);
+        hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
+                           cb, ce, g.fast_rw[i], g.fast_rh[i]);
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -40,6 +40,7 @@ struct LevelGeom {
     float scale;              // mvScaleFactor[l]
     float inv_scale;          // mvInvScaleFactor[l]
     float patch_size;         // (float)(int)(PATCH_SIZE * scale)
+    int roi_mw, roi_mh;       // largest FAST cell ROI of this level
 };
 
 struct Geometry {
@@ -50,7 +51,12 @@ struct Geometry {
     int out_per_frame;        // sum of level caps
     int spill_per_frame;      // quadtree register-overflow keypoints per frame
     int max_cells_level;      // largest per-level cell count
-    int max_roi_w, max_roi_h; // largest FAST cell ROI (sizes the per-wave LDS tiles)
+    int max_roi_w, max_roi_h; // largest FAST cell ROI
+    // FAST launches: cells [fast_cb[i], fast_cb[i + 1]) with per-wave LDS sized from that
+    // group's largest ROI (fast_rw/rh).  The short, tall cells of the coarse levels get their
+    // own launch so they do not lower the occupancy of the fine levels' launch.
+    int fast_groups;
+    int fast_cb[3], fast_rw[2], fast_rh[2];
     int lcap;                 // quadtree list capacity (max level cap + slack)
     int qt_kpt0;              // level-0 quadtree keypoints per thread (16, or 24 for large frames)
     long long pyr_bytes;      // bytes per frame for levels 1..L-1

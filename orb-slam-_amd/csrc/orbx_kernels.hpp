@@ -62,6 +62,7 @@ __host__ __device__ inline int qt_kpt(const Geometry& g, int l) { return l == 0 
 __host__ __device__ inline int qt_regcap(const Geometry& g, int l) { return qt_nt(l) * qt_kpt(g, l); }
 
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
+void fast_groups(Geometry& g);   // host: FAST launch groups (cell ranges, LDS sizes)
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
 void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s);
 void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, orbx_keypoint* kps,
