@@ -238,6 +238,7 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* m, int p, int W2, int t)
 // (a 37x38 ROI is 6 passes of 64 lanes); bigger ROIs load their remainder synchronously.
 constexpr int kFastLd = 6;
 constexpr int kCellsPerWave = 3;   // cells per wave: the next cell's ROI loads fly under this one's passes
+constexpr int kFastWaves = 1;      // waves per workgroup: LDS is allocated per wave, not in 4-wave steps
 
 struct FastPrefetch {
     uint32_t lo[kFastLd], hi[kFastLd], sh[kFastLd];
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
-    const int c0 = cb + ((lb - f * gridDim.x) * 4 + wave) * kCellsPerWave;
+    const int c0 = cb + ((lb - f * gridDim.x) * kFastWaves + wave) * kCellsPerWave;
     const int c1 = min(c0 + kCellsPerWave, ce);
     if (c0 >= c1) return;   // wave-uniform; no block barriers below
     uint32_t* tile = (uint32_t*)(s_fast + (size_t)wave * fast_wave_bytes(rw, rh));
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
 
 // LDS per CU on gfx950: the occupancy a FAST launch's per-wave tiles allow
 constexpr size_t kLdsPerCu = 160 * 1024;
-static int fast_blocks_per_cu(int w, int h) { return (int)(kLdsPerCu / (4 * fast_wave_bytes(w, h))); }
+static int fast_blocks_per_cu(int w, int h) { return (int)(kLdsPerCu / (kFastWaves * fast_wave_bytes(w, h))); }
 
 void fast_groups(Geometry& g)
 {
@@ -497,14 +498,14 @@ void fast_groups(Geometry& g)
 
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
-    const int per_block = 4 * kCellsPerWave;
+    const int per_block = kFastWaves * kCellsPerWave;
     for (int i = 0; i < g.fast_groups; ++i) {
         const int cb = g.fast_cb[i], ce = g.fast_cb[i + 1];
         if (ce <= cb) continue;
         dim3 grid((ce - cb + per_block - 1) / per_block, batch);
-        const size_t smem = 4 * fast_wave_bytes(g.fast_rw[i], g.fast_rh[i]);
+        const size_t smem = kFastWaves * fast_wave_bytes(g.fast_rw[i], g.fast_rh[i]);
         hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        hipLaunchKernelGGL(k_fast_cells, grid, dim3(256), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
+        hipLaunchKernelGGL(k_fast_cells, grid, dim3(64 * kFastWaves), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
                            cb, ce, g.fast_rw[i], g.fast_rh[i]);
     }
 }
