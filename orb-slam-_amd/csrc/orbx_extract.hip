@@ -237,8 +237,11 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* m, int p, int W2, int t)
 // ROI bytes of one cell staged in registers: up to kFastLd aligned dword pairs per lane
 // (a 37x38 ROI is 6 passes of 64 lanes); bigger ROIs load their remainder synchronously.
 constexpr int kFastLd = 6;
-constexpr int kCellsPerWave = 3;   // cells per wave: the next cell's ROI loads fly under this one's passes
-constexpr int kFastWaves = 1;      // waves per workgroup: LDS is allocated per wave, not in 4-wave steps
+#ifndef ORBX_FAST_CPW
+#define ORBX_FAST_CPW 3
+#endif
+constexpr int kCellsPerWave = ORBX_FAST_CPW;   // cells per wave: the next cell's ROI loads fly under this one's passes
+constexpr int kFastWaves = 1;                  // waves per workgroup: LDS is allocated per wave, not in 4-wave steps
 
 struct FastPrefetch {
     uint32_t lo[kFastLd], hi[kFastLd], sh[kFastLd];
