@@ -54,6 +54,9 @@ CONFIGS = [
     ("small", 320, 240, 300, "gen"),
     ("kitti_init2x", 1241, 376, 4000, "kitti"),
     ("hd1080", 1920, 1080, 4000, "gen"),   # config 5; quadtree levels 0 and 2+ overflow their registers
+    # uniform noise: ~35% of level-0 pixels are FAST corners at minThFAST, so cells outgrow the
+    # 376-entry candidate list and take the whole-window NMS path (csrc/orbx_extract.hip, K2)
+    ("noise640", 640, 480, 1000, "noise"),
 ]
 
 
@@ -61,6 +64,8 @@ def _frames(kind, W, H, n, seed0=1):
     import orbx_synth
     if kind == "kitti":
         return orbx_synth.kitti_sequence(n, start=seed0 * 7)
+    if kind == "noise":
+        return np.random.default_rng(seed0).integers(0, 256, (n, H, W), dtype=np.uint8)
     return np.stack([orbx_synth.gen_image(seed0 + i, W, H) for i in range(n)])
 
 
