@@ -123,8 +123,8 @@ def cpu_baseline_all_cores(frames: np.ndarray, budget_s: float, threads: int = 1
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=192, help="frames per GPU per step")
     ap.add_argument("--pool", type=int, default=4, help="distinct batches resident per GPU (4 x 192 frames = 358 MB > the 256 MB Infinity Cache)")
     ap.add_argument("--streams", type=int, default=3, help="pipeline depth (batches in flight per GPU); "
