@@ -206,7 +206,7 @@ def test_search_for_initialization_contended(orbref, cuda, seed, noise, nproto):
             assert want_n > 0
 
 
-@pytest.mark.parametrize("nq,nt", [(1000, 777), (257, 5000), (10000, 1024)])
+@pytest.mark.parametrize("nq,nt", [(1000, 777), (257, 5000), (10000, 1024), (300, 2056)])
 def test_allpairs(orbref, cuda, nq, nt):
     import torch
     import orbx
@@ -220,9 +220,12 @@ def test_allpairs(orbref, cuda, nq, nt):
     torch.cuda.synchronize()
     # reference: popcount of xor
     x = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=2).sum(axis=2) if nq * nt <= 4_000_000 else None
+    sel = np.arange(0, nq, max(1, nq // 300))
     if x is not None:
         assert np.array_equal(full.cpu().numpy().astype(np.int64), x)
-    sel = np.arange(0, nq, max(1, nq // 300))
+    else:   # sampled rows of the large matrix
+        xs = np.unpackbits(q[sel, None, :] ^ t[None, :, :], axis=2).sum(axis=2)
+        assert np.array_equal(full.cpu().numpy()[sel].astype(np.int64), xs)
     wi, w1, w2 = orbref.allpairs_top2(q[sel], t)
     assert np.array_equal(bi.cpu().numpy()[sel], wi)
     assert np.array_equal(b1.cpu().numpy()[sel], w1)
