@@ -7,8 +7,12 @@
  *
  * Threading: a handle is single-threaded and owns one HIP stream plus its
  * device workspace (one extractor per thread, like the reference's left/right
- * extractors, src/Frame.cc:94-103).  The orbm_* matchers keep no global
- * mutable state and are re-entrant.
+ * extractors, src/Frame.cc:94-103).  The orbm_* matchers are re-entrant and
+ * thread-safe: each synchronous host call runs on a non-blocking stream of its
+ * own with pooled pinned / device buffers (no per-call device allocation, no
+ * device-wide synchronisation), so concurrent callers (Tracking, LocalMapping,
+ * LoopClosing) never wait on each other's or an extractor's stream.  Every
+ * entry point leaves the calling thread's current HIP device as it found it.
  */
 #ifndef ORBX_H
 #define ORBX_H
@@ -179,12 +183,46 @@ orbx_status orbm_stereo_band_device(const orbx_keypoint* d_kps, const uint8_t* d
                                     int nlevels, float min_d, float max_d, int* d_best_idx, int* d_best_dist,
                                     void* stream);
 
-/* ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:417-588) for `npairs`
- * frame pairs (F1 = pair_a[p], F2 = pair_b[p]) of an `nframes` device batch produced by
- * orbx_extract_batch_device (kps/desc/counts, per-frame capacity `cap`).  Grid
- * and window follow Frame::GetFeaturesInArea (src/Frame.cc:410-495) for
- * undistorted rows x cols frames; vbPrevMatched = F1 keypoint positions.
- * Outputs: d_matches12[p*cap + i1] (-1 = none), d_nmatches[p]. */
+/* The Frame grid (Frame's static members, src/Frame.cc:32-33): the image bounds of
+ * Frame::ComputeImageBounds (src/Frame.cc:563-621; 0..cols x 0..rows without distortion, the
+ * undistorted corners otherwise) and the FRAME_GRID_COLS x FRAME_GRID_ROWS = 64 x 48 cells over
+ * them, mfGridElementWidthInv = 64.f / (mnMaxX - mnMinX) and HeightInv = 48.f / (mnMaxY - mnMinY)
+ * in float (src/Frame.cc:127-128). */
+typedef struct {
+    float min_x, min_y;              /* mnMinX, mnMinY */
+    float grid_w_inv, grid_h_inv;    /* mfGridElementWidthInv, mfGridElementHeightInv */
+} orbm_grid;
+
+/* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+ * (src/ORBmatcher.cc:417-588) for `npairs` frame pairs (F1 = pair_a[p], F2 = pair_b[p]) of an
+ * `nframes` device batch in orbx_extract_batch_device's layout (kps/desc/counts, per-frame
+ * capacity `cap`).  The keypoints are the frames' mvKeysUn (the extractor's own output for an
+ * undistorted camera) in extractor order: level 0 first.  Candidates come from
+ * F2.GetFeaturesInArea (src/Frame.cc:410-495) over `grid`.
+ * d_prev_matched: vbPrevMatched per pair, d_prev_matched[(p*cap + i1)*2 + {0,1}] = (x, y), read as
+ * the window centres and updated in place with F2's matched keypoint positions (:580-584), as
+ * Tracking::MonocularInitialization keeps it across attempts (src/Tracking.cc:599-602, 639-644);
+ * NULL = F1's own keypoint positions (the first attempt), not written.
+ * Outputs: d_matches12[p*cap + i1] (-1 = none) and d_nmatches[p] (the return value).
+ * cap <= 32767, and the greedy pass's LDS (about 43 * cap bytes) must fit one workgroup
+ * (ORBX_ENOSPC otherwise).  Asynchronous on `stream`. */
+orbx_status orbm_search_for_initialization_device(const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                                                  const int* d_counts, int nframes, int cap, const int* d_pair_a,
+                                                  const int* d_pair_b, int npairs, const orbm_grid* grid,
+                                                  int window, float nnratio, int check_ori, float* d_prev_matched,
+                                                  int* d_matches12, int* d_nmatches, void* stream);
+
+/* Host path for one (F1, F2) pair (host arrays), on HIP device `device`: kps1/desc1 = F1.mvKeysUn /
+ * mDescriptors (n1), kps2/desc2 = F2's (n2), prev_matched = vbPrevMatched (n1 (x, y) pairs, in/out),
+ * matches12 = vnMatches12 (n1), *nmatches = the return value.  nnratio / check_ori are the
+ * ORBmatcher(nnratio, checkOri) arguments (Tracking uses 0.9, true).  Synchronous. */
+orbx_status orbm_search_for_initialization(int device, const orbx_keypoint* kps1, const uint8_t* desc1, int n1,
+                                           const orbx_keypoint* kps2, const uint8_t* desc2, int n2,
+                                           const orbm_grid* grid, float* prev_matched, int window, float nnratio,
+                                           int check_ori, int* matches12, int* nmatches);
+
+/* The undistorted-camera shorthand of orbm_search_for_initialization_device: bounds 0..cols x
+ * 0..rows and vbPrevMatched = F1's keypoints (the benchmark's replay of consecutive pairs). */
 orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint8_t* d_desc,
                                           const int* d_counts, int nframes, int cap, const int* d_pair_a,
                                           const int* d_pair_b, int npairs, int rows, int cols,

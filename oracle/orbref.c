@@ -754,11 +754,11 @@ static void three_maxima(const int* hist, int* i1, int* i2, int* i3)
 
 int orbref_search_for_initialization(const orbref_keypoint* k1, const uint8_t* d1, int n1,
                                      const orbref_keypoint* k2, const uint8_t* d2, int n2,
-                                     int cols, int rows, float* prev_xy, int* matches12,
-                                     int window, float nnratio, int check_ori)
+                                     float minX, float maxX, float minY, float maxY, float* prev_xy,
+                                     int* matches12, int window, float nnratio, int check_ori)
 {
-    /* Frame::ComputeImageBounds (undistorted) + grid scale, src/Frame.cc:202-209, 614-620 */
-    const float minX = 0.0f, maxX = (float)cols, minY = 0.0f, maxY = (float)rows;
+    /* Frame's static image bounds (Frame::ComputeImageBounds, src/Frame.cc:563-621: 0..cols x 0..rows
+       without distortion, the undistorted corners otherwise) and grid scale (src/Frame.cc:127-128) */
     const float invW = (float)GRID_COLS / (maxX - minX);
     const float invH = (float)GRID_ROWS / (maxY - minY);
 

@@ -128,8 +128,8 @@ int orbref_descriptor_distance(const uint8_t* a, const uint8_t* b);
  * Returns nmatches. */
 int orbref_search_for_initialization(const orbref_keypoint* k1, const uint8_t* d1, int n1,
                                      const orbref_keypoint* k2, const uint8_t* d2, int n2,
-                                     int cols, int rows, float* prev_xy, int* matches12,
-                                     int window, float nnratio, int check_ori);
+                                     float min_x, float max_x, float min_y, float max_y, float* prev_xy,
+                                     int* matches12, int window, float nnratio, int check_ori);
 
 /* a15: Frame::ComputeStereoMatches (src/Frame.cc:630-872) for one rectified stereo
  * pair.  pyrL / pyrR: concatenated level images of the left / right extractor

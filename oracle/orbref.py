@@ -14,6 +14,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liborbref.so")
+_FAITHFUL_PATH = os.path.join(_HERE, "_build", "liborbref_faithful.so")
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -66,7 +67,7 @@ class FeatVec(C.Structure):
 
 
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(_LIB_PATH):
+    if force or not os.path.exists(_LIB_PATH) or not os.path.exists(_FAITHFUL_PATH):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
 
@@ -97,7 +98,8 @@ def lib():
                                      u8p, i32p, u8p, i32p, i32p]
         L.orbref_descriptor_distance.argtypes = [u8p, u8p]
         L.orbref_search_for_initialization.argtypes = [C.c_void_p, u8p, C.c_int, C.c_void_p, u8p, C.c_int,
-                                                       C.c_int, C.c_int, f32p, i32p, C.c_int, C.c_float, C.c_int]
+                                                       C.c_float, C.c_float, C.c_float, C.c_float, f32p, i32p,
+                                                       C.c_int, C.c_float, C.c_int]
         L.orbref_compute_stereo_matches.argtypes = [P(Params), C.c_int, C.c_int, u8p, u8p, C.c_void_p, u8p,
                                                      C.c_int, C.c_void_p, u8p, C.c_int, C.c_float, C.c_float,
                                                      f32p, f32p, i32p]
@@ -206,6 +208,29 @@ def distribute(cands: np.ndarray, w: int, h: int, N: int) -> np.ndarray:
     return out[:n].copy()
 
 
+_faithful = None
+
+
+def distribute_faithful(cands: np.ndarray, w: int, h: int, N: int, tie_mode: int = 0) -> np.ndarray:
+    """DistributeOctTree with the reference's std::list nodes and (size, ExtractorNode*) sort
+    (oracle/orbref_faithful.cpp): size ties broken by heap address, as in the reference process
+    (tie_mode 0), or by creation order (tie_mode 1, which must equal distribute())."""
+    global _faithful
+    if _faithful is None:
+        build()
+        _faithful = C.CDLL(_FAITHFUL_PATH)
+        i32p = C.POINTER(C.c_int)
+        _faithful.orbref_distribute_faithful.argtypes = [i32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                         C.c_int, i32p, C.c_int]
+    cands = np.ascontiguousarray(cands, dtype=np.int32)
+    cap = len(cands) + 8
+    out = np.empty(cap, np.int32)
+    n = _faithful.orbref_distribute_faithful(_i32(cands), len(cands), 16, w - 16, 16, h - 16, N, tie_mode, _i32(out),
+                                             cap)
+    assert n >= 0
+    return out[:n].copy()
+
+
 def fast_atan2(y: float, x: float) -> float:
     return lib().orbref_fast_atan2(y, x)
 
@@ -271,7 +296,10 @@ def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
 
 
 def search_for_initialization(kps1, desc1, kps2, desc2, cols, rows, window=100, nnratio=0.9, check_ori=True,
-                              prev_xy=None):
+                              prev_xy=None, bounds=None):
+    """ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:417-588).  bounds = (mnMinX, mnMaxX, mnMinY,
+    mnMaxY) (default 0..cols x 0..rows); prev_xy = vbPrevMatched (n1, 2) (default F1's keypoints).
+    Returns (nmatches, vnMatches12, updated vbPrevMatched)."""
     kps1 = np.ascontiguousarray(kps1, KEYPOINT_DTYPE)
     kps2 = np.ascontiguousarray(kps2, KEYPOINT_DTYPE)
     desc1 = np.ascontiguousarray(desc1, np.uint8)
@@ -281,9 +309,11 @@ def search_for_initialization(kps1, desc1, kps2, desc2, cols, rows, window=100, 
         prev_xy = np.stack([kps1["x"], kps1["y"]], axis=1).astype(np.float32)
     prev_xy = np.ascontiguousarray(prev_xy, np.float32).copy()
     m12 = np.full(max(n1, 1), -1, np.int32)
+    if bounds is None:
+        bounds = (0.0, float(cols), 0.0, float(rows))
     nm = lib().orbref_search_for_initialization(kps1.ctypes.data, _u8(desc1), n1, kps2.ctypes.data, _u8(desc2),
-                                                n2, cols, rows, _f32(prev_xy), _i32(m12), window, nnratio,
-                                                1 if check_ori else 0)
+                                                n2, *[float(np.float32(b)) for b in bounds], _f32(prev_xy),
+                                                _i32(m12), window, nnratio, 1 if check_ori else 0)
     return nm, m12[:n1].copy(), prev_xy
 
 

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/orbx.h"
+#include "orbx_host.hpp"
 #include "orbx_kernels.hpp"
 
 using namespace orbx;
@@ -148,6 +149,9 @@ struct orbx_handle {
     uint8_t* d_desc = nullptr;
     int* d_counts = nullptr;
     int single_cap = 0;
+    uint8_t* h_pin = nullptr;   // pinned staging: image in, count + keypoints + descriptors out
+    int* h_status = nullptr;    // pinned status word (a pageable D2H copy can stall on other streams' work)
+    size_t pin_bytes = 0;
 
     // last batch (for pyramid / debug readback)
     FramePtrs last{};
@@ -162,6 +166,23 @@ struct orbx_handle {
 };
 
 namespace {
+
+// The handle's own stream serves the synchronous host paths only.  It is created on
+// first use: device-batch users bring their own streams, and every idle stream would
+// still take one of the process's few hardware queues (GPU_MAX_HW_QUEUES).  HIP maps streams
+// onto those queues round-robin, and streams that share a queue run in order, so a host call
+// could wait behind an unrelated kernel of the application's.  High-priority streams get
+// queues of their own, apart from the application's default-priority streams (measured:
+// tests/test_gpu_threads.py); the host matchers' streams are high-priority too (orbx_host.hip).
+hipStream_t own_stream(orbx_handle* h)
+{
+    if (!h->stream) {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+        hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi);
+    }
+    return h->stream;
+}
 
 orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
 {
@@ -263,14 +284,16 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     g.spill_per_frame = std::max(spill, 1);
     if (lcap >= 65535 || quadtree_smem_bytes(g) > 160 * 1024) return ORBX_EINVAL;
 
-    hipSetDevice(h->device);
+    // once per image size: the tables go up on the handle's own stream (never the legacy null stream)
     if (!dalloc(h->d_geom, 1) || !dalloc(h->d_cells, cells.size()) || !dalloc(h->d_xtab, xt.size()) ||
         !dalloc(h->d_ytab, yt.size()))
         return ORBX_ENOMEM;
-    hipMemcpy(h->d_geom, &g, sizeof(g), hipMemcpyHostToDevice);
-    hipMemcpy(h->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice);
-    if (!xt.empty()) hipMemcpy(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice);
-    if (!yt.empty()) hipMemcpy(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice);
+    hipStream_t s = own_stream(h);
+    hipMemcpyAsync(h->d_geom, &g, sizeof(g), hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(h->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice, s);
+    if (!xt.empty()) hipMemcpyAsync(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice, s);
+    if (!yt.empty()) hipMemcpyAsync(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice, s);
+    if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
     h->geom = g;
     h->cells = std::move(cells);
     h->grows = rows;
@@ -346,21 +369,16 @@ orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_key
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
-// The handle's own stream serves the synchronous host paths only.  It is created on
-// first use: device-batch users bring their own streams, and every idle stream would
-// still take one of the process's few hardware queues (GPU_MAX_HW_QUEUES).
-hipStream_t own_stream(orbx_handle* h)
-{
-    if (!h->stream) hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-    return h->stream;
-}
-
 orbx_status status_from_device(orbx_handle* h, hipStream_t s)
 {
-    int st = 0;
-    if (hipMemcpyAsync(&st, h->d_status, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
+    if (!h->h_status && hipHostMalloc((void**)&h->h_status, 64, hipHostMallocDefault) != hipSuccess) {
+        h->h_status = nullptr;
+        return ORBX_ENOMEM;
+    }
+    if (hipMemcpyAsync(h->h_status, h->d_status, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
         return ORBX_EDEVICE;
     if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    const int st = *h->h_status;
     if (st & kStatusCapOverflow) return ORBX_ENOSPC;
     if (st) return ORBX_EDEVICE;
     return ORBX_OK;
@@ -387,7 +405,6 @@ orbx_status orbx_create(const orbx_params* params, int device, orbx_handle** out
         return ORBX_EDEVICE;
     }
     h->device = device;
-    hipSetDevice(device);
     h->h_levels.resize(kMaxLevels);
     h->level_cached.assign(kMaxLevels, false);
     *out = h;
@@ -397,8 +414,10 @@ orbx_status orbx_create(const orbx_params* params, int device, orbx_handle** out
 void orbx_destroy(orbx_handle* h)
 {
     if (!h) return;
-    hipSetDevice(h->device);
+    DeviceGuard guard(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->h_pin) hipHostFree(h->h_pin);
+    if (h->h_status) hipHostFree(h->h_status);
     dfree(h->d_geom);
     dfree(h->d_cells);
     dfree(h->d_xtab);
@@ -442,6 +461,7 @@ int orbx_capacity(const orbx_handle* h, int rows, int cols)
 {
     if (!h) return -1;
     orbx_handle* m = const_cast<orbx_handle*>(h);
+    DeviceGuard guard(m->device);
     if (ensure_geometry(m, rows, cols) != ORBX_OK) return -1;
     return m->geom.out_per_frame;
 }
@@ -452,7 +472,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     if (!h || !n_out) return ORBX_EINVAL;
     if (!img || rows <= 0 || cols <= 0) return ORBX_EMPTY;   // src/ORBextractor.cc:1252
     if (step < (size_t)cols || !kps || !desc || cap < 0) return ORBX_EINVAL;
-    hipSetDevice(h->device);
+    DeviceGuard guard(h->device);
     orbx_status st = ensure_geometry(h, rows, cols);
     if (st != ORBX_OK) return st;
     if ((st = ensure_batch(h, 1)) != ORBX_OK) return st;
@@ -468,19 +488,34 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
             return ORBX_ENOMEM;
         h->single_cap = ocap;
     }
+    // pinned staging: [image rows x cols][count][keypoints ocap][descriptors ocap x 32]
+    const size_t img_b = ((size_t)rows * cols + 63) & ~(size_t)63;
+    const size_t kp_off = img_b + 64, ds_off = kp_off + (((size_t)ocap * sizeof(orbx_keypoint) + 63) & ~(size_t)63);
+    const size_t pin_need = ds_off + (size_t)ocap * 32;
+    if (pin_need > h->pin_bytes) {
+        if (h->h_pin) hipHostFree(h->h_pin);
+        h->h_pin = nullptr;
+        h->pin_bytes = 0;
+        if (hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
+        h->pin_bytes = pin_need;
+    }
+    for (int r = 0; r < rows; ++r) std::memcpy(h->h_pin + (size_t)r * cols, img + (size_t)r * step, (size_t)cols);
     hipStream_t s = own_stream(h);
-    hipMemcpy2DAsync(h->d_img, pitch, img, step, cols, rows, hipMemcpyHostToDevice, s);
+    hipMemcpy2DAsync(h->d_img, pitch, h->h_pin, cols, cols, rows, hipMemcpyHostToDevice, s);
     FramePtrs P{h->d_img, need, pitch, h->d_pyr, (size_t)h->geom.pyr_bytes};
     st = run_pipeline(h, P, 1, h->d_kps, h->d_desc, h->d_counts, ocap, s);
     if (st != ORBX_OK) return st;
-    int n = 0;
-    hipMemcpyAsync(&n, h->d_counts, sizeof(int), hipMemcpyDeviceToHost, s);
+    // one round trip: count, status and the whole output capacity come back together
+    int* pc = (int*)(h->h_pin + img_b);
+    hipMemcpyAsync(pc, h->d_counts, sizeof(int), hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(h->h_pin + kp_off, h->d_kps, sizeof(orbx_keypoint) * (size_t)ocap, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(h->h_pin + ds_off, h->d_desc, (size_t)ocap * 32, hipMemcpyDeviceToHost, s);
     if ((st = status_from_device(h, s)) != ORBX_OK) return st;
+    const int n = *pc;
     if (n > cap) return ORBX_ENOSPC;
     if (n > 0) {
-        hipMemcpyAsync(kps, h->d_kps, sizeof(orbx_keypoint) * n, hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(desc, h->d_desc, (size_t)n * 32, hipMemcpyDeviceToHost, s);
-        if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+        std::memcpy(kps, h->h_pin + kp_off, sizeof(orbx_keypoint) * (size_t)n);
+        std::memcpy(desc, h->h_pin + ds_off, (size_t)n * 32);
     }
     *n_out = n;
     return ORBX_OK;
@@ -489,6 +524,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
 orbx_status orbx_get_level(orbx_handle* h, int level, const uint8_t** data, int* rows, int* cols, size_t* step)
 {
     if (!h || !h->geom_ok || h->last_batch <= 0 || level < 0 || level >= h->geom.nlevels) return ORBX_EINVAL;
+    DeviceGuard guard(h->device);
     const LevelGeom& L = h->geom.lv[level];
     if (!h->level_cached[level]) {
         std::vector<uint8_t>& v = h->h_levels[level];
@@ -520,7 +556,7 @@ orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int
 {
     if (!h || !d_imgs || batch <= 0 || !d_kps || !d_desc || !d_counts || cap <= 0) return ORBX_EINVAL;
     if (step < (size_t)cols || frame_stride < step * (size_t)rows) return ORBX_EINVAL;
-    hipSetDevice(h->device);
+    DeviceGuard guard(h->device);
     orbx_status st = ensure_geometry(h, rows, cols);
     if (st != ORBX_OK) return st;
     if ((st = ensure_batch(h, batch)) != ORBX_OK) return st;
@@ -532,7 +568,7 @@ orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int
 orbx_status orbx_sync(orbx_handle* h, void* stream)
 {
     if (!h) return ORBX_EINVAL;
-    hipSetDevice(h->device);
+    DeviceGuard guard(h->device);
     if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return ORBX_EDEVICE;
     if (!h->d_status) return ORBX_OK;
     return status_from_device(h, (hipStream_t)stream);
@@ -565,7 +601,7 @@ orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n)
 orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t out_size)
 {
     if (!h || !out || frame < 0 || frame >= h->last_batch) return ORBX_EINVAL;
-    hipSetDevice(h->device);
+    DeviceGuard guard(h->device);
     size_t o = 0;
     for (int l = 0; l < h->geom.nlevels; ++l) {
         const LevelGeom& L = h->geom.lv[l];
@@ -588,7 +624,7 @@ orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t o
 orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys, int cap, int* n)
 {
     if (!h || !n || frame < 0 || frame >= h->last_batch || level < 0 || level >= h->geom.nlevels) return ORBX_EINVAL;
-    hipSetDevice(h->device);
+    DeviceGuard guard(h->device);
     const Geometry& g = h->geom;
     std::vector<int> cnt(g.ncells);
     std::vector<uint32_t> sl(g.slots_per_frame);
@@ -657,25 +693,24 @@ orbx_status orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, c
         return ORBX_EINVAL;
     const int cap = std::max(n_l, n_r);
     if (cap > 32767) return ORBX_EINVAL;
-    hipSetDevice(left->device);
-    hipStream_t s = own_stream(left);
-    const size_t kb = sizeof(orbx_keypoint) * 2 * (size_t)cap, db = (size_t)64 * cap;
-    const size_t ob = sizeof(float) * (size_t)cap;
-    uint8_t* buf = nullptr;
-    const size_t total = kb + db + 3 * ob + 64;
-    if (hipMallocAsync((void**)&buf, total, s) != hipSuccess) return ORBX_ENOMEM;
-    orbx_keypoint* dk = (orbx_keypoint*)buf;
-    uint8_t* dd = buf + kb;
-    float* du = (float*)(dd + db);
-    float* dz = du + cap;
-    int* dsad = (int*)(dz + cap);
-    int* meta = (int*)(buf + kb + db + 3 * ob);   // counts[2], fl, fr, ngood
-    const int hmeta[5] = {n_l, n_r, 0, 1, 0};
-    hipMemcpyAsync(dk, kps_l, sizeof(orbx_keypoint) * n_l, hipMemcpyHostToDevice, s);
-    if (n_r > 0) hipMemcpyAsync(dk + cap, kps_r, sizeof(orbx_keypoint) * n_r, hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(dd, desc_l, (size_t)32 * n_l, hipMemcpyHostToDevice, s);
-    if (n_r > 0) hipMemcpyAsync(dd + (size_t)32 * cap, desc_r, (size_t)32 * n_r, hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(meta, hmeta, sizeof(hmeta), hipMemcpyHostToDevice, s);
+    HostCall c(left->device);
+    const int hmeta[5] = {n_l, n_r, 0, 1, 0};   // counts[2], fl, fr, ngood
+    const size_t om = c.in(hmeta, sizeof(hmeta));
+    // the kernels address frame f's keypoints at kps + f * cap: left rows at 0, right rows at cap
+    const size_t ok = c.in(nullptr, sizeof(orbx_keypoint) * 2 * (size_t)cap);
+    const size_t od = c.in(nullptr, (size_t)64 * cap);
+    const size_t ou = c.out(sizeof(float) * (size_t)cap), oz = c.out(sizeof(float) * (size_t)cap);
+    const size_t osad = c.out(sizeof(int) * (size_t)cap);
+    orbx_status st = c.prepare();
+    if (st != ORBX_OK) return st;
+    uint8_t* hk = c.host(ok);
+    uint8_t* hd = c.host(od);
+    if (!hk || !hd) return ORBX_ENOMEM;
+    std::memcpy(hk, kps_l, sizeof(orbx_keypoint) * (size_t)n_l);
+    if (n_r > 0) std::memcpy(hk + sizeof(orbx_keypoint) * (size_t)cap, kps_r, sizeof(orbx_keypoint) * (size_t)n_r);
+    std::memcpy(hd, desc_l, (size_t)32 * n_l);
+    if (n_r > 0) std::memcpy(hd + (size_t)32 * cap, desc_r, (size_t)32 * n_r);
+    if ((st = c.upload()) != ORBX_OK) return st;
     // single images: frame strides 0, so frame indices 0 / 1 both address the handle's image
     FramePtrs PL = left->last, PR = right->last;
     PL.in_fstride = PL.pyr_fstride = 0;
@@ -683,17 +718,18 @@ orbx_status orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, c
     float maxD;
     int rband;
     stereo_limits(left, bf, fx, &maxD, &rband);
-    launch_stereo(left->geom, left->d_geom, PL, PR, dk, dd, meta, cap, meta + 2, meta + 3, 1, bf, maxD, rband, du, dz,
-                  dsad, meta + 4, s);
-    orbx_status st = hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+    int* meta = c.dev_as<int>(om);
+    launch_stereo(left->geom, left->d_geom, PL, PR, c.dev_as<orbx_keypoint>(ok), c.dev(od), meta, cap, meta + 2,
+                  meta + 3, 1, bf, maxD, rband, c.dev_as<float>(ou), c.dev_as<float>(oz), c.dev_as<int>(osad),
+                  meta + 4, c.stream());
+    if (hipGetLastError() != hipSuccess) return ORBX_EDEVICE;
     int ng = 0;
-    hipMemcpyAsync(u_right, du, sizeof(float) * n_l, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(depth, dz, sizeof(float) * n_l, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(&ng, meta + 4, sizeof(int), hipMemcpyDeviceToHost, s);
-    hipFreeAsync(buf, s);
-    if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    c.fetch(ou, u_right, sizeof(float) * (size_t)n_l);
+    c.fetch(oz, depth, sizeof(float) * (size_t)n_l);
+    c.fetch(om + 16, &ng, sizeof(int));
+    if ((st = c.finish()) != ORBX_OK) return st;
     *n_good = ng;
-    return st;
+    return ORBX_OK;
 }
 
 orbx_status orbx_stereo_batch_device(orbx_handle* h, const orbx_keypoint* d_kps, const uint8_t* d_desc,
@@ -706,7 +742,7 @@ orbx_status orbx_stereo_batch_device(orbx_handle* h, const orbx_keypoint* d_kps,
         return ORBX_EINVAL;
     if (!h->geom_ok || h->last_batch <= 0) return ORBX_EINVAL;
     if (npairs == 0) return ORBX_OK;
-    hipSetDevice(h->device);
+    DeviceGuard guard(h->device);
     hipStream_t s = (hipStream_t)stream;
     int* dsad = nullptr;
     if (hipMallocAsync((void**)&dsad, sizeof(int) * (size_t)npairs * cap, s) != hipSuccess) return ORBX_ENOMEM;
@@ -741,18 +777,6 @@ orbx_status orbm_bow_search_device(int mode, const orbm_bow_view* d_view1, const
 
 namespace {
 
-// host view -> bytes staged in one device buffer; returns the device view
-struct BowStage {
-    std::vector<uint8_t> host;
-    size_t add(const void* p, size_t bytes)
-    {
-        const size_t o = (host.size() + 15) & ~(size_t)15;
-        host.resize(o + bytes);
-        if (bytes && p) std::memcpy(host.data() + o, p, bytes);
-        return o;
-    }
-};
-
 bool bow_view_ok(const orbm_bow_view* v)
 {
     if (!v || v->n < 0 || v->fv_nnodes < 0 || v->n > 8192) return false;
@@ -766,24 +790,24 @@ bool bow_view_ok(const orbm_bow_view* v)
     return v->fv_nnodes == 0 || v->fv_ptr[0] == 0;
 }
 
-// offsets of one staged view (device pointers are patched in after the upload)
+// offsets of one staged view (device pointers are patched in after the buffers are sized)
 struct BowOffs {
     size_t kps, desc, mp, ur, node, ptr, idx;
     bool has_mp, has_ur;
 };
 
-BowOffs bow_stage(BowStage& st, const orbm_bow_view* v)
+BowOffs bow_stage(HostCall& c, const orbm_bow_view* v)
 {
     BowOffs o;
-    o.kps = st.add(v->kps, sizeof(orbx_keypoint) * (size_t)v->n);
-    o.desc = st.add(v->desc, (size_t)32 * v->n);
+    o.kps = c.in(v->kps, sizeof(orbx_keypoint) * (size_t)v->n);
+    o.desc = c.in(v->desc, (size_t)32 * v->n);
     o.has_mp = v->has_mp != nullptr;
     o.has_ur = v->u_right != nullptr;
-    o.mp = o.has_mp ? st.add(v->has_mp, (size_t)v->n) : 0;
-    o.ur = o.has_ur ? st.add(v->u_right, sizeof(float) * (size_t)v->n) : 0;
-    o.node = st.add(v->fv_node, sizeof(int32_t) * (size_t)v->fv_nnodes);
-    o.ptr = st.add(v->fv_ptr, sizeof(int32_t) * ((size_t)v->fv_nnodes + 1));
-    o.idx = st.add(v->fv_idx, sizeof(int32_t) * (size_t)(v->fv_nnodes ? v->fv_ptr[v->fv_nnodes] : 0));
+    o.mp = o.has_mp ? c.in(v->has_mp, (size_t)v->n) : 0;
+    o.ur = o.has_ur ? c.in(v->u_right, sizeof(float) * (size_t)v->n) : 0;
+    o.node = c.in(v->fv_node, sizeof(int32_t) * (size_t)v->fv_nnodes);
+    o.ptr = c.in(v->fv_ptr, sizeof(int32_t) * ((size_t)v->fv_nnodes + 1));
+    o.idx = c.in(v->fv_idx, sizeof(int32_t) * (size_t)(v->fv_nnodes ? v->fv_ptr[v->fv_nnodes] : 0));
     return o;
 }
 
@@ -814,32 +838,27 @@ orbx_status orbm_bow_search(int device, int mode, const orbm_bow_view* view1, co
     if (nout > 0 && !match) return ORBX_EINVAL;
     *nmatches = 0;
     if (nout == 0) return ORBX_OK;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
-    hipSetDevice(device);
-    BowStage st;
-    const BowOffs o1 = bow_stage(st, view1), o2 = bow_stage(st, view2);
-    const size_t ov = st.add(nullptr, 2 * sizeof(orbm_bow_view) + sizeof(orbm_triang_params));
-    const size_t om = st.add(nullptr, sizeof(int) * ((size_t)nout + 1));
-    uint8_t* d = nullptr;
-    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
-    orbm_bow_view dv[2] = {bow_device_view(d, o1, view1), bow_device_view(d, o2, view2)};
-    std::memcpy(st.host.data() + ov, dv, sizeof(dv));
-    if (tp) std::memcpy(st.host.data() + ov + sizeof(dv), tp, sizeof(*tp));
-    orbx_status rc = ORBX_OK;
-    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
-    if (rc == ORBX_OK) {
-        const orbm_bow_view* d1 = (const orbm_bow_view*)(d + ov);
-        const orbm_triang_params* dtp = (const orbm_triang_params*)(d + ov + sizeof(dv));
-        int* dm = (int*)(d + om);
-        rc = orbm_bow_search_device(mode, d1, d1 + 1, dtp, 1, view1->fv_nnodes, nnratio, check_ori, dm + 1, nout, dm,
-                                    nullptr);
-        if (rc == ORBX_OK && (hipMemcpy(match, dm + 1, sizeof(int) * (size_t)nout, hipMemcpyDeviceToHost) != hipSuccess ||
-                              hipMemcpy(nmatches, dm, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess))
-            rc = ORBX_EDEVICE;
-    }
-    hipFree(d);
-    return rc;
+    HostCall c(device);
+    // the two device view structs (+ tp) first: they are patched after the buffers are sized
+    const size_t ov = c.in(nullptr, 2 * sizeof(orbm_bow_view) + sizeof(orbm_triang_params));
+    const BowOffs o1 = bow_stage(c, view1), o2 = bow_stage(c, view2);
+    const size_t om = c.out(sizeof(int) * ((size_t)nout + 1));
+    orbx_status rc = c.prepare();
+    if (rc != ORBX_OK) return rc;
+    uint8_t* base = c.dev(0);
+    orbm_bow_view dv[2] = {bow_device_view(base, o1, view1), bow_device_view(base, o2, view2)};
+    std::memcpy(c.host(ov), dv, sizeof(dv));
+    if (tp) std::memcpy(c.host(ov) + sizeof(dv), tp, sizeof(*tp));
+    if ((rc = c.upload()) != ORBX_OK) return rc;
+    const orbm_bow_view* d1 = c.dev_as<const orbm_bow_view>(ov);
+    const orbm_triang_params* dtp = (const orbm_triang_params*)(c.dev(ov) + sizeof(dv));
+    int* dm = c.dev_as<int>(om);
+    rc = orbm_bow_search_device(mode, d1, d1 + 1, dtp, 1, view1->fv_nnodes, nnratio, check_ori, dm + 1, nout, dm,
+                                c.stream());
+    if (rc != ORBX_OK) return rc;
+    c.fetch(om + sizeof(int), match, sizeof(int) * (size_t)nout);
+    c.fetch(om, nmatches, sizeof(int));
+    return c.finish();
 }
 
 orbx_status orbm_search_by_projection_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const float* d_uright,
@@ -873,34 +892,28 @@ orbx_status orbm_search_by_projection(int device, const orbx_keypoint* kps, cons
         if ((pts[i].flags & 1) && (pts[i].level < 0 || pts[i].level >= 16)) return ORBX_EINVAL;
     for (int i = 0; i < n; ++i) match[i] = -1;
     if (np == 0) return ORBX_OK;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
-    hipSetDevice(device);
-    BowStage st;
-    const size_t ok = st.add(kps, sizeof(orbx_keypoint) * (size_t)n);
-    const size_t od = st.add(desc, (size_t)32 * n);
-    const size_t ou = st.add(uright, sizeof(float) * (size_t)n);
-    const size_t oc = st.add(claimed, (size_t)n);
-    const size_t op = st.add(pts, sizeof(orbm_proj_point) * (size_t)np);
-    const size_t opd = st.add(pdesc, (size_t)32 * np);
+    HostCall c(device);
     const int cn[2] = {n, np};
-    const size_t ocn = st.add(cn, sizeof(cn));
-    const size_t om = st.add(nullptr, sizeof(int) * ((size_t)n + 1));
-    uint8_t* d = nullptr;
-    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
-    orbx_status rc = ORBX_OK;
-    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
-    if (rc == ORBX_OK) {
-        int* dm = (int*)(d + om);
-        rc = orbm_search_by_projection_device((const orbx_keypoint*)(d + ok), d + od, (const float*)(d + ou), d + oc,
-                                              (const int*)(d + ocn), 1, n, (const orbm_proj_point*)(d + op), d + opd,
-                                              (const int*)(d + ocn) + 1, np, params, dm + 1, dm, nullptr);
-        if (rc == ORBX_OK && (hipMemcpy(match, dm + 1, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
-                              hipMemcpy(nmatches, dm, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess))
-            rc = ORBX_EDEVICE;
-    }
-    hipFree(d);
-    return rc;
+    const size_t ocn = c.in(cn, sizeof(cn));
+    const size_t ok = c.in(kps, sizeof(orbx_keypoint) * (size_t)n);
+    const size_t od = c.in(desc, (size_t)32 * n);
+    const size_t ou = c.in(uright, sizeof(float) * (size_t)n);
+    const size_t oc = c.in(claimed, (size_t)n);
+    const size_t op = c.in(pts, sizeof(orbm_proj_point) * (size_t)np);
+    const size_t opd = c.in(pdesc, (size_t)32 * np);
+    const size_t om = c.out(sizeof(int) * ((size_t)n + 1));
+    orbx_status rc = c.prepare();
+    if (rc == ORBX_OK) rc = c.upload();
+    if (rc != ORBX_OK) return rc;
+    int* dm = c.dev_as<int>(om);
+    const int* dcn = c.dev_as<const int>(ocn);
+    rc = orbm_search_by_projection_device(c.dev_as<const orbx_keypoint>(ok), c.dev(od), c.dev_as<const float>(ou),
+                                          c.dev(oc), dcn, 1, n, c.dev_as<const orbm_proj_point>(op), c.dev(opd),
+                                          dcn + 1, np, params, dm + 1, dm, c.stream());
+    if (rc != ORBX_OK) return rc;
+    c.fetch(om + sizeof(int), match, sizeof(int) * (size_t)n);
+    c.fetch(om, nmatches, sizeof(int));
+    return c.finish();
 }
 
 orbx_status orbm_project_search_device(int mode, const orbx_keypoint* d_kps, const uint8_t* d_desc,
@@ -944,36 +957,30 @@ orbx_status orbm_project_search(int device, int mode, const orbx_keypoint* kps, 
             if ((pts[i].flags & 1) && (pts[i].octave < 0 || pts[i].octave >= 16)) return ORBX_EINVAL;
     for (int i = 0; i < nout; ++i) match[i] = -1;
     if (n == 0 || np == 0) return ORBX_OK;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
-    hipSetDevice(device);
-    BowStage st;
-    const size_t ok = st.add(kps, sizeof(orbx_keypoint) * (size_t)n);
-    const size_t od = st.add(desc, (size_t)32 * n);
-    const size_t ou = st.add(uright, sizeof(float) * (size_t)n);
-    const size_t oc = st.add(search ? claimed : nullptr, (size_t)n);
-    const size_t opo = st.add(pose, sizeof(float) * 24);
-    const size_t op = st.add(pts, sizeof(orbm_map_point) * (size_t)np);
-    const size_t opd = st.add(pdesc, (size_t)32 * np);
+    HostCall c(device);
     const int cn[2] = {n, np};
-    const size_t ocn = st.add(cn, sizeof(cn));
-    const size_t om = st.add(nullptr, sizeof(int) * ((size_t)nout + 1));
-    uint8_t* d = nullptr;
-    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
-    orbx_status rc = ORBX_OK;
-    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
-    if (rc == ORBX_OK) {
-        int* dm = (int*)(d + om);
-        rc = orbm_project_search_device(mode, (const orbx_keypoint*)(d + ok), d + od, (const float*)(d + ou), d + oc,
-                                        (const int*)(d + ocn), 1, n, (const float*)(d + opo),
-                                        (const orbm_map_point*)(d + op), d + opd, (const int*)(d + ocn) + 1, np,
-                                        params, dm + 1, dm, nullptr);
-        if (rc == ORBX_OK && (hipMemcpy(match, dm + 1, sizeof(int) * (size_t)nout, hipMemcpyDeviceToHost) != hipSuccess ||
-                              hipMemcpy(nmatches, dm, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess))
-            rc = ORBX_EDEVICE;
-    }
-    hipFree(d);
-    return rc;
+    const size_t ocn = c.in(cn, sizeof(cn));
+    const size_t opo = c.in(pose, sizeof(float) * 24);
+    const size_t ok = c.in(kps, sizeof(orbx_keypoint) * (size_t)n);
+    const size_t od = c.in(desc, (size_t)32 * n);
+    const size_t ou = c.in(uright, sizeof(float) * (size_t)n);
+    const size_t oc = c.in(search ? claimed : nullptr, (size_t)n);
+    const size_t op = c.in(pts, sizeof(orbm_map_point) * (size_t)np);
+    const size_t opd = c.in(pdesc, (size_t)32 * np);
+    const size_t om = c.out(sizeof(int) * ((size_t)nout + 1));
+    orbx_status rc = c.prepare();
+    if (rc == ORBX_OK) rc = c.upload();
+    if (rc != ORBX_OK) return rc;
+    int* dm = c.dev_as<int>(om);
+    const int* dcn = c.dev_as<const int>(ocn);
+    rc = orbm_project_search_device(mode, c.dev_as<const orbx_keypoint>(ok), c.dev(od), c.dev_as<const float>(ou),
+                                    c.dev(oc), dcn, 1, n, c.dev_as<const float>(opo),
+                                    c.dev_as<const orbm_map_point>(op), c.dev(opd), dcn + 1, np, params, dm + 1, dm,
+                                    c.stream());
+    if (rc != ORBX_OK) return rc;
+    c.fetch(om + sizeof(int), match, sizeof(int) * (size_t)nout);
+    c.fetch(om, nmatches, sizeof(int));
+    return c.finish();
 }
 
 orbx_status orbx_ingest_batch_device(const uint8_t* d_src, int batch, int rows, int cols, int channels, int rgb,
@@ -1033,31 +1040,25 @@ orbx_status orbm_best2_csr(int device, const uint8_t* q, int nq, const uint8_t* 
     if (cand_ptr[0] != 0 || ncand < 0 || (ncand > 0 && (!cand_idx || !t))) return ORBX_EINVAL;
     for (int i = 0; i < nq; ++i)
         if (cand_ptr[i + 1] < cand_ptr[i]) return ORBX_EINVAL;
-    for (int c = 0; c < ncand; ++c)
-        if (cand_idx[c] < 0 || cand_idx[c] >= nt) return ORBX_EINVAL;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
-    hipSetDevice(device);
-    BowStage st;
-    const size_t oq = st.add(q, (size_t)32 * nq);
-    const size_t ot = st.add(t, (size_t)32 * nt);
-    const size_t op = st.add(cand_ptr, sizeof(int) * ((size_t)nq + 1));
-    const size_t oi = st.add(cand_idx, sizeof(int) * (size_t)ncand);
-    const size_t oo = st.add(nullptr, sizeof(int) * 3 * (size_t)nq);
-    uint8_t* d = nullptr;
-    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
-    orbx_status rc = ORBX_OK;
-    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
-    int* o = (int*)(d + oo);
-    if (rc == ORBX_OK)
-        rc = orbm_best2_csr_device(d + oq, nq, d + ot, nt, (const int*)(d + op), (const int*)(d + oi), tie_mode, o,
-                                   o + nq, o + 2 * nq, nullptr);
-    if (rc == ORBX_OK && (hipMemcpy(best_idx, o, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
-                          hipMemcpy(best, o + nq, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
-                          hipMemcpy(second, o + 2 * nq, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess))
-        rc = ORBX_EDEVICE;
-    hipFree(d);
-    return rc;
+    for (int k = 0; k < ncand; ++k)
+        if (cand_idx[k] < 0 || cand_idx[k] >= nt) return ORBX_EINVAL;
+    HostCall c(device);
+    const size_t oq = c.in(q, (size_t)32 * nq);
+    const size_t ot = c.in(t, (size_t)32 * nt);
+    const size_t op = c.in(cand_ptr, sizeof(int) * ((size_t)nq + 1));
+    const size_t oi = c.in(cand_idx, sizeof(int) * (size_t)ncand);
+    const size_t oo = c.out(sizeof(int) * 3 * (size_t)nq);
+    orbx_status rc = c.prepare();
+    if (rc == ORBX_OK) rc = c.upload();
+    if (rc != ORBX_OK) return rc;
+    int* o = c.dev_as<int>(oo);
+    rc = orbm_best2_csr_device(c.dev(oq), nq, c.dev(ot), nt, c.dev_as<const int>(op), c.dev_as<const int>(oi),
+                               tie_mode, o, o + nq, o + 2 * nq, c.stream());
+    if (rc != ORBX_OK) return rc;
+    c.fetch(oo, best_idx, sizeof(int) * (size_t)nq);
+    c.fetch(oo + sizeof(int) * (size_t)nq, best, sizeof(int) * (size_t)nq);
+    c.fetch(oo + sizeof(int) * 2 * (size_t)nq, second, sizeof(int) * (size_t)nq);
+    return c.finish();
 }
 
 orbx_status orbm_stereo_band_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const int* d_counts, int cap,
@@ -1099,33 +1100,30 @@ orbx_status orbm_stereo_band(int device, const orbx_keypoint* kps_l, const uint8
         if (kps_r[i].octave < 0 || kps_r[i].octave >= nlevels) return ORBX_EINVAL;
     const int cap = std::max(n_l, n_r);
     if (stereo_band_smem(rows, cap) > 160 * 1024) return ORBX_ENOSPC;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
-    hipSetDevice(device);
-    BowStage st;
-    const size_t ok = st.add(nullptr, sizeof(orbx_keypoint) * 2 * (size_t)cap);
-    std::memcpy(st.host.data() + ok, kps_l, sizeof(orbx_keypoint) * (size_t)n_l);
-    if (n_r) std::memcpy(st.host.data() + ok + sizeof(orbx_keypoint) * (size_t)cap, kps_r, sizeof(orbx_keypoint) * n_r);
-    const size_t od = st.add(nullptr, (size_t)64 * cap);
-    std::memcpy(st.host.data() + od, desc_l, (size_t)32 * n_l);
-    if (n_r) std::memcpy(st.host.data() + od + (size_t)32 * cap, desc_r, (size_t)32 * n_r);
+    HostCall c(device);
     const int meta[4] = {n_l, n_r, 0, 1};   // counts[2], left frame, right frame
-    const size_t om = st.add(meta, sizeof(meta));
-    const size_t oo = st.add(nullptr, sizeof(int) * 2 * (size_t)cap);
-    uint8_t* d = nullptr;
-    if (hipMalloc((void**)&d, st.host.size()) != hipSuccess) return ORBX_ENOMEM;
-    orbx_status rc = ORBX_OK;
-    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
-    const int* m = (const int*)(d + om);
-    int* o = (int*)(d + oo);
-    if (rc == ORBX_OK)
-        rc = orbm_stereo_band_device((const orbx_keypoint*)(d + ok), d + od, m, cap, m + 2, m + 3, 1, rows, scale,
-                                     nlevels, min_d, max_d, o, o + cap, nullptr);
-    if (rc == ORBX_OK && (hipMemcpy(best_idx, o, sizeof(int) * (size_t)n_l, hipMemcpyDeviceToHost) != hipSuccess ||
-                          hipMemcpy(best_dist, o + cap, sizeof(int) * (size_t)n_l, hipMemcpyDeviceToHost) != hipSuccess))
-        rc = ORBX_EDEVICE;
-    hipFree(d);
-    return rc;
+    const size_t om = c.in(meta, sizeof(meta));
+    const size_t ok = c.in(nullptr, sizeof(orbx_keypoint) * 2 * (size_t)cap);   // frame f at kps + f * cap
+    const size_t od = c.in(nullptr, (size_t)64 * cap);
+    const size_t oo = c.out(sizeof(int) * 2 * (size_t)cap);
+    orbx_status rc = c.prepare();
+    if (rc != ORBX_OK) return rc;
+    uint8_t* hk = c.host(ok);
+    uint8_t* hd = c.host(od);
+    if (!hk || !hd) return ORBX_ENOMEM;
+    std::memcpy(hk, kps_l, sizeof(orbx_keypoint) * (size_t)n_l);
+    if (n_r) std::memcpy(hk + sizeof(orbx_keypoint) * (size_t)cap, kps_r, sizeof(orbx_keypoint) * (size_t)n_r);
+    std::memcpy(hd, desc_l, (size_t)32 * n_l);
+    if (n_r) std::memcpy(hd + (size_t)32 * cap, desc_r, (size_t)32 * n_r);
+    if ((rc = c.upload()) != ORBX_OK) return rc;
+    const int* m = c.dev_as<const int>(om);
+    int* o = c.dev_as<int>(oo);
+    rc = orbm_stereo_band_device(c.dev_as<const orbx_keypoint>(ok), c.dev(od), m, cap, m + 2, m + 3, 1, rows, scale,
+                                 nlevels, min_d, max_d, o, o + cap, c.stream());
+    if (rc != ORBX_OK) return rc;
+    c.fetch(oo, best_idx, sizeof(int) * (size_t)n_l);
+    c.fetch(oo + sizeof(int) * (size_t)cap, best_dist, sizeof(int) * (size_t)n_l);
+    return c.finish();
 }
 
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b)
@@ -1179,31 +1177,46 @@ orbx_status orbm_allpairs(int device, const uint8_t* q, int nq, const uint8_t* t
             }
         return ORBX_OK;
     }
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
-    hipSetDevice(device);
-    BowStage st;
-    const size_t oq = st.add(q, (size_t)32 * nq);
-    const size_t ot = st.add(t, (size_t)32 * nt);
+    HostCall c(device);
+    const size_t oq = c.in(q, (size_t)32 * nq);
+    const size_t ot = c.in(t, (size_t)32 * nt);
     const size_t out_bytes = mode == ORBM_TOP2 ? sizeof(int) * 3 * (size_t)nq : sizeof(uint16_t) * (size_t)nq * nt;
-    uint8_t* d = nullptr;
-    if (hipMalloc((void**)&d, st.host.size() + out_bytes + 16) != hipSuccess) return ORBX_ENOMEM;
-    uint8_t* dout = d + ((st.host.size() + 15) & ~(size_t)15);
-    orbx_status rc = ORBX_OK;
-    if (hipMemcpy(d, st.host.data(), st.host.size(), hipMemcpyHostToDevice) != hipSuccess) rc = ORBX_EDEVICE;
-    int* o = (int*)dout;
-    if (rc == ORBX_OK)
-        rc = orbm_allpairs_device(d + oq, nq, d + ot, nt, mode, o, o + nq, o + 2 * nq, (uint16_t*)dout, nullptr);
-    if (rc == ORBX_OK && hipDeviceSynchronize() != hipSuccess) rc = ORBX_EDEVICE;
-    if (rc == ORBX_OK && mode == ORBM_TOP2 &&
-        (hipMemcpy(best_idx, o, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(best, o + nq, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(second, o + 2 * nq, sizeof(int) * (size_t)nq, hipMemcpyDeviceToHost) != hipSuccess))
-        rc = ORBX_EDEVICE;
-    if (rc == ORBX_OK && mode == ORBM_FULL_U16 && hipMemcpy(full, dout, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)
-        rc = ORBX_EDEVICE;
-    hipFree(d);
-    return rc;
+    const size_t oo = c.out(out_bytes);
+    orbx_status rc = c.prepare();
+    if (rc == ORBX_OK) rc = c.upload();
+    if (rc != ORBX_OK) return rc;
+    int* o = c.dev_as<int>(oo);
+    rc = orbm_allpairs_device(c.dev(oq), nq, c.dev(ot), nt, mode, o, o + nq, o + 2 * nq, (uint16_t*)o, c.stream());
+    if (rc != ORBX_OK) return rc;
+    if (mode == ORBM_TOP2) {
+        c.fetch(oo, best_idx, sizeof(int) * (size_t)nq);
+        c.fetch(oo + sizeof(int) * (size_t)nq, best, sizeof(int) * (size_t)nq);
+        c.fetch(oo + sizeof(int) * 2 * (size_t)nq, second, sizeof(int) * (size_t)nq);
+    } else {
+        c.fetch(oo, full, out_bytes);
+    }
+    return c.finish();
+}
+
+orbx_status orbm_search_for_initialization_device(const orbx_keypoint* d_kps, const uint8_t* d_desc,
+                                                  const int* d_counts, int nframes, int cap, const int* d_pair_a,
+                                                  const int* d_pair_b, int npairs, const orbm_grid* grid,
+                                                  int window, float nnratio, int check_ori, float* d_prev_matched,
+                                                  int* d_matches12, int* d_nmatches, void* stream)
+{
+    if (!d_kps || !d_desc || !d_counts || nframes <= 0 || cap <= 0 || cap > 32767 || npairs < 0 || !grid)
+        return ORBX_EINVAL;
+    if (npairs == 0) return ORBX_OK;
+    if (!d_pair_a || !d_pair_b || !d_matches12 || !d_nmatches) return ORBX_EINVAL;
+    if (search_init_smem_bytes(cap) > 160 * 1024) return ORBX_ENOSPC;
+    hipStream_t s = (hipStream_t)stream;
+    void* scratch = nullptr;
+    if (hipMallocAsync(&scratch, search_init_scratch_bytes(nframes, npairs, cap), s) != hipSuccess)
+        return ORBX_ENOMEM;
+    launch_search_init(d_kps, d_desc, d_counts, nframes, cap, d_pair_a, d_pair_b, npairs, *grid, window, nnratio,
+                       check_ori, d_prev_matched, scratch, d_matches12, d_nmatches, s);
+    hipFreeAsync(scratch, s);
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
 orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const int* d_counts,
@@ -1211,18 +1224,60 @@ orbx_status orbm_search_init_batch_device(const orbx_keypoint* d_kps, const uint
                                           int rows, int cols, int window, float nnratio, int check_ori,
                                           int* d_matches12, int* d_nmatches, void* stream)
 {
-    if (!d_kps || !d_desc || !d_counts || nframes <= 0 || cap <= 0 || cap > 32767 || npairs < 0 || rows <= 0 ||
-        cols <= 0)
-        return ORBX_EINVAL;
-    if (npairs == 0) return ORBX_OK;
-    hipStream_t s = (hipStream_t)stream;
-    void* scratch = nullptr;
-    if (hipMallocAsync(&scratch, search_init_scratch_bytes(nframes, npairs, cap), s) != hipSuccess)
-        return ORBX_ENOMEM;
-    launch_search_init(d_kps, d_desc, d_counts, nframes, cap, d_pair_a, d_pair_b, npairs, rows, cols, window, nnratio,
-                       check_ori, scratch, d_matches12, d_nmatches, s);
-    hipFreeAsync(scratch, s);
-    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+    if (rows <= 0 || cols <= 0) return ORBX_EINVAL;
+    // Frame::ComputeImageBounds without distortion (src/Frame.cc:614-620) and the grid scale (:127-128)
+    const orbm_grid g{0.0f, 0.0f, 64.0f / ((float)cols - 0.0f), 48.0f / ((float)rows - 0.0f)};
+    return orbm_search_for_initialization_device(d_kps, d_desc, d_counts, nframes, cap, d_pair_a, d_pair_b, npairs,
+                                                 &g, window, nnratio, check_ori, nullptr, d_matches12, d_nmatches,
+                                                 stream);
+}
+
+orbx_status orbm_search_for_initialization(int device, const orbx_keypoint* kps1, const uint8_t* desc1, int n1,
+                                           const orbx_keypoint* kps2, const uint8_t* desc2, int n2,
+                                           const orbm_grid* grid, float* prev_matched, int window, float nnratio,
+                                           int check_ori, int* matches12, int* nmatches)
+{
+    if (n1 < 0 || n2 < 0 || n1 > 32767 || n2 > 32767 || !grid || !nmatches) return ORBX_EINVAL;
+    *nmatches = 0;
+    if (n1 == 0) return ORBX_OK;   // vnMatches12 is empty
+    if (!kps1 || !desc1 || !prev_matched || !matches12 || (n2 > 0 && (!kps2 || !desc2))) return ORBX_EINVAL;
+    // extractor order (ORBextractor::operator() concatenates the levels, src/ORBextractor.cc:1290-1333): the
+    // device finds level 0 as a prefix
+    for (int i = 1; i < n1; ++i)
+        if (kps1[i].octave < kps1[i - 1].octave) return ORBX_EINVAL;
+    for (int i = 1; i < n2; ++i)
+        if (kps2[i].octave < kps2[i - 1].octave) return ORBX_EINVAL;
+    for (int i = 0; i < n1; ++i) matches12[i] = -1;
+    if (n2 == 0) return ORBX_OK;   // every GetFeaturesInArea is empty
+    const int cap = std::max(n1, n2);
+    if (search_init_smem_bytes(cap) > 160 * 1024) return ORBX_ENOSPC;
+    HostCall c(device);
+    const int meta[4] = {n1, n2, 0, 1};   // counts[2], pair (0, 1)
+    const size_t om = c.in(meta, sizeof(meta));
+    const size_t ok = c.in(nullptr, sizeof(orbx_keypoint) * 2 * (size_t)cap);   // frame f at kps + f * cap
+    const size_t od = c.in(nullptr, (size_t)64 * cap);
+    const size_t opv = c.in(prev_matched, sizeof(float) * 2 * (size_t)n1);
+    const size_t ores = c.out(sizeof(int) * ((size_t)cap + 1));
+    const size_t osc = c.out(search_init_scratch_bytes(2, 1, cap));
+    orbx_status rc = c.prepare();
+    if (rc != ORBX_OK) return rc;
+    uint8_t* hk = c.host(ok);
+    uint8_t* hd = c.host(od);
+    if (!hk || !hd) return ORBX_ENOMEM;
+    std::memcpy(hk, kps1, sizeof(orbx_keypoint) * (size_t)n1);
+    std::memcpy(hk + sizeof(orbx_keypoint) * (size_t)cap, kps2, sizeof(orbx_keypoint) * (size_t)n2);
+    std::memcpy(hd, desc1, (size_t)32 * n1);
+    std::memcpy(hd + (size_t)32 * cap, desc2, (size_t)32 * n2);
+    if ((rc = c.upload()) != ORBX_OK) return rc;
+    const int* m = c.dev_as<const int>(om);
+    int* res = c.dev_as<int>(ores);
+    launch_search_init(c.dev_as<const orbx_keypoint>(ok), c.dev(od), m, 2, cap, m + 2, m + 3, 1, *grid, window,
+                       nnratio, check_ori, c.dev_as<float>(opv), c.dev(osc), res + 1, res, c.stream());
+    if (hipGetLastError() != hipSuccess) return ORBX_EDEVICE;
+    c.fetch(ores + sizeof(int), matches12, sizeof(int) * (size_t)n1);
+    c.fetch(ores, nmatches, sizeof(int));
+    c.fetch(opv, prev_matched, sizeof(float) * 2 * (size_t)n1);
+    return c.finish();
 }
 
 }  // extern "C"

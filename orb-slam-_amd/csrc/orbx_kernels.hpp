@@ -74,9 +74,11 @@ void launch_best2_csr(const uint8_t* q, int nq, const uint8_t* t, const int* ptr
                       int* bi, int* b1, int* b2, hipStream_t s);
 void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, uint16_t* out, hipStream_t s);
 size_t search_init_scratch_bytes(int nframes, int npairs, int cap);
+size_t search_init_smem_bytes(int cap);   // k_si_greedy's LDS (must fit 160 KiB)
+// prev: [npairs][cap] float2 vbPrevMatched (window centres in, matched F2 positions out) or NULL
 void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int nframes, int cap,
-                        const int* pa, const int* pb, int npairs, int rows, int cols, int window, float nnratio,
-                        int check_ori, void* scratch, int* m12, int* nm, hipStream_t s);
+                        const int* pa, const int* pb, int npairs, const orbm_grid& G, int window, float nnratio,
+                        int check_ori, float* prev, void* scratch, int* m12, int* nm, hipStream_t s);
 
 size_t stereo_match_smem(const Geometry& g, int cap);
 void launch_stereo(const Geometry& g, const Geometry* d_geom, const FramePtrs& PL, const FramePtrs& PR,

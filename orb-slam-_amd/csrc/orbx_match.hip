@@ -269,7 +269,7 @@ __device__ __forceinline__ int level0_count(const orbx_keypoint* k, int n)
 }
 
 __global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict__ kps, const int* __restrict__ counts,
-                                                 int cap, int rows, int cols, uint32_t* __restrict__ gkeys,
+                                                 int cap, orbm_grid G, uint32_t* __restrict__ gkeys,
                                                  float2* __restrict__ gxy, int* __restrict__ gn)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
@@ -282,13 +282,11 @@ __global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict
     while (p2 < n0) p2 <<= 1;
     if (tid == 0) s_ng = 0;
     __syncthreads();
-    const float invW = (float)kGridCols / ((float)cols - 0.0f);
-    const float invH = (float)kGridRows / ((float)rows - 0.0f);
     for (int i = tid; i < p2; i += 256) {
         uint32_t key = 0xFFFFFFFFu;
         if (i < n0) {
-            const int px = (int)roundf((k[i].x - 0.0f) * invW);
-            const int py = (int)roundf((k[i].y - 0.0f) * invH);
+            const int px = (int)roundf((k[i].x - G.min_x) * G.grid_w_inv);
+            const int py = (int)roundf((k[i].y - G.min_y) * G.grid_h_inv);
             if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {   // PosInGrid
                 key = ((uint32_t)(px * kGridRows + py) << 16) | (uint32_t)i;
                 atomicAdd(&s_ng, 1);
@@ -332,17 +330,17 @@ struct SiWindow {
     float x, y, r;
 };
 
-__device__ __forceinline__ SiWindow si_window(const uint32_t* keys, int ng, float x, float y, float r, float invW,
-                                              float invH)
+__device__ __forceinline__ SiWindow si_window(const uint32_t* keys, int ng, float2 c, float r, const orbm_grid& G)
 {
     SiWindow w;
+    const float x = c.x, y = c.y;
     w.x = x;
     w.y = y;
     w.r = r;
-    const int cx0 = max(0, (int)floorf((x - 0.0f - r) * invW));
-    const int cx1 = min(kGridCols - 1, (int)ceilf((x - 0.0f + r) * invW));
-    w.cy0 = max(0, (int)floorf((y - 0.0f - r) * invH));
-    w.cy1 = min(kGridRows - 1, (int)ceilf((y - 0.0f + r) * invH));
+    const int cx0 = max(0, (int)floorf((x - G.min_x - r) * G.grid_w_inv));
+    const int cx1 = min(kGridCols - 1, (int)ceilf((x - G.min_x + r) * G.grid_w_inv));
+    w.cy0 = max(0, (int)floorf((y - G.min_y - r) * G.grid_h_inv));
+    w.cy1 = min(kGridRows - 1, (int)ceilf((y - G.min_y + r) * G.grid_h_inv));
     w.lo = w.hi = 0;
     if (cx0 < kGridCols && cx1 >= 0 && w.cy0 < kGridRows && w.cy1 >= 0) {
         w.lo = lower_bound_u32(keys, ng, (uint32_t)(cx0 * kGridRows) << 16);
@@ -366,7 +364,7 @@ __device__ __forceinline__ bool si_in_window(const uint32_t* keys, const float2*
 __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* __restrict__ kps,
                                                           const uint8_t* __restrict__ desc, int cap,
                                                           const int* __restrict__ pa, const int* __restrict__ pb,
-                                                          int rows, int cols, int window,
+                                                          orbm_grid G, int window, const float2* __restrict__ prev,
                                                           const uint32_t* __restrict__ gkeys,
                                                           const float2* __restrict__ gxy, const int* __restrict__ gn,
                                                           int* __restrict__ qcnt, uint4* __restrict__ qtop)
@@ -385,13 +383,14 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
     const orbx_keypoint* k1 = kps + (size_t)fa * cap;
     const uint8_t* d1 = desc + (size_t)fa * cap * 32;
     const uint8_t* d2 = desc + (size_t)fb * cap * 32;
-    const float invW = (float)kGridCols / ((float)cols - 0.0f);
-    const float invH = (float)kGridRows / ((float)rows - 0.0f);
+    const float2* pv = prev ? prev + (size_t)pair * cap : nullptr;
     const int nwaves = gridDim.y * (SI_BUILD_NT / 64);
     for (int i1 = blockIdx.y * (SI_BUILD_NT / 64) + wave; i1 < n10; i1 += nwaves) {
         const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
         const ulonglong2 a0 = a[0], a1 = a[1];
-        const SiWindow w = si_window(keys, ng, k1[i1].x, k1[i1].y, (float)window, invW, invH);
+        // window centre vbPrevMatched[i1] (src/ORBmatcher.cc:456-460); F1's own keypoint when not given
+        const float2 c = pv ? pv[i1] : make_float2(k1[i1].x, k1[i1].y);
+        const SiWindow w = si_window(keys, ng, c, (float)window, G);
         // lane-local 4 smallest (Hamming << 16 | visit position), with their i2
         uint32_t hk[SI_TOPK], hi2[SI_TOPK];
 #pragma unroll
@@ -474,7 +473,8 @@ __host__ __device__ inline SgLayout sg_layout(int cap)
 __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restrict__ kps,
                                                    const uint8_t* __restrict__ desc, const int* __restrict__ counts,
                                                    int cap, const int* __restrict__ pa, const int* __restrict__ pb,
-                                                   int rows, int cols, int window, float nnratio, int check_ori,
+                                                   orbm_grid G, int window, float nnratio, int check_ori,
+                                                   float2* __restrict__ prev,
                                                    const uint32_t* __restrict__ gkeys,
                                                    const float2* __restrict__ gxy, const int* __restrict__ gn,
                                                    const int* __restrict__ qcnt, const uint4* __restrict__ qtop,
@@ -542,8 +542,7 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
     // before it, which is the sequential result.  A step that needs a full scan ends the
     // chunk's exact prefix: it is replayed on its own with the wave.
     const int n2c = max(n2 - 1, 0);
-    const float invW = (float)kGridCols / ((float)cols - 0.0f);
-    const float invH = (float)kGridRows / ((float)rows - 0.0f);
+    float2* pv = prev ? prev + (size_t)pair * cap : nullptr;
     auto decide = [&](const uint32_t (&e)[SI_TOPK], const uint32_t (&md)[SI_TOPK], int c, int& bi, int& bd,
                       bool& scan) -> bool {
         bool ok[SI_TOPK];
@@ -676,7 +675,8 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
             const float2* xy = gxy + (size_t)fb * cap;
             const ulonglong2* a = (const ulonglong2*)(desc + ((size_t)fa * cap + q1) * 32);
             const ulonglong2 a0 = a[0], a1 = a[1];
-            const SiWindow w = si_window(keys, ng, k1[q1].x, k1[q1].y, (float)window, invW, invH);
+            const float2 c = pv ? pv[q1] : make_float2(k1[q1].x, k1[q1].y);
+            const SiWindow w = si_window(keys, ng, c, (float)window, G);
             uint32_t b1 = 0x1FF, b2 = 0x1FF, bp = 0xFFFF, bx = 0;
             int count = 0;
             for (int g0 = w.lo; g0 < w.hi; g0 += 64) {
@@ -763,6 +763,7 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
         const int v = i < n1 ? (int)m12[i] : -1;
         out[i] = v;
         nmatches += v >= 0;
+        if (pv && v >= 0) pv[i] = make_float2(k2[v].x, k2[v].y);   // update vbPrevMatched (:580-584)
     }
     for (int o = 32; o > 0; o >>= 1) nmatches += __shfl_xor(nmatches, o);
     if (lane == 0) nm_out[pair] = nmatches;
@@ -782,9 +783,11 @@ size_t search_init_scratch_bytes(int nframes, int npairs, int cap)
     return (size_t)nframes * cap * (4 + 8) + (size_t)nframes * 2 * 4 + (size_t)npairs * cap * (4 + 16) + 64 * 6;
 }
 
+size_t search_init_smem_bytes(int cap) { return sg_layout(cap).total; }
+
 void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int nframes, int cap,
-                        const int* pa, const int* pb, int npairs, int rows, int cols, int window, float nnratio,
-                        int check_ori, void* scratch, int* m12, int* nm, hipStream_t s)
+                        const int* pa, const int* pb, int npairs, const orbm_grid& G, int window, float nnratio,
+                        int check_ori, float* prev, void* scratch, int* m12, int* nm, hipStream_t s)
 {
     uint8_t* p = (uint8_t*)scratch;
     auto carve = [&](size_t bytes) {
@@ -799,17 +802,16 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     uint4* qtop = (uint4*)carve((size_t)npairs * cap * 16);
     int p2 = 1;
     while (p2 < cap) p2 <<= 1;
-    hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)p2 * 4, s, kps, counts, cap, rows, cols, gkeys,
-                       gxy, gn);
+    hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)p2 * 4, s, kps, counts, cap, G, gkeys, gxy, gn);
     const size_t bsmem = (((size_t)cap * 4 + 15) & ~(size_t)15) + (size_t)cap * 8;
     // query slices per pair: about 8 waves per SIMD over the chip, at least 4 queries per wave
     const int qsplit = std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
-    hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, rows,
-                       cols, window, gkeys, gxy, gn, qcnt, qtop);
+    hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, G,
+                       window, (const float2*)prev, gkeys, gxy, gn, qcnt, qtop);
     const size_t gsmem = sg_layout(cap).total;
     hipFuncSetAttribute((const void*)k_si_greedy, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gsmem);
-    hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), gsmem, s, kps, desc, counts, cap, pa, pb, rows, cols,
-                       window, nnratio, check_ori, gkeys, gxy, gn, qcnt, qtop, m12, nm);
+    hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), gsmem, s, kps, desc, counts, cap, pa, pb, G, window,
+                       nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm);
 }
 
 }  // namespace orbx

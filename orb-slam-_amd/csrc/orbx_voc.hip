@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/orbx.h"
+#include "orbx_host.hpp"
 
 struct orbx_vocabulary {
     int device = 0;
@@ -249,7 +250,7 @@ orbx_status orbv_create(int k, int L, int scoring, int weighting, int nnodes, co
         if (parent[i] < 0 || parent[i] >= i) return ORBX_EINVAL;   // parents precede children (file order)
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORBX_EDEVICE;
-    hipSetDevice(device);
+    orbx::DeviceGuard guard(device);
     std::vector<int> cbegin(nnodes + 1, 0), child(nnodes, 0), fill(nnodes, 0), word(nnodes, 0);
     for (int i = 1; i < nnodes; ++i) cbegin[parent[i] + 1]++;
     for (int i = 0; i < nnodes; ++i) cbegin[i + 1] += cbegin[i];
@@ -320,7 +321,7 @@ orbx_status orbv_load_text(const char* path, int device, orbx_vocabulary** out)
 void orbv_destroy(orbx_vocabulary* v)
 {
     if (!v) return;
-    hipSetDevice(v->device);
+    orbx::DeviceGuard guard(v->device);
     if (v->d_cbegin) hipFree(v->d_cbegin);
     if (v->d_child) hipFree(v->d_child);
     if (v->d_desc) hipFree(v->d_desc);
@@ -351,7 +352,7 @@ orbx_status orbv_transform_batch_device(const orbx_vocabulary* v, const uint8_t*
         !d_bow_n || !d_fv_node || !d_fv_ptr || !d_fv_idx || !d_fv_nnodes)
         return ORBX_EINVAL;
     if (nframes == 0) return ORBX_OK;
-    hipSetDevice(v->device);
+    orbx::DeviceGuard guard(v->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t nf = (size_t)nframes * cap;
     void* scratch = nullptr;
@@ -383,43 +384,36 @@ orbx_status orbv_transform(const orbx_vocabulary* v, const uint8_t* desc, int n,
     fv_ptr[0] = 0;
     if (n == 0) return ORBX_OK;
     if (!desc || !bow_word || !bow_weight || !fv_node || !fv_idx) return ORBX_EINVAL;
-    hipSetDevice(v->device);
     const size_t cap = (size_t)n;
-    uint8_t* d = nullptr;
-    const size_t bytes = cap * 32 + 16 + cap * (4 + 8 + 4 + 4) + (cap + 1) * 4 + 16;
-    if (hipMalloc((void**)&d, bytes) != hipSuccess) return ORBX_ENOMEM;
-    uint8_t* dd = d;
-    int* cnt = (int*)(d + cap * 32);
-    double* bw = (double*)(d + cap * 32 + 16);
-    int32_t* bwd = (int32_t*)(bw + cap);
-    int32_t* fnode = bwd + cap;
-    int32_t* fidx = fnode + cap;
-    int32_t* fptr = fidx + cap;
-    int* meta = fptr + cap + 1;   // bow_n, fv_nnodes
-    orbx_status st = ORBX_OK;
-    if (hipMemcpy(dd, desc, cap * 32, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(cnt, &n, sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
-        st = ORBX_EDEVICE;
-    if (st == ORBX_OK)
-        st = orbv_transform_batch_device(v, dd, cnt, 1, n, levelsup, bwd, bw, meta, fnode, fptr, fidx, meta + 1,
-                                         nullptr);
+    orbx::HostCall c(v->device);
+    const size_t ocnt = c.in(&n, sizeof(int));
+    const size_t odesc = c.in(desc, cap * 32);
+    const size_t ometa = c.out(2 * sizeof(int));   // bow_n, fv_nnodes
+    const size_t obw = c.out(cap * sizeof(double));
+    const size_t obwd = c.out(cap * sizeof(int32_t));
+    const size_t ofnode = c.out(cap * sizeof(int32_t));
+    const size_t ofptr = c.out((cap + 1) * sizeof(int32_t));
+    const size_t ofidx = c.out(cap * sizeof(int32_t));
+    orbx_status st = c.prepare();
+    if (st == ORBX_OK) st = c.upload();
+    if (st != ORBX_OK) return st;
+    int* meta = c.dev_as<int>(ometa);
+    st = orbv_transform_batch_device(v, c.dev(odesc), c.dev_as<const int>(ocnt), 1, n, levelsup,
+                                     c.dev_as<int32_t>(obwd), c.dev_as<double>(obw), meta, c.dev_as<int32_t>(ofnode),
+                                     c.dev_as<int32_t>(ofptr), c.dev_as<int32_t>(ofidx), meta + 1, c.stream());
+    if (st != ORBX_OK) return st;
+    // every output has room for n entries: fetch them whole with the counts (one round trip)
     int m[2] = {0, 0};
-    if (st == ORBX_OK && hipMemcpy(m, meta, sizeof(m), hipMemcpyDeviceToHost) != hipSuccess) st = ORBX_EDEVICE;
-    if (st == ORBX_OK && (hipMemcpy(bow_word, bwd, sizeof(int32_t) * m[0], hipMemcpyDeviceToHost) != hipSuccess ||
-                          hipMemcpy(bow_weight, bw, sizeof(double) * m[0], hipMemcpyDeviceToHost) != hipSuccess ||
-                          hipMemcpy(fv_node, fnode, sizeof(int32_t) * m[1], hipMemcpyDeviceToHost) != hipSuccess ||
-                          hipMemcpy(fv_ptr, fptr, sizeof(int32_t) * (m[1] + 1), hipMemcpyDeviceToHost) != hipSuccess))
-        st = ORBX_EDEVICE;
-    int nv = 0;
-    if (st == ORBX_OK && m[1] > 0) nv = fv_ptr[m[1]];
-    if (st == ORBX_OK && nv > 0 && hipMemcpy(fv_idx, fidx, sizeof(int32_t) * nv, hipMemcpyDeviceToHost) != hipSuccess)
-        st = ORBX_EDEVICE;
-    hipFree(d);
-    if (st == ORBX_OK) {
-        *bow_n = m[0];
-        *fv_nnodes = m[1];
-    }
-    return st;
+    c.fetch(ometa, m, sizeof(m));
+    c.fetch(obwd, bow_word, cap * sizeof(int32_t));
+    c.fetch(obw, bow_weight, cap * sizeof(double));
+    c.fetch(ofnode, fv_node, cap * sizeof(int32_t));
+    c.fetch(ofptr, fv_ptr, (cap + 1) * sizeof(int32_t));
+    c.fetch(ofidx, fv_idx, cap * sizeof(int32_t));
+    if ((st = c.finish()) != ORBX_OK) return st;
+    *bow_n = m[0];
+    *fv_nnodes = m[1];
+    return ORBX_OK;
 }
 
 }  // extern "C"

@@ -34,7 +34,8 @@ EXPORTED = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_capacity", "orbx_extract", "orbx_get_level",
     "orbx_extract_batch_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
     "orbx_debug_pyramid", "orbx_debug_candidates", "orbm_descriptor_distance", "orbm_allpairs_device", "orbm_allpairs",
-    "orbm_search_init_batch_device", "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
+    "orbm_search_init_batch_device", "orbm_search_for_initialization_device", "orbm_search_for_initialization",
+    "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
     "orbm_bow_search_device", "orbm_bow_search",
     "orbm_search_by_projection_device", "orbm_search_by_projection",
     "orbm_project_search_device", "orbm_project_search", "orbx_ingest_batch_device", "orbx_depth_batch_device",
@@ -84,6 +85,22 @@ def proj_params(grid, scale, th=1.0, nnratio=0.8):
 
 
 PROJ_LAST_FRAME, PROJ_KEYFRAME, PROJ_SIM3, FUSE, FUSE_SIM3 = 0, 1, 2, 3, 4
+
+
+class Grid(C.Structure):
+    """orbm_grid: Frame's image bounds and grid cell inverses (src/Frame.cc:32-33, 127-128)."""
+    _fields_ = [("min_x", C.c_float), ("min_y", C.c_float), ("grid_w_inv", C.c_float), ("grid_h_inv", C.c_float)]
+
+
+def frame_grid(bounds):
+    """bounds = (mnMinX, mnMaxX, mnMinY, mnMaxY) -> Grid, with the inverses computed in float like
+    Frame's constructor: 64.f / (mnMaxX - mnMinX), 48.f / (mnMaxY - mnMinY)."""
+    b = [np.float32(v) for v in bounds]
+    g = Grid()
+    g.min_x, g.min_y = float(b[0]), float(b[2])
+    g.grid_w_inv = float(np.float32(64) / np.float32(b[1] - b[0]))
+    g.grid_h_inv = float(np.float32(48) / np.float32(b[3] - b[2]))
+    return g
 
 MAP_POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
                             ("max_dist", "<f4"), ("min_dist", "<f4"), ("angle", "<f4"), ("octave", "<i4"),
@@ -156,6 +173,10 @@ def _load():
     L.orbm_allpairs.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, C.c_int, vp, vp, vp, vp]
     L.orbm_search_init_batch_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int,
                                                 C.c_int, C.c_float, C.c_int, vp, vp, vp]
+    L.orbm_search_for_initialization_device.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp, vp, C.c_int, vp,
+                                                        C.c_int, C.c_float, C.c_int, vp, vp, vp, vp]
+    L.orbm_search_for_initialization.argtypes = [C.c_int, vp, u8p, C.c_int, vp, u8p, C.c_int, vp, f32p, C.c_int,
+                                                 C.c_float, C.c_int, i32p, i32p]
     L.orbx_compute_stereo_matches.argtypes = [vp, vp, vp, u8p, C.c_int, vp, u8p, C.c_int, C.c_float, C.c_float,
                                               f32p, f32p, i32p]
     L.orbx_stereo_batch_device.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_float, C.c_float, vp, vp,
@@ -619,8 +640,11 @@ class ORBmatcher:
         return self.project_search(FUSE_SIM3, kf[0], kf[1], kf[2], None, Scw, pts, pdesc, prm, device)
 
     def search_for_initialization_batch(self, kps, desc, counts, pair_a, pair_b, rows, cols, window=100,
-                                        matches12=None, nmatches=None, stream=None):
-        """SearchForInitialization over device frame pairs; returns (matches12, nmatches) tensors."""
+                                        matches12=None, nmatches=None, stream=None, bounds=None, prev_matched=None):
+        """SearchForInitialization over device frame pairs; returns (matches12, nmatches) tensors.
+        bounds = (mnMinX, mnMaxX, mnMinY, mnMaxY) (default 0..cols x 0..rows); prev_matched: float32
+        (npairs, cap, 2) cuda tensor holding each pair's vbPrevMatched, updated in place (default: F1's
+        keypoints, not written)."""
         import torch
         npairs = pair_a.shape[0]
         cap = kps.shape[1]
@@ -628,13 +652,50 @@ class ORBmatcher:
             matches12 = torch.empty((npairs, cap), dtype=torch.int32, device=kps.device)
         if nmatches is None:
             nmatches = torch.empty((npairs,), dtype=torch.int32, device=kps.device)
-        rc = lib.orbm_search_init_batch_device(_ptr(kps), _ptr(desc), _ptr(counts), kps.shape[0], cap, _ptr(pair_a),
-                                               _ptr(pair_b),
-                                               npairs, rows, cols, window, self.mfNNratio,
-                                               1 if self.mbCheckOrientation else 0, _ptr(matches12), _ptr(nmatches),
-                                               _stream(stream))
-        _check("orbm_search_init_batch_device", rc)
+        ori = 1 if self.mbCheckOrientation else 0
+        if bounds is None and prev_matched is None:
+            rc = lib.orbm_search_init_batch_device(_ptr(kps), _ptr(desc), _ptr(counts), kps.shape[0], cap,
+                                                   _ptr(pair_a), _ptr(pair_b), npairs, rows, cols, window,
+                                                   self.mfNNratio, ori, _ptr(matches12), _ptr(nmatches),
+                                                   _stream(stream))
+            _check("orbm_search_init_batch_device", rc)
+            return matches12, nmatches
+        g = frame_grid(bounds if bounds is not None else (0.0, cols, 0.0, rows))
+        if prev_matched is not None:
+            assert prev_matched.dtype == torch.float32 and tuple(prev_matched.shape) == (npairs, cap, 2)
+            assert prev_matched.is_contiguous()
+        rc = lib.orbm_search_for_initialization_device(_ptr(kps), _ptr(desc), _ptr(counts), kps.shape[0], cap,
+                                                       _ptr(pair_a), _ptr(pair_b), npairs, C.byref(g), window,
+                                                       self.mfNNratio, ori, _ptr(prev_matched), _ptr(matches12),
+                                                       _ptr(nmatches), _stream(stream))
+        _check("orbm_search_for_initialization_device", rc)
         return matches12, nmatches
+
+    def SearchForInitialization(self, F1, F2, vbPrevMatched, windowSize=100, bounds=None, device=0):
+        """ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+        (src/ORBmatcher.cc:417-588) on host arrays: F = (mvKeysUn, mDescriptors[, (cols, rows)]);
+        bounds = (mnMinX, mnMaxX, mnMinY, mnMaxY) (default 0..cols x 0..rows from F2).  vbPrevMatched is
+        a float32 (n1, 2) numpy array, updated in place like the reference's.  Returns (nmatches, vnMatches12)."""
+        k1 = np.ascontiguousarray(F1[0], KEYPOINT_DTYPE)
+        k2 = np.ascontiguousarray(F2[0], KEYPOINT_DTYPE)
+        n1, n2 = len(k1), len(k2)
+        d1 = np.ascontiguousarray(F1[1] if n1 else np.zeros((1, 32), np.uint8), np.uint8)
+        d2 = np.ascontiguousarray(F2[1] if n2 else np.zeros((1, 32), np.uint8), np.uint8)
+        if bounds is None:
+            cols, rows = F2[2]
+            bounds = (0.0, cols, 0.0, rows)
+        assert isinstance(vbPrevMatched, np.ndarray) and vbPrevMatched.dtype == np.float32
+        assert vbPrevMatched.shape == (n1, 2) and vbPrevMatched.flags.c_contiguous
+        g = frame_grid(bounds)
+        m12 = np.full(max(n1, 1), -1, np.int32)
+        nm = C.c_int(0)
+        pv = vbPrevMatched if n1 else np.zeros((1, 2), np.float32)
+        _check("orbm_search_for_initialization",
+               lib.orbm_search_for_initialization(device, k1.ctypes.data, _u8(d1), n1, k2.ctypes.data, _u8(d2), n2,
+                                                  C.byref(g), pv.ctypes.data_as(C.POINTER(C.c_float)), windowSize,
+                                                  self.mfNNratio, 1 if self.mbCheckOrientation else 0,
+                                                  m12.ctypes.data_as(C.POINTER(C.c_int)), C.byref(nm)))
+        return nm.value, m12[:n1].copy()
 
 
 def _host_view(kps, desc, fv, has_mp=None, u_right=None):

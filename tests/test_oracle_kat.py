@@ -343,3 +343,40 @@ def test_search_init_eviction_and_ratio(orbref):
     d2[1, :2] = [0xFF, 0x07]
     n, m12, _ = orbref.search_for_initialization(k1[:1], d1, k2, d2, 640, 480)
     assert n == 0 and list(m12) == [-1]
+
+
+def test_search_init_window_follows_prev_matched(orbref):
+    """The window is centred on vbPrevMatched[i1], not on F1's keypoint (src/ORBmatcher.cc:456-460),
+    and a match moves vbPrevMatched[i1] to F2's keypoint (:580-584)."""
+    k1 = _kp([(100, 100, 0)])
+    k2 = _kp([(101, 100, 0), (402, 301, 0)])
+    d1 = np.zeros((1, 32), np.uint8)
+    d2 = np.zeros((2, 32), np.uint8)
+    d2[0, 0] = 0x01                                   # a: distance 1 (near F1's keypoint)
+    d2[1, 0] = 0x03                                   # b: distance 2 (near vbPrevMatched)
+    n, m12, prev = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480)
+    assert n == 1 and list(m12) == [0] and tuple(prev[0]) == (101.0, 100.0)
+    n, m12, prev = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480,
+                                                    prev_xy=np.array([[400, 300]], np.float32))
+    assert n == 1 and list(m12) == [1] and tuple(prev[0]) == (402.0, 301.0)
+    # no match: vbPrevMatched keeps its value
+    n, m12, prev = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480,
+                                                    prev_xy=np.array([[250, 200]], np.float32))
+    assert n == 0 and list(m12) == [-1] and tuple(prev[0]) == (250.0, 200.0)
+
+
+def test_search_init_frame_bounds(orbref):
+    """Frame::PosInGrid drops keypoints outside the grid (src/Frame.cc:504-518): an undistorted
+    keypoint at x = -20 is unreachable with bounds 0..640 but found with the undistorted corners'
+    bounds -30..650 (ComputeImageBounds, src/Frame.cc:563-621)."""
+    k1 = _kp([(5, 100, 0)])
+    k2 = _kp([(-20, 100, 0)])
+    d = np.zeros((1, 32), np.uint8)
+    n, m12, _ = orbref.search_for_initialization(k1, d, k2, d, 640, 480)
+    assert n == 0 and list(m12) == [-1]
+    n, m12, prev = orbref.search_for_initialization(k1, d, k2, d, 640, 480, bounds=(-30.0, 650.0, -25.0, 505.0))
+    assert n == 1 and list(m12) == [0] and tuple(prev[0]) == (-20.0, 100.0)
+    # bounds (0, cols, 0, rows) are the default
+    a = orbref.search_for_initialization(k1, d, k2, d, 640, 480, bounds=(0.0, 640.0, 0.0, 480.0))
+    b = orbref.search_for_initialization(k1, d, k2, d, 640, 480)
+    assert a[0] == b[0] and np.array_equal(a[1], b[1])
