@@ -282,3 +282,44 @@ def test_cpp_mirror_example(orbref, cuda, tmp_path):
     desc = np.frombuffer(raw[4 + 28 * n:], np.uint8).reshape(n, 32)
     ref = orbref.extract(img, orbref.make_params(1000, 1.2, 8, 20, 7))
     assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "c++ mirror")
+
+
+def test_allpairs_config5_full_size(orbref, cuda):
+    """Config 5 at its stated size: 10,000 x 10,000 brute-force 256-bit Hamming.  TOP2 (best index,
+    best and second distance, first-min tie rule) on EVERY query against the oracle's scalar loop
+    (10^8 pairs), through both the device and the host entry points; the FULL_U16 matrix on 500
+    sampled rows (10,000 columns each) against numpy popcount, plus a checksum of every row's sum."""
+    import torch
+    import orbx
+    import orbx_synth
+    n = 10000
+    q = orbx_synth.random_descriptors(n, 501)
+    t = orbx_synth.random_descriptors(n, 502)
+    rng = np.random.default_rng(5)
+    near = rng.choice(n, n // 10, replace=False)   # 10% of targets are noisy copies of queries: real minima
+    t[near] = q[near] ^ np.packbits(rng.random((n // 10, 256)) < 0.05, axis=1)
+    t[7] = t[3]                                    # exact duplicate targets: first-min tie rule
+    wi, w1, w2 = orbref.allpairs_top2(q, t)
+    dq, dt = torch.from_numpy(q).to(cuda), torch.from_numpy(t).to(cuda)
+    bi, b1, b2 = orbx.allpairs(dq, dt, orbx.TOP2)
+    torch.cuda.synchronize()
+    assert np.array_equal(bi.cpu().numpy(), wi)
+    assert np.array_equal(b1.cpu().numpy(), w1)
+    assert np.array_equal(b2.cpu().numpy(), w2)
+    hi, h1, h2 = orbx.allpairs_host(q, t)
+    assert np.array_equal(hi, wi) and np.array_equal(h1, w1) and np.array_equal(h2, w2)
+    full = orbx.allpairs(dq, dt, orbx.FULL_U16)
+    rows = full.sum(dim=1, dtype=torch.int64).cpu().numpy()
+    torch.cuda.synchronize()
+    sel = np.sort(rng.choice(n, 500, replace=False))
+    got = full[torch.from_numpy(sel).to(cuda)].cpu().numpy().view(np.uint16).astype(np.int64)
+    pop = np.array([bin(i).count("1") for i in range(256)], np.uint8)
+    for c in range(0, len(sel), 100):   # popcount LUT in 100-row chunks (160 MB of xor at a time)
+        want = pop[q[sel[c:c + 100], None, :] ^ t[None, :, :]].sum(axis=2, dtype=np.int64)
+        assert np.array_equal(got[c:c + 100], want)
+    # every row: sum of its distances = sum over targets of popcount(q ^ t), computed bit-plane-wise
+    qb = np.unpackbits(q, axis=1).astype(np.int64)               # (n, 256)
+    tb = np.unpackbits(t, axis=1).astype(np.int64).sum(axis=0)   # ones per bit position over targets
+    want_rows = (qb * (n - tb) + (1 - qb) * tb).sum(axis=1)
+    assert np.array_equal(rows, want_rows)
+    assert (wi >= 0).all() and w1[near].max() <= 40
