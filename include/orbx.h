@@ -74,7 +74,11 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
                          orbx_keypoint* kps, int cap, uint8_t* desc, int* n_out);
 
 /* The public ORBextractor::mvImagePyramid (include/ORBextractor.h:85): level l of
- * the last orbx_extract, copied to host lazily; valid until the next extract. */
+ * the last orbx_extract, copied to host on the first call after each extract (cached
+ * until the next one).  The level is unpadded (rows x cols bytes, pitch `step`); the
+ * reference's level is a view inside a buffer with an EDGE_THRESHOLD = 19 px
+ * BORDER_REFLECT_101 border (src/ORBextractor.cc:1352-1373), which copyMakeBorder of
+ * this level rebuilds exactly (FetchPyramid). */
 orbx_status orbx_get_level(orbx_handle* h, int level, const uint8_t** data, int* rows, int* cols,
                            size_t* step);
 
