@@ -39,7 +39,24 @@ import orbx_synth  # noqa: E402
 
 BASELINE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-VALU_PEAK_GINST = 614.4   # 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction
+# VALU issue peaks measured on the MI355X by tools/probes/valu_rate.hip (profiles/r02/valu_rate.json): the
+# kernels' dominant instructions (v_pk_maximum3_f16 in FAST, v_dot4_u32_u8 / v_alignbyte_b32 in describe and the
+# pyramid, v_perm_b32) issue once per 4 cycles per SIMD (about 545-580 G wave-instr/s over the chip at 8 waves
+# per SIMD), plain ALU ops (v_xor_b32, v_fma_f32) once per 2 (about 990-1050).  A kernel's VALU fraction is taken
+# against the measured rate of its dominant instruction.
+VALU_RATES = os.path.join(ROOT, "profiles", "r02", "valu_rate.json")
+VALU_DOMINANT = {"k_fast_cells": "v_pk_maximum3_f16", "k_describe": "v_dot4_u32_u8", "k_pyramid_level": "v_dot4_u32_u8",
+                 "k_quadtree<512,16|512,8|256,4>": "v_xor_b32", "k_si_grid+k_si_build+k_si_greedy": "v_bcnt_u32_b32"}
+
+
+def valu_peak(kname):
+    """(peak G wave-instr/s of the kernel's dominant instruction at 8 waves/SIMD, instruction, 2-cycle class peak)."""
+    try:
+        d = json.load(open(VALU_RATES))
+        ins = VALU_DOMINANT.get(kname, "v_pk_maximum3_f16")
+        return float(d["rates"][ins][-1]), ins, float(d["rates"]["v_xor_b32"][-1])
+    except Exception:
+        return 614.4, "assumed 4 cycles per wave64 instruction", 1228.8
 W, H, NFEAT, NLEVELS, SCALE, INI, MINTH = 1241, 376, 2000, 8, 1.2, 20, 7
 WINDOW, NNRATIO = 100, 0.9
 
@@ -364,8 +381,11 @@ def main():
                     per = d["per_dispatch_averages"]
                     ins = sum(per[k]["SQ_INSTS_VALU"] for k in parts)
                     rate = ins / t_launch / 1e9
-                    r["valu"] = {"insts_per_launch": int(ins), "achieved": round(rate, 1), "peak": VALU_PEAK_GINST,
-                                 "unit": "G wave-instr/s", "frac": round(rate / VALU_PEAK_GINST, 4)}
+                    pk, pins, p2 = valu_peak(kname)
+                    r["valu"] = {"insts_per_launch": int(ins), "achieved": round(rate, 1), "peak": pk,
+                                 "unit": "G wave-instr/s", "frac": round(rate / pk, 4),
+                                 "peak_basis": "measured issue rate of %s, 8 waves/SIMD (profiles/r02/valu_rate.json)"
+                                               % pins, "peak_2cycle_ops": p2}
             except Exception:
                 pass
         return r
