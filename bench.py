@@ -177,8 +177,9 @@ def main():
     exs = [orbx.ORBextractor(NFEAT, SCALE, NLEVELS, INI, MINTH, device=local) for _ in range(P)]
     ex = exs[0]
     cap = ex.capacity(H, W)
-    payloads = [orbx_dist.Payload(B, cap, dev) for _ in range(P)]
-    gatherers = [orbx_dist.Gatherer(pl, world, rank) for pl in payloads]
+    # each slot double-buffers its payload: batch k's hand-back to rank 0 overlaps batch k+1's extraction
+    hands = [orbx_dist.HandBack(B, cap, dev, world, rank) for _ in range(P)]
+    last_payload = [None]
     matcher = orbx.ORBmatcher(NNRATIO, True)
     pa = torch.arange(0, B - 1, dtype=torch.int32, device=dev)
     pb = torch.arange(1, B, dtype=torch.int32, device=dev)
@@ -190,7 +191,9 @@ def main():
     def step(k, timed=False, j=None):
         base = (k % nb) * B
         j = k % P if j is None else j
-        s, pl = streams[j], payloads[j]
+        s = streams[j]
+        with torch.cuda.stream(s):
+            pl = hands[j].next_payload()
         exs[j].extract_batch_device(frames[base:base + B], pl.kps, pl.desc, pl.counts, s)
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -200,7 +203,8 @@ def main():
             e1.record(s)
             ev_m.append((e0, e1))
         with torch.cuda.stream(s):
-            gatherers[j].gather()
+            hands[j].send()
+        last_payload[0] = pl
 
     for k in range(args.warmup):
         step(k)
@@ -225,7 +229,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    payload = payloads[(args.warmup + args.steps - 1) % P]
+    payload = last_payload[0]
     nm = nm[(args.warmup + args.steps - 1) % P]
     used = sorted({(args.warmup + k) % P for k in range(args.steps)})
     stage_ms = sum(exs[j].stage_times() for j in used)   # sums over the timed steps (all streams)
@@ -261,7 +265,9 @@ def main():
         def hstep(k):
             base = (k % nb) * B
             j = k % P
-            s, pl = streams[j], payloads[j]
+            s = streams[j]
+            with torch.cuda.stream(s):
+                pl = hands[j].next_payload()
             cstream.wait_event(ex_done[j])
             with torch.cuda.stream(cstream):
                 dbuf[j].copy_(hseq[base:base + B], non_blocking=True)
@@ -272,7 +278,7 @@ def main():
             matcher.search_for_initialization_batch(pl.kps, pl.desc, pl.counts, pa, pb, H, W, WINDOW, m12[j], nm[j],
                                                     s)
             with torch.cuda.stream(s):
-                gatherers[j].gather()
+                hands[j].send()
 
         for k in range(min(args.warmup, 2 * P)):
             hstep(k)
@@ -308,6 +314,10 @@ def main():
                     "input": "pinned host memory, H2D on a copy stream overlapped with extraction (PCIe-inclusive)"}
         del hseq
 
+    for j in range(P):
+        with torch.cuda.stream(streams[j]):
+            hands[j].drain()
+    torch.cuda.synchronize()
     counts = payload.counts.cpu().numpy()
     nmatch = nm.cpu().numpy()
 

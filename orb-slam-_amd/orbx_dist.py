@@ -59,16 +59,60 @@ class Gatherer:
         if rank == 0 and world > 1:
             self.recv = [torch.empty_like(payload.buf) for _ in range(world - 1)]
 
-    def gather(self):
+    def gather_async(self):
+        """Queue the hand-back and return its work handles without waiting.  The sends read the
+        payload after the work already queued on the current stream (the extraction that filled
+        it); call finish() on the stream that next writes this payload, before writing it."""
         if self.world == 1:
-            return [self.payload.buf]
+            return []
         if self.rank == 0:
             ops = [dist.P2POp(dist.irecv, self.recv[r - 1], r) for r in range(1, self.world)]
         else:
             ops = [dist.P2POp(dist.isend, self.payload.buf, 0)]
-        for w in dist.batch_isend_irecv(ops):
+        return list(dist.batch_isend_irecv(ops))
+
+    @staticmethod
+    def finish(works):
+        """Order the current stream after the hand-back (NCCL: a stream wait, the host does not block)."""
+        for w in works:
             w.wait()
+
+    def gather(self):
+        self.finish(self.gather_async())
+        if self.world == 1:
+            return [self.payload.buf]
         return [self.payload.buf] + self.recv if self.rank == 0 else None
+
+
+class HandBack:
+    """Double-buffered payloads for one pipeline slot: batch k of the slot fills payload k % 2 while
+    payload (k - 1) % 2 may still be on its way to rank 0.  A payload's send is waited for (a stream
+    wait, not a host wait) only when the slot is about to overwrite it, so the hand-back of batch k
+    overlaps the extraction of batch k + 1 on the same stream instead of sitting in its way."""
+
+    def __init__(self, batch: int, cap: int, device, world: int, rank: int, depth: int = 2):
+        self.payloads = [Payload(batch, cap, device) for _ in range(depth)]
+        self.gatherers = [Gatherer(p, world, rank) for p in self.payloads]
+        self.pending = [[] for _ in range(depth)]
+        self.k = 0
+
+    def next_payload(self) -> Payload:
+        """The payload the slot's next batch writes; orders the current stream after its last send."""
+        i = self.k % len(self.payloads)
+        Gatherer.finish(self.pending[i])
+        self.pending[i] = []
+        return self.payloads[i]
+
+    def send(self):
+        """Hand the payload returned by next_payload() back to rank 0 (asynchronously)."""
+        i = self.k % len(self.payloads)
+        self.pending[i] = self.gatherers[i].gather_async()
+        self.k += 1
+
+    def drain(self):
+        for i in range(len(self.pending)):
+            Gatherer.finish(self.pending[i])
+            self.pending[i] = []
 
 
 # ---- config 5: 10k x 10k brute-force Hamming sharded over ranks ----------------

@@ -118,3 +118,75 @@ def test_sharded_allpairs_top2(world, nt):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+# ---- config 4 with real extractor-format payloads ------------------------------------------
+_OR_W, _OR_H, _OR_N, _OR_B = 320, 240, 300, 2   # frames per batch
+
+
+def _oracle_payload(orbref, frames, cap):
+    """The bytes orbx_extract_batch_device leaves in a Payload for `frames`, from the CPU oracle."""
+    p = orbref.make_params(_OR_N, 1.2, 8, 20, 7)
+    kps = np.zeros((len(frames), cap, 7), np.int32)
+    desc = np.zeros((len(frames), cap, 32), np.uint8)
+    counts = np.zeros(len(frames), np.int32)
+    for f, img in enumerate(frames):
+        r = orbref.extract(img, p, want_pyramid=False)
+        n = len(r.keypoints)
+        kps[f, :n] = np.ascontiguousarray(r.keypoints).view(np.int32).reshape(n, 7)
+        desc[f, :n] = r.descriptors
+        counts[f] = n
+    return np.concatenate([kps.view(np.uint8).ravel(), desc.ravel(), counts.view(np.uint8)])
+
+
+def _oracle_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "orb-slam-_amd"), os.path.join(root, "oracle")]
+    import orbref
+    import orbx_dist
+    import orbx_synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cap = _OR_N + 64
+        nfr = 2 * _OR_B * world                        # two batches per rank, contiguous shards
+        a, b = orbx_dist.shard_range(nfr, rank, world)
+        seq = [orbx_synth.gen_image(900 + i, _OR_W, _OR_H) for i in range(nfr)]
+        hb = orbx_dist.HandBack(_OR_B, cap, torch.device("cpu"), world, rank)
+        for k in range(2):                             # batch k fills payload k % 2 while k - 1 is in flight
+            pl = hb.next_payload()
+            mine = _oracle_payload(orbref, seq[a + k * _OR_B:a + (k + 1) * _OR_B], cap)
+            pl.buf.copy_(torch.from_numpy(mine))
+            hb.send()
+        hb.drain()
+        if rank == 0:
+            ok = True
+            for r in range(world):
+                ra, _ = orbx_dist.shard_range(nfr, r, world)
+                for k in range(2):
+                    want = _oracle_payload(orbref, seq[ra + k * _OR_B:ra + (k + 1) * _OR_B], cap)
+                    got = hb.payloads[k].buf if r == 0 else hb.gatherers[k].recv[r - 1]
+                    kps, desc, counts = orbx_dist.Payload.unpack(got, _OR_B, cap)
+                    ok &= bool(np.array_equal(got.numpy(), want)) and int(counts.min()) > 100
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_hand_back_of_oracle_payloads(world):
+    """Each rank extracts its shard of a frame sequence into the extractor's payload layout (the CPU
+    oracle stands in for the device here) and hands two batches back through the double-buffered
+    HandBack; rank 0 must hold every rank's payloads byte for byte."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_oracle_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True
