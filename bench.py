@@ -255,12 +255,17 @@ def main():
     host_fed = None
     if args.host_steps > 0:
         hseq = torch.from_numpy(seq).pin_memory()
-        dbuf = [torch.empty((B, H, W), dtype=torch.uint8, device=dev) for _ in range(P)]
-        cstream = torch.cuda.Stream(device=dev)
-        up_done = [torch.cuda.Event() for _ in range(P)]
-        ex_done = [torch.cuda.Event() for _ in range(P)]
-        for j in range(P):
-            ex_done[j].record(streams[j])
+        # input ring deeper than the pipeline: an upload may run two batches ahead of the oldest extraction
+        # still reading its buffer (a slot's extraction lasts about P step times while it shares the chip)
+        R = int(os.environ.get("ORBX_HOST_RING", str(2 * P)))
+        dbuf = [torch.empty((B, H, W), dtype=torch.uint8, device=dev) for _ in range(R)]
+        # high priority: HIP keeps it off the hardware queues the default-priority compute streams use
+        # (GPU_MAX_HW_QUEUES = 4), so an upload never waits behind another slot's kernels
+        cstream = torch.cuda.Stream(device=dev, priority=int(os.environ.get("ORBX_COPY_PRIO", "-1")))
+        up_done = [torch.cuda.Event() for _ in range(R)]
+        ex_done = [torch.cuda.Event() for _ in range(R)]
+        for i in range(R):
+            ex_done[i].record(streams[i % P])
 
         def hstep(k):
             base = (k % nb) * B
@@ -268,13 +273,14 @@ def main():
             s = streams[j]
             with torch.cuda.stream(s):
                 pl = hands[j].next_payload()
-            cstream.wait_event(ex_done[j])
+            i = k % R
+            cstream.wait_event(ex_done[i])
             with torch.cuda.stream(cstream):
-                dbuf[j].copy_(hseq[base:base + B], non_blocking=True)
-                up_done[j].record(cstream)
-            s.wait_event(up_done[j])
-            exs[j].extract_batch_device(dbuf[j], pl.kps, pl.desc, pl.counts, s)
-            ex_done[j].record(s)
+                dbuf[i].copy_(hseq[base:base + B], non_blocking=True)
+                up_done[i].record(cstream)
+            s.wait_event(up_done[i])
+            exs[j].extract_batch_device(dbuf[i], pl.kps, pl.desc, pl.counts, s)
+            ex_done[i].record(s)
             matcher.search_for_initialization_batch(pl.kps, pl.desc, pl.counts, pa, pb, H, W, WINDOW, m12[j], nm[j],
                                                     s)
             with torch.cuda.stream(s):
@@ -304,7 +310,7 @@ def main():
         with torch.cuda.stream(cstream):
             u0.record(cstream)
             for k in range(4):
-                dbuf[k % P].copy_(hseq[(k % nb) * B:(k % nb) * B + B], non_blocking=True)
+                dbuf[k % R].copy_(hseq[(k % nb) * B:(k % nb) * B + B], non_blocking=True)
             u1.record(cstream)
         torch.cuda.synchronize()
         up_gbs = 4 * B * H * W / (u0.elapsed_time(u1) * 1e-3) / 1e9
