@@ -526,8 +526,40 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
 // ---------------------------------------------------------------------------
 constexpr int QT_NT = 512;
 constexpr int QT_NW = QT_NT / 64;
+#ifdef ORBX_QT_PROF
+// per-level phase cycle sums (thread 0 of each workgroup): gather, init, phase-1 rounds, phase-2
+// rounds, phase-2 sorts, retain, #phase-1 rounds, #phase-2 rounds, #workgroups
+__device__ unsigned long long g_qt_prof[16][16];
+#define QT_STAMP(slot, t0)                                                            \
+    do {                                                                              \
+        if (threadIdx.x == 0) {                                                       \
+            const long long t1_ = clock64();                                          \
+            atomicAdd(&g_qt_prof[l][slot], (unsigned long long)(t1_ - (t0)));         \
+            t0 = t1_;                                                                 \
+        }                                                                             \
+    } while (0)
+#else
+#define QT_STAMP(slot, t0) ((void)0)
+#endif
 constexpr uint16_t kNone = 0xFFFF;
 
+// Inclusive wave64 prefix sum with DPP: row shifts within each 16-lane row, then row broadcasts
+// (lane 15 into row 1 and 3, lane 31 into rows 2 and 3).  Six dependent VALU steps of a few cycles
+// each, where a __shfl_up ladder is six ds_bpermute round trips through the LDS crossbar.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
+// Exclusive scan of a[0..n) in LDS by the whole block; returns the total.  Each thread scans a
+// contiguous run of per = ceil(n / NT) entries; wave totals meet in wsum, which every thread then
+// reads whole (QT_NW broadcast reads) instead of waiting on one thread's serial pass.
 template <int QT_NT>
 __device__ uint32_t block_scan_excl(uint32_t* a, int n, uint32_t* wsum)
 {
@@ -537,53 +569,24 @@ __device__ uint32_t block_scan_excl(uint32_t* a, int n, uint32_t* wsum)
     const int b = tid * per, e = min(n, b + per);
     uint32_t local = 0;
     for (int i = b; i < e; ++i) local += a[i];
-    uint32_t inc = local;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o);
-        if (lane >= o) inc += y;
-    }
+    const uint32_t inc = wave_incl_scan(local);
     if (lane == 63) wsum[wid] = inc;
     __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        for (int w = 0; w < QT_NW; ++w) {
-            const uint32_t t = wsum[w];
-            wsum[w] = run;
-            run += t;
-        }
-        wsum[QT_NW] = run;
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < QT_NW; ++w) {
+        const uint32_t t = wsum[w];
+        before += w < wid ? t : 0u;
+        total += t;
     }
-    __syncthreads();
-    uint32_t run = wsum[wid] + inc - local;
+    uint32_t run = before + inc - local;
     for (int i = b; i < e; ++i) {
         const uint32_t t = a[i];
         a[i] = run;
         run += t;
     }
-    const uint32_t total = wsum[QT_NW];
     __syncthreads();
     return total;
-}
-
-template <int QT_NT>
-__device__ void block_bitonic_desc(uint32_t* k, int p2)
-{
-    for (int size = 2; size <= p2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < (p2 >> 1); i += QT_NT) {
-                const int lo = 2 * i - (i & (stride - 1));
-                const int hi = lo + stride;
-                const bool desc = (lo & size) == 0;
-                const uint32_t a = k[lo], b = k[hi];
-                if ((a < b) == desc) {
-                    k[lo] = b;
-                    k[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
 }
 
 __device__ __forceinline__ int next_pow2(int v)
@@ -621,7 +624,7 @@ __host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap)
     L.cpos = take(sizeof(uint16_t) * 4 * lcap);
     L.vprev = take(sizeof(uint16_t) * lcap);
     L.vnew = take(sizeof(uint16_t) * lcap);
-    L.skey = take(sizeof(uint32_t) * p2);
+    L.skey = take(sizeof(uint32_t) * (p2 + 4));   // + padding to whole 16-byte groups (rank sort)
     L.best = take(sizeof(unsigned long long) * lcap);
     L.wsum = take(sizeof(uint32_t) * (QT_NW + 1));
     L.sh = take(sizeof(int) * 16);
@@ -633,6 +636,22 @@ size_t quadtree_smem_bytes(const Geometry& g) { return qt_layout(g.lcap, g.max_c
 
 // shared scalar slots
 enum { SH_N = 0, SH_L, SH_PHASE, SH_M, SH_DONE, SH_KK, SH_ERR, SH_S, SH_C, SH_NEWL };
+
+// ctr[key] += 1 for every lane with key >= 0, one LDS atomic per run of equal keys in consecutive
+// lanes.  Lanes hold consecutive candidates (cell order), which are spatial neighbours and mostly fall
+// into the same node and quadrant: in the first split rounds thousands of keypoints meet at a handful
+// of counters, and one atomic per lane serialises on them.  Called by whole waves (uniform control).
+__device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
+{
+    const int lane = threadIdx.x & 63;
+    const int prev = __builtin_amdgcn_update_dpp(-2, key, 0x138, 0xF, 0xF, false);   // wave_shr:1, lane 0 <- -2
+    const unsigned long long heads = __ballot(key != prev);
+    if (key >= 0 && key != prev) {
+        const unsigned long long later = lane == 63 ? 0ull : heads >> (lane + 1);
+        const int len = later ? (int)__builtin_ctzll(later) + 1 : 64 - lane;
+        atomicAdd(&ctr[key], (uint32_t)len);
+    }
+}
 
 template <int QT_NT, int QT_KPT>
 __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* __restrict__ G,
@@ -647,6 +666,9 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int l = level0 + blockIdx.x, f = blockIdx.y;
     const int tid = threadIdx.x;
+#ifdef ORBX_QT_PROF
+    const long long qt_t0 = clock64();
+#endif
     const LevelGeom& LG = G->lv[l];
     const int lcap = G->lcap;
     const QtLayout Ly = qt_layout(lcap, G->max_cells_level);
@@ -696,13 +718,30 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
         return fslots[cells[cb + lo].slot_base + (i - (int)scan[lo])];
     };
     uint32_t kp[QT_KPT], nd[QT_KPT];
+    // The node arrays (rect .. wsum) are not in use yet: when the level's candidates
+    // fit there, every thread copies whole cells into it (a cell's candidates are contiguous in its
+    // slots) and then reads its own indices, instead of a binary search over the cells plus a
+    // dependent cell-table load per candidate.
+    uint32_t* stage = (uint32_t*)(smem + Ly.rect);
+    // (small levels keep the search: their few hundred candidates spread over few cells, and a
+    // thread's serial copy of a whole cell costs more there than the lanes' parallel searches)
+    const bool staged = n >= 1024 && (size_t)n * 4 <= Ly.wsum - Ly.rect;   // block-uniform; wsum / sh untouched
+    if (staged) {
+        for (int c = tid; c < ncl; c += QT_NT) {
+            const int base = (int)scan[c], cnt = (c + 1 < ncl ? (int)scan[c + 1] : n) - base;
+            const uint32_t* src = fslots + cells[cb + c].slot_base;
+            for (int j = 0; j < cnt; ++j) stage[base + j] = src[j];
+        }
+        __syncthreads();
+    }
 #pragma unroll
     for (int r = 0; r < QT_KPT; ++r) {
         const int i = tid + r * QT_NT;
-        kp[r] = i < n ? fetch(i) : 0u;
+        kp[r] = i < n ? (staged ? stage[i] : fetch(i)) : 0u;
         nd[r] = 0;
     }
-    for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) fspill[i - QT_NT * QT_KPT] = fetch(i);
+    for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) fspill[i - QT_NT * QT_KPT] = staged ? stage[i] : fetch(i);
+    __syncthreads();   // the staging area becomes the node arrays
 
     // visit every keypoint (register part unrolled, spill part in a loop)
     auto visit = [&](auto&& fn) {
@@ -719,19 +758,39 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
         }
     };
 
+#ifdef ORBX_QT_PROF
+    __syncthreads();
+    long long qt_t = 0;
+    if (threadIdx.x == 0) qt_t = qt_t0;
+    QT_STAMP(0, qt_t);
+#endif
     // ---- 2. initial nodes, src/ORBextractor.cc:650-699 ------------------------
     const int nIni = LG.nIni;
     const float hX = LG.hX;
     const int N = LG.nfeat;
     for (int i = tid; i < nIni; i += QT_NT) ccnt[i] = 0;
     __syncthreads();
-    visit([&](uint32_t& k, uint32_t& d, int) {
-        const int x = (int)(k & 0xFFF);
-        int r = (int)((float)x / hX);
-        if (r >= nIni) r = nIni - 1;
-        d = (uint32_t)r;
-        atomicAdd(&ccnt[r], 1u);
-    });
+    auto root_of = [&](uint32_t k) {
+        int r = (int)((float)(int)(k & 0xFFF) / hX);
+        return r >= nIni ? nIni - 1 : r;
+    };
+    const int wave_i0 = tid - (tid & 63);   // this wave's first candidate index in register slot 0
+#pragma unroll
+    for (int r = 0; r < QT_KPT; ++r) {
+        if (wave_i0 + r * QT_NT >= n) break;   // wave-uniform
+        const int i = tid + r * QT_NT;
+        int key = -1;
+        if (i < n) {
+            key = root_of(kp[r]);
+            nd[r] = (uint32_t)key;
+        }
+        wave_run_add(ccnt, key);
+    }
+    for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) {   // spilled candidates
+        const int key = root_of(fspill[i - QT_NT * QT_KPT]);
+        fspill_node[i - QT_NT * QT_KPT] = (uint32_t)key;
+        atomicAdd(&ccnt[key], 1u);
+    }
     __syncthreads();
     if (tid == 0) {
         int L = 0;
@@ -760,9 +819,19 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
     visit([&](uint32_t&, uint32_t& d, int) { d = npos[d]; });
 
     int cur = 0;
+#ifdef ORBX_QT_PROF
+    __syncthreads();
+    QT_STAMP(1, qt_t);
+#endif
     while (true) {
         __syncthreads();
         if (sh[SH_DONE]) break;
+#ifdef ORBX_QT_PROF
+        const int qt_phase = sh[SH_PHASE];
+        if (threadIdx.x == 0) atomicAdd(&g_qt_prof[l][qt_phase == 1 ? 6 : 7], 1ull);
+        long long qr = 0;
+        if (threadIdx.x == 0) qr = clock64();
+#endif
         const int L = sh[SH_L];
         const int phase = sh[SH_PHASE];
         uint32_t* cntc = cntb + (size_t)cur * lcap;
@@ -788,22 +857,41 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
                 npos[p] = (uint16_t)(p - (int)scan[p]);   // rank among non-split nodes
             }
         } else {
-            // phase 2: sort vPrev by (size, creation) and split from the back
+            // phase 2: sort vPrev by (size, creation) descending and split from the front.  The keys
+            // are unique (creation index in the low bits), so an element's place is the number of
+            // larger keys: every thread ranks its elements against the whole key array by broadcast
+            // 16-byte reads, with one barrier in place of a bitonic network's log2(m)^2 / 2 stages.
             m = sh[SH_M];
-            const int p2 = next_pow2(m);
-            for (int k = tid; k < p2; k += QT_NT)
-                skey[k] = k < m ? ((cntc[vprev[k]] << 16) | (uint32_t)k) : 0u;
+            const int m4 = (m + 3) >> 2;
+            for (int k = tid; k < 4 * m4; k += QT_NT)
+                skey[k] = k < m ? ((cntc[vprev[k]] << 16) | (uint32_t)k) : 0u;   // 0: below every key
             for (int p = tid; p < L; p += QT_NT) srank[p] = kNone;
             __syncthreads();
-            block_bitonic_desc<QT_NT>(skey, p2);
-            for (int j = tid; j < m; j += QT_NT) {
-                const int p = vprev[skey[j] & 0xFFFF];
+#ifdef ORBX_QT_PROF
+            long long qs = 0;
+            if (threadIdx.x == 0) qs = clock64();
+#endif
+            const uint4* k4 = (const uint4*)skey;
+            for (int k = tid; k < m; k += QT_NT) {
+                const uint32_t key = skey[k];
+                int j = 0;
+                for (int i4 = 0; i4 < m4; ++i4) {
+                    const uint4 v = k4[i4];
+                    j += (int)(v.x > key) + (int)(v.y > key) + (int)(v.z > key) + (int)(v.w > key);
+                }
+                const int p = vprev[k];
                 srank[p] = (uint16_t)j;
                 snode[j] = (uint16_t)p;
             }
+#ifdef ORBX_QT_PROF
+            if (threadIdx.x == 0) atomicAdd(&g_qt_prof[l][4], (unsigned long long)(clock64() - qs));
+#endif
             S = m;
         }
         __syncthreads();
+#ifdef ORBX_QT_PROF
+        QT_STAMP(3, qr);
+#endif
         // midlines of candidate nodes (ExtractorNode::DivideNode, :572-573)
         for (int s = tid; s < S; s += QT_NT) {
             const int p = snode[s];
@@ -814,15 +902,32 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
             ccnt[4 * s] = ccnt[4 * s + 1] = ccnt[4 * s + 2] = ccnt[4 * s + 3] = 0;
         }
         __syncthreads();
-        visit([&](uint32_t& k, uint32_t& d, int) {
-            const int s = srank[d];
-            if (s != kNone) {
-                const int x = (int)(k & 0xFFF), y = (int)((k >> 12) & 0xFFF);
-                const int q = (x >= smx[s] ? 1 : 0) + (y >= smy[s] ? 2 : 0);
-                atomicAdd(&ccnt[4 * s + q], 1u);
-            }
-        });
+        // a keypoint's child slot 4 * split rank + quadrant is kept in the upper half of its node word
+        // for the relabel below (the lower half is the node's list position)
+        auto child_key = [&](uint32_t k, uint32_t d) {
+            const int s = srank[d & 0xFFFF];
+            if (s == kNone) return -1;
+            const int x = (int)(k & 0xFFF), y = (int)((k >> 12) & 0xFFF);
+            return 4 * s + (x >= smx[s] ? 1 : 0) + (y >= smy[s] ? 2 : 0);
+        };
+#pragma unroll
+        for (int r = 0; r < QT_KPT; ++r) {
+            if (wave_i0 + r * QT_NT >= n) break;   // wave-uniform
+            const int i = tid + r * QT_NT;
+            const int key = i < n ? child_key(kp[r], nd[r]) : -1;
+            nd[r] = (nd[r] & 0xFFFFu) | ((uint32_t)(key + 1) << 16);
+            wave_run_add(ccnt, key);
+        }
+        for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) {
+            uint32_t& d = fspill_node[i - QT_NT * QT_KPT];
+            const int key = child_key(fspill[i - QT_NT * QT_KPT], d);
+            d = (d & 0xFFFFu) | ((uint32_t)(key + 1) << 16);
+            if (key >= 0) atomicAdd(&ccnt[key], 1u);
+        }
         __syncthreads();
+#ifdef ORBX_QT_PROF
+        QT_STAMP(9, qr);
+#endif
 
         // how many candidates are actually split (phase 2 stops once size >= N)
         int kk = S;
@@ -839,7 +944,8 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
                 int cs = 0;
                 for (int q = 0; q < 4; ++q) cs += ccnt[4 * j + q] > 0;
                 const int run = L + (int)scan[j] + cs - (j + 1);   // size after splitting j
-                if (run >= N) atomicMin(&sh[SH_KK], j + 1);
+                // run grows with j (a split node leaves >= 1 child): the one j that crosses N writes
+                if (run >= N && L + (int)scan[j] - j < N) sh[SH_KK] = j + 1;
             }
             __syncthreads();
             kk = sh[SH_KK];
@@ -850,6 +956,9 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
             for (int p = tid; p < L; p += QT_NT) npos[p] = (uint16_t)(p - (int)scan[p]);
             __syncthreads();
         }
+#ifdef ORBX_QT_PROF
+        QT_STAMP(10, qr);
+#endif
 
         // children: count and exclusive offsets over split ranks 0..kk-1
         for (int s = tid; s < kk; s += QT_NT) {
@@ -903,6 +1012,9 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
             }
         }
         __syncthreads();
+#ifdef ORBX_QT_PROF
+        QT_STAMP(11, qr);
+#endif
         // new expandable children in creation order (split rank, then n1..n4)
         for (int e = tid; e < 4 * kk; e += QT_NT) scan[e] = ccnt[e] > 1 ? 1u : 0u;
         __syncthreads();
@@ -910,17 +1022,14 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
         for (int e = tid; e < 4 * kk; e += QT_NT)
             if (ccnt[e] > 1) vnew[scan[e]] = cpos[e];
         // relabel keypoints with their new list position
-        visit([&](uint32_t& k, uint32_t& d, int) {
-            const int s = srank[d];
-            if (s != kNone && s < kk) {
-                const int x = (int)(k & 0xFFF), y = (int)((k >> 12) & 0xFFF);
-                const int q = (x >= smx[s] ? 1 : 0) + (y >= smy[s] ? 2 : 0);
-                d = cpos[4 * s + q];
-            } else {
-                d = npos[d];
-            }
+        visit([&](uint32_t&, uint32_t& d, int) {
+            const int ck = (int)(d >> 16) - 1;   // child slot from the count pass, -1 if the node was not a candidate
+            d = (ck >= 0 && (ck >> 2) < kk) ? cpos[ck] : npos[d & 0xFFFF];
         });
         __syncthreads();
+#ifdef ORBX_QT_PROF
+        QT_STAMP(12, qr);
+#endif
         if (tid == 0) {
             // src/ORBextractor.cc:793-803 and :871-872
             sh[SH_L] = newL;
@@ -935,9 +1044,17 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
         }
         // vnew -> vprev for the next round
         for (int e = tid; e < nexp; e += QT_NT) vprev[e] = vnew[e];
+#ifdef ORBX_QT_PROF
+        QT_STAMP(13, qr);
+#endif
         cur ^= 1;
     }
 
+#ifdef ORBX_QT_PROF
+    // (the round loop's time: stamped at each round's end below would need the phase; charge the
+    // whole loop to slot 2 and let the caller split it with the sort and round counts)
+    QT_STAMP(2, qt_t);
+#endif
     // ---- 4. retain the best keypoint per node (first max wins), :882-906 -----
     const int L = sh[SH_L];
     const bool ok = sh[SH_ERR] == 0;
@@ -962,6 +1079,10 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
     }
     if (tid == 0) {
         qt_cnt[(size_t)f * G->nlevels + l] = outn;
+#ifdef ORBX_QT_PROF
+        QT_STAMP(5, qt_t);
+        atomicAdd(&g_qt_prof[l][8], 1ull);
+#endif
         atomicAdd(&frame_counts[f], outn);
         int err = sh[SH_ERR];
         if (ok && L > LG.cap) err |= kStatusOutOverflow;
@@ -969,42 +1090,55 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
     }
 }
 
+template <int NT, int KPT>
+static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, int l0, int nl, int batch,
+                      size_t smem, hipStream_t s)
+{
+    hipFuncSetAttribute((const void*)k_quadtree<NT, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL((k_quadtree<NT, KPT>), dim3(nl, batch), dim3(NT), smem, s, l0, b.geom, b.cells, b.slots,
+                       b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+}
+
+#ifdef ORBX_QT_PROF
+}  // namespace orbx
+extern "C" int orbx_debug_qt_prof(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_qt_prof), sizeof(orbx::g_qt_prof)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[16][16];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(orbx::g_qt_prof), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+namespace orbx {
+#endif
+
 void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s)
 {
     const size_t smem = quadtree_smem_bytes(g);
-    // register capacity per level (qt_kpt): level 0 holds most candidates; levels >= 2 hold a
-    // few hundred, and their small register file lets describe / FAST waves share the CU
-    hipFuncSetAttribute((const void*)k_quadtree<512, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipFuncSetAttribute((const void*)k_quadtree<512, 24>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipFuncSetAttribute((const void*)k_quadtree<512, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipFuncSetAttribute((const void*)k_quadtree<256, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     // Small batches (the per-frame host path): one launch of the level-0 kernel over every level, so
-    // the levels run concurrently instead of as three dependent launches (latency, not throughput).
+    // the levels run concurrently instead of as dependent launches (latency, not throughput).
     // A level run with more register capacity than qt_regcap(g, l) spills less than its region holds.
     if (batch <= kQtMergedMaxBatch) {
         if (g.qt_kpt0 == 24)
-            hipLaunchKernelGGL((k_quadtree<512, 24>), dim3(g.nlevels, batch), dim3(512), smem, s, 0, b.geom, b.cells,
-                               b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts,
-                               b.status);
+            qt_launch<512, 24>(g, b, frame_counts, 0, g.nlevels, batch, smem, s);
         else
-            hipLaunchKernelGGL((k_quadtree<512, 16>), dim3(g.nlevels, batch), dim3(512), smem, s, 0, b.geom, b.cells,
-                               b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts,
-                               b.status);
+            qt_launch<512, 16>(g, b, frame_counts, 0, g.nlevels, batch, smem, s);
         return;
     }
-    // the launched templates must match qt_regcap(g, l), which sizes the spill regions
-    if (g.qt_kpt0 == 24)
-        hipLaunchKernelGGL((k_quadtree<512, 24>), dim3(1, batch), dim3(512), smem, s, 0, b.geom, b.cells, b.slots,
-                           b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
-    else
-        hipLaunchKernelGGL((k_quadtree<512, 16>), dim3(1, batch), dim3(512), smem, s, 0, b.geom, b.cells, b.slots,
-                           b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
-    if (g.nlevels > 1)
-        hipLaunchKernelGGL((k_quadtree<512, 8>), dim3(1, batch), dim3(512), smem, s, 1, b.geom, b.cells, b.slots,
-                           b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
-    if (g.nlevels > 2)
-        hipLaunchKernelGGL((k_quadtree<256, 4>), dim3(g.nlevels - 2, batch), dim3(256), smem, s, 2, b.geom, b.cells,
-                           b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+    // one launch per run of consecutive levels with the same configuration; the launched template is
+    // exactly qt_nt / qt_kpt, which size the spill regions
+    for (int l0 = 0; l0 < g.nlevels;) {
+        const int nt = qt_nt(g, l0), kpt = qt_kpt(g, l0);
+        int l1 = l0 + 1;
+        while (l1 < g.nlevels && qt_nt(g, l1) == nt && qt_kpt(g, l1) == kpt) ++l1;
+        const int nl = l1 - l0;
+        if (nt == 512 && kpt == 24) qt_launch<512, 24>(g, b, frame_counts, l0, nl, batch, smem, s);
+        else if (nt == 512 && kpt == 16) qt_launch<512, 16>(g, b, frame_counts, l0, nl, batch, smem, s);
+        else if (nt == 512) qt_launch<512, 8>(g, b, frame_counts, l0, nl, batch, smem, s);
+        else qt_launch<256, 4>(g, b, frame_counts, l0, nl, batch, smem, s);
+        l0 = l1;
+    }
 }
 
 // ---------------------------------------------------------------------------

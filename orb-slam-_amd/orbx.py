@@ -22,7 +22,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liborbx.so")
+# ORBX_LIB: an instrumented build of the same library for profiling experiments (tools/diag)
+LIB_PATH = os.environ.get("ORBX_LIB") or os.path.join(_HERE, "liborbx.so")
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])

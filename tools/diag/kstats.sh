@@ -1,0 +1,12 @@
+# per-kernel average durations of one-stream bench steps (rocprofv3 kernel trace), for quick A/B checks
+#   bash tools/diag/kstats.sh TAG [bench args...]
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+TAG=$1; shift
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/ks_$TAG -o run -- python3 $R/bench.py --no-cpu --streams 1 --iso-steps 0 --host-steps 0 --steps 20 "$@" > $R/gpurun_out/ks_$TAG.json 2> $R/gpurun_out/ks_$TAG.err || { tail -5 $R/gpurun_out/ks_$TAG.err; exit 1; }
+python3 - $R/gpurun_out/ks_$TAG/run_kernel_stats.csv <<'PY'
+import csv, sys
+for r in list(csv.DictReader(open(sys.argv[1])))[:12]:
+    print("%-34s %6s calls  avg %9.1f us" % (r["Name"].split("(")[0].replace("void ", "")[:34], r["Calls"], float(r["AverageNs"]) / 1e3))
+PY

@@ -35,6 +35,18 @@ __device__ __forceinline__ void op(uint32_t& r, uint32_t b, uint32_t c)
     else if constexpr (K == 5) OP3("v_alignbyte_b32");
     else if constexpr (K == 6) OP3("v_fma_f32");
     else if constexpr (K == 7) OP3("v_pk_minimum3_f16");
+    else if constexpr (K == 8) OP2("v_pk_max_f16");
+    else if constexpr (K == 9) OP2("v_pk_add_u16");
+    else if constexpr (K == 10) OP3("v_max3_u32");
+    else if constexpr (K == 11) OP2("v_max_u32");
+    else if constexpr (K == 12) OP3("v_dot2_u32_u16");
+    else if constexpr (K == 13) OP3("v_lshl_or_b32");
+    else if constexpr (K == 14) OP3("v_add3_u32");
+    else if constexpr (K == 15) OP2("v_mul_lo_u32");
+    else if constexpr (K == 16) OP3("v_mad_u32_u24");
+    else if constexpr (K == 17) OP3("v_sad_u32");
+    else if constexpr (K == 18) OP3("v_bfi_b32");
+    else if constexpr (K == 19) OP2("v_pk_sub_u16");
 }
 
 template <int K>
@@ -85,13 +97,16 @@ int main()
     const int cus = p.multiProcessorCount;
     uint32_t* out = nullptr;
     CHECK(hipMalloc(&out, sizeof(uint32_t) * 256 * cus * 8));
-    const char* names[8] = {"v_pk_maximum3_f16", "v_perm_b32", "v_xor_b32", "v_bcnt_u32_b32",
-                            "v_dot4_u32_u8", "v_alignbyte_b32", "v_fma_f32", "v_pk_minimum3_f16"};
+    constexpr int kOps = 20;
+    const char* names[kOps] = {"v_pk_maximum3_f16", "v_perm_b32", "v_xor_b32", "v_bcnt_u32_b32", "v_dot4_u32_u8",
+                               "v_alignbyte_b32", "v_fma_f32", "v_pk_minimum3_f16", "v_pk_max_f16", "v_pk_add_u16",
+                               "v_max3_u32", "v_max_u32", "v_dot2_u32_u16", "v_lshl_or_b32", "v_add3_u32",
+                               "v_mul_lo_u32", "v_mad_u32_u24", "v_sad_u32", "v_bfi_b32", "v_pk_sub_u16"};
     const double clk = p.clockRate * 1e3;   // Hz
     std::printf("{\"cus\": %d, \"clock_mhz\": %.0f, \"issue_peak_2cyc\": %.1f, \"rates\": {", cus, clk / 1e6,
                 cus * 4 * clk / 2 / 1e9);
     const int occ[4] = {1, 2, 4, 8};
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kOps; ++k) {
         std::printf("%s\"%s\": [", k ? ", " : "", names[k]);
         for (int o = 0; o < 4; ++o) {
             double g = 0;
@@ -104,6 +119,18 @@ int main()
                 case 5: g = run<5>(occ[o], cus, out); break;
                 case 6: g = run<6>(occ[o], cus, out); break;
                 case 7: g = run<7>(occ[o], cus, out); break;
+                case 8: g = run<8>(occ[o], cus, out); break;
+                case 9: g = run<9>(occ[o], cus, out); break;
+                case 10: g = run<10>(occ[o], cus, out); break;
+                case 11: g = run<11>(occ[o], cus, out); break;
+                case 12: g = run<12>(occ[o], cus, out); break;
+                case 13: g = run<13>(occ[o], cus, out); break;
+                case 14: g = run<14>(occ[o], cus, out); break;
+                case 15: g = run<15>(occ[o], cus, out); break;
+                case 16: g = run<16>(occ[o], cus, out); break;
+                case 17: g = run<17>(occ[o], cus, out); break;
+                case 18: g = run<18>(occ[o], cus, out); break;
+                case 19: g = run<19>(occ[o], cus, out); break;
             }
             std::printf("%s%.1f", o ? ", " : "", g);
         }
