@@ -330,7 +330,18 @@ struct SiWindow {
     float x, y, r;
 };
 
-__device__ __forceinline__ SiWindow si_window(const uint32_t* keys, int ng, float2 c, float r, const orbm_grid& G)
+// first key of every grid column (keys are sorted by column-major cell): colstart[c] for c = 0..64
+__device__ __forceinline__ void si_colstart(const uint32_t* keys, int ng, int* colstart, int tid, int nt)
+{
+    for (int g = tid; g <= ng; g += nt) {
+        const int cp = g > 0 ? (int)(keys[g - 1] >> 16) / kGridRows : -1;
+        const int cc = g < ng ? (int)(keys[g] >> 16) / kGridRows : kGridCols;
+        for (int c = cp + 1; c <= cc; ++c) colstart[c] = g;
+    }
+}
+
+__device__ __forceinline__ SiWindow si_window(const uint32_t* keys, int ng, float2 c, float r, const orbm_grid& G,
+                                              const int* colstart = nullptr)
 {
     SiWindow w;
     const float x = c.x, y = c.y;
@@ -343,8 +354,13 @@ __device__ __forceinline__ SiWindow si_window(const uint32_t* keys, int ng, floa
     w.cy1 = min(kGridRows - 1, (int)ceilf((y - G.min_y + r) * G.grid_h_inv));
     w.lo = w.hi = 0;
     if (cx0 < kGridCols && cx1 >= 0 && w.cy0 < kGridRows && w.cy1 >= 0) {
-        w.lo = lower_bound_u32(keys, ng, (uint32_t)(cx0 * kGridRows) << 16);
-        w.hi = lower_bound_u32(keys, ng, (uint32_t)((cx1 + 1) * kGridRows) << 16);
+        if (colstart) {   // two independent table reads instead of two binary searches
+            w.lo = colstart[cx0];
+            w.hi = colstart[cx1 + 1];
+        } else {
+            w.lo = lower_bound_u32(keys, ng, (uint32_t)(cx0 * kGridRows) << 16);
+            w.hi = lower_bound_u32(keys, ng, (uint32_t)((cx1 + 1) * kGridRows) << 16);
+        }
     }
     return w;
 }
@@ -375,10 +391,13 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
     const int n10 = gn[2 * fa], ng = gn[2 * fb + 1];
     uint32_t* keys = (uint32_t*)smem;
     float2* xy = (float2*)(smem + (((size_t)cap * 4 + 15) & ~(size_t)15));
+    __shared__ int colstart[kGridCols + 1];
     for (int g = tid; g < ng; g += SI_BUILD_NT) {
         keys[g] = gkeys[(size_t)fb * cap + g];
         xy[g] = gxy[(size_t)fb * cap + g];
     }
+    __syncthreads();
+    si_colstart(keys, ng, colstart, tid, SI_BUILD_NT);
     __syncthreads();
     const orbx_keypoint* k1 = kps + (size_t)fa * cap;
     const uint8_t* d1 = desc + (size_t)fa * cap * 32;
@@ -390,7 +409,7 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
         const ulonglong2 a0 = a[0], a1 = a[1];
         // window centre vbPrevMatched[i1] (src/ORBmatcher.cc:456-460); F1's own keypoint when not given
         const float2 c = pv ? pv[i1] : make_float2(k1[i1].x, k1[i1].y);
-        const SiWindow w = si_window(keys, ng, c, (float)window, G);
+        const SiWindow w = si_window(keys, ng, c, (float)window, G, colstart);
         // lane-local 4 smallest (Hamming << 16 | visit position), with their i2
         uint32_t hk[SI_TOPK], hi2[SI_TOPK];
 #pragma unroll

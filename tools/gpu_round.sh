@@ -21,9 +21,9 @@ timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo BENC
 cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
 # one stream: kernel durations are the kernels' own (bench.py's roofline timing)
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu --streams 1 > $O/bench_prof.json 2> $O/bench_prof.err || { echo PROF_FAIL; tail -20 $O/bench_prof.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-cpu --streams 1 --host-steps 0 > $O/bench_prof.json 2> $O/bench_prof.err || { echo PROF_FAIL; tail -20 $O/bench_prof.err; exit 1; }
 # the pipelined default command as well (durations stretched by the concurrent streams)
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_pipelined -o run -- python3 $R/bench.py --no-cpu > $O/bench_prof_pipelined.json 2> $O/bench_prof_pipelined.err || { echo PROF_FAIL; tail -20 $O/bench_prof_pipelined.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_pipelined -o run -- python3 $R/bench.py --no-cpu --host-steps 0 > $O/bench_prof_pipelined.json 2> $O/bench_prof_pipelined.err || { echo PROF_FAIL; tail -20 $O/bench_prof_pipelined.err; exit 1; }
 python3 - $O/prof/run_kernel_stats.csv <<'PY'
 import csv, sys
 for r in list(csv.DictReader(open(sys.argv[1])))[:14]:
