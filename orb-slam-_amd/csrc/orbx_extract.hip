@@ -1170,7 +1170,7 @@ constexpr int kDescPerWave = 4;                       // keypoints per wave (lan
 // Horizontal-pass items (row pair rp << 8 | column group cg) that BRIEF can read: a sample
 // (18 + xx, 18 + yy) has |(x, y)| <= 18.39 before rounding (the pattern's largest radius), so a
 // column group needs only the row pairs its disc chord reaches, plus the 7-tap reach of
-// blur_at.  189 of the 22 x 10 items: three per lane, row-pair major so that the lanes of a
+// blur_acc.  189 of the 22 x 10 items: three per lane, row-pair major so that the lanes of a
 // load read neighbouring raw dwords (distinct LDS banks).
 __constant__ uint16_t c_blur_items[192] = {2,3,4,5,6,257,258,259,260,261,262,263,513,514,515,516,517,518,519,768,769,770,771,772,773,774,775,776,1024,1025,1026,1027,1028,1029,1030,1031,1032,1280,1281,1282,1283,1284,1285,1286,1287,1288,1536,1537,1538,1539,1540,1541,1542,1543,1544,1545,1792,1793,1794,1795,1796,1797,1798,1799,1800,1801,2048,2049,2050,2051,2052,2053,2054,2055,2056,2057,2304,2305,2306,2307,2308,2309,2310,2311,2312,2313,2560,2561,2562,2563,2564,2565,2566,2567,2568,2569,2816,2817,2818,2819,2820,2821,2822,2823,2824,2825,3072,3073,3074,3075,3076,3077,3078,3079,3080,3081,3328,3329,3330,3331,3332,3333,3334,3335,3336,3337,3584,3585,3586,3587,3588,3589,3590,3591,3592,3593,3840,3841,3842,3843,3844,3845,3846,3847,3848,3849,4096,4097,4098,4099,4100,4101,4102,4103,4104,4352,4353,4354,4355,4356,4357,4358,4359,4360,4609,4610,4611,4612,4613,4614,4615,4616,4865,4866,4867,4868,4869,4870,4871,5122,5123,5124,5125,5126,5127,5379,5380,5381,5382,65535,65535,65535};
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
@@ -1203,24 +1203,33 @@ __device__ __forceinline__ ushort2_t as_us2(uint32_t v)
     return r;
 }
 
-// blurred value at patch row y (0..36), column x (0..36): sum_t k[t] * rowblur[y+t][x]
-__device__ __forceinline__ int blur_at(const uint32_t* rowT, int y, int x)
+// Sample coordinates as float bits: fl + 1.5 * 2^23 rounds fl to the nearest integer, ties to even
+// (one f32 addition into [2^23, 2^24), whose ulp is 1; the magic number is even, so the tie parity
+// is fl's), exactly __float2int_rn for |fl| < 2^22, and leaves that integer in the low mantissa
+// bits: bits = 0x4B400000 + round(fl).  The blur lookup indexes with these bits directly.
+constexpr float kRoundMagic = 12582912.0f;
+constexpr uint32_t kRoundBits = 0x4B400000u;
+
+// blurred value at patch row 18 + yy, column 18 + xx (|xx|, |yy| <= 19, given as kRoundMagic
+// bits by, bx): sum_t k[t] * rowblur[y+t][x], + 2^15 (the >> 16 rounding) folded into the sum.
+// The dword index (18 + xx) * kTP + ((18 + yy) >> 1) is kBlurIdx0 + (by >> 1) + bx * kTP in
+// wrapping u32 arithmetic (bx as its low 24 bits, 0x400000 + xx).
+constexpr uint32_t kBlurIdx0 = 9u - (kRoundBits >> 1) + (18u - (kRoundBits & 0xFFFFFFu)) * (uint32_t)kTP;
+__device__ __forceinline__ uint32_t blur_acc(const uint32_t* rowT, uint32_t by, uint32_t bx)
 {
-    const uint32_t* col = rowT + x * kTP;
-    const int base = y >> 1;
-    const uint32_t d0 = col[base], d1 = col[base + 1], d2 = col[base + 2], d3 = col[base + 3];
+    const uint32_t idx = kBlurIdx0 + (by >> 1) + __umul24(bx, (uint32_t)kTP);   // < 40 * kTP
+    const uint32_t* col = rowT + idx;
+    const uint32_t d0 = col[0], d1 = col[1], d2 = col[2], d3 = col[3];
     // even y: rows y..y+6 = (d0.lo d0.hi d1.lo d1.hi d2.lo d2.hi d3.lo); odd y: (d0.hi .. d3.hi)
-    const bool odd = y & 1;
+    const bool odd = by & 1u;
     const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
     const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
     const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
     const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
-    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), w0, 0u, false);
+    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), w0, 1u << 15, false);
     acc = __builtin_amdgcn_udot2(as_us2(d1), w1, acc, false);
     acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
-    acc = __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
-    const int v = (int)((acc + (1u << 15)) >> 16);
-    return v > 255 ? 255 : v;
+    return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
 }
 
 __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
@@ -1392,18 +1401,19 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
         const float ang = angle * kFactorPI;
         float a, b;
         glibc_sincosf_pair(ang, &b, &a);   // a = cosf, b = sinf (src/ORBextractor.cc:148)
+        // GaussianBlur's u8 saturation: min(t0, 255) < min(t1, 255) iff t0 < min(t1, 255)
         unsigned long long words[4];
 #pragma unroll
         for (int wd = 0; wd < 4; ++wd) {
-            int t2[2];
+            uint32_t t2[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const float px = ppx[2 * wd + e], py = ppy[2 * wd + e];
-                const int yy = __float2int_rn(__builtin_fmaf(px, b, py * a));
-                const int xx = __float2int_rn(__builtin_fmaf(px, a, -(py * b)));
-                t2[e] = blur_at(rowT, 18 + yy, 18 + xx);
+                const uint32_t by = __float_as_uint(__builtin_fmaf(px, b, py * a) + kRoundMagic);
+                const uint32_t bx = __float_as_uint(__builtin_fmaf(px, a, -(py * b)) + kRoundMagic);
+                t2[e] = blur_acc(rowT, by, bx) >> 16;
             }
-            words[wd] = __ballot(t2[0] < t2[1]);
+            words[wd] = __ballot(t2[0] < (t2[1] < 255u ? t2[1] : 255u));
         }
         const size_t o = (size_t)f * cap + oidx;
         if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
