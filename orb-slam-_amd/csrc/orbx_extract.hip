@@ -13,9 +13,6 @@
 
 namespace orbx {
 
-__constant__ int c_pattern[1024] = {
-#include "orb_pattern.inc"
-};
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -1173,7 +1170,47 @@ constexpr int kDescPerWave = 4;                       // keypoints per wave (lan
 // blur_acc.  189 of the 22 x 10 items: three per lane, row-pair major so that the lanes of a
 // load read neighbouring raw dwords (distinct LDS banks).
 __constant__ uint16_t c_blur_items[192] = {2,3,4,5,6,257,258,259,260,261,262,263,513,514,515,516,517,518,519,768,769,770,771,772,773,774,775,776,1024,1025,1026,1027,1028,1029,1030,1031,1032,1280,1281,1282,1283,1284,1285,1286,1287,1288,1536,1537,1538,1539,1540,1541,1542,1543,1544,1545,1792,1793,1794,1795,1796,1797,1798,1799,1800,1801,2048,2049,2050,2051,2052,2053,2054,2055,2056,2057,2304,2305,2306,2307,2308,2309,2310,2311,2312,2313,2560,2561,2562,2563,2564,2565,2566,2567,2568,2569,2816,2817,2818,2819,2820,2821,2822,2823,2824,2825,3072,3073,3074,3075,3076,3077,3078,3079,3080,3081,3328,3329,3330,3331,3332,3333,3334,3335,3336,3337,3584,3585,3586,3587,3588,3589,3590,3591,3592,3593,3840,3841,3842,3843,3844,3845,3846,3847,3848,3849,4096,4097,4098,4099,4100,4101,4102,4103,4104,4352,4353,4354,4355,4356,4357,4358,4359,4360,4609,4610,4611,4612,4613,4614,4615,4616,4865,4866,4867,4868,4869,4870,4871,5122,5123,5124,5125,5126,5127,5379,5380,5381,5382,65535,65535,65535};
-__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+constexpr int kPattern[1024] = {
+#include "orb_pattern.inc"
+};
+
+// Keypoint-independent lane state of k_describe, a function of the lane alone, built at compile time
+// (the kernel loads it instead of computing ~235 VALU instructions per wave).
+//   IC_Angle: lane 2i + h owns disc row v = i - 15 (i < 31), half h: u = -15..0 or 1..15, as 4
+//   realigned dwords of the raw row dotted (v_dot4_u32_u8) with per-lane weights that are zero
+//   outside |u| <= umax[|v|]: w1 = (u + 16) for m10 (minus 16 * sum I), w0 = 1 for sum I.
+//   rBRIEF: the lane's 8 pattern points (tests m = 64 wd + lane, wd = q >> 1; e = q & 1), as floats.
+struct DescLane {
+    uint32_t w1[4], w0[4];
+    float px[8], py[8];
+};
+struct DescLaneTable {
+    DescLane l[64];
+};
+constexpr DescLaneTable make_desc_lanes()
+{
+    DescLaneTable t{};
+    for (int lane = 0; lane < 64; ++lane) {
+        const int icv = lane >> 1, ich = lane & 1, vrow = icv - 15;
+        const int rmax = icv < 31 ? kUmax[vrow < 0 ? -vrow : vrow] : -1;
+        for (int k = 0; k < 4; ++k)
+            for (int b = 0; b < 4; ++b) {
+                const int uu = (ich ? 1 : -15) + 4 * k + b;
+                if (uu <= (ich ? 15 : 0) && (uu < 0 ? -uu : uu) <= rmax) {
+                    t.l[lane].w1[k] |= (uint32_t)(uu + 16) << (8 * b);
+                    t.l[lane].w0[k] |= 1u << (8 * b);
+                }
+            }
+        for (int q = 0; q < 8; ++q) {
+            const int m = (q >> 1) * 64 + lane, e = q & 1;
+            t.l[lane].px[q] = (float)kPattern[4 * m + 2 * e];
+            t.l[lane].py[q] = (float)kPattern[4 * m + 2 * e + 1];
+        }
+    }
+    return t;
+}
+__constant__ DescLaneTable c_desc_lanes = make_desc_lanes();
 
 __device__ __forceinline__ int reflect101(int p, int len)
 {
@@ -1250,39 +1287,26 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
     uint32_t* rowT = s_rowT[wave];
     const int g0 = (bx * 4 + wave) * kDescPerWave;
 
-    // ---- keypoint-independent lane state, set up once for the wave's keypoints ----
-    // IC_Angle: lane 2i + h owns disc row v = i - 15 (i < 31), half h: u = -15..0 or 1..15, as
-    // 4 realigned dwords of the raw row dotted (v_dot4_u32_u8) with per-lane weights that are
-    // zero outside |u| <= umax[|v|]: (u + 16) for m10 (minus 16 * sum I) and 1 for sum I.
+    // ---- keypoint-independent lane state (c_desc_lanes), loaded once for the wave's keypoints ----
     const int icv = lane >> 1, ich = lane & 1;
     const int vrow = icv - 15;
-    const int rmax = icv < 31 ? c_umax[vrow < 0 ? -vrow : vrow] : -1;
+    const DescLane& DL = c_desc_lanes.l[lane];
     uint32_t W1[4], W0[4];
+    float ppx[8], ppy[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        W1[k] = 0u;
-        W0[k] = 0u;
+        W1[k] = DL.w1[k];
+        W0[k] = DL.w0[k];
+    }
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int uu = (ich ? 1 : -15) + 4 * k + b;
-            if (uu <= (ich ? 15 : 0) && (uu < 0 ? -uu : uu) <= rmax) {
-                W1[k] |= (uint32_t)(uu + 16) << (8 * b);
-                W0[k] |= 1u << (8 * b);
-            }
-        }
+    for (int q = 0; q < 8; ++q) {
+        ppx[q] = DL.px[q];
+        ppy[q] = DL.py[q];
     }
     const int ic_row = 21 + vrow, ic_col = ich ? 22 : 6;   // raw row, patch column of the first pixel
     int bitem[3];
 #pragma unroll
     for (int it = 0; it < 3; ++it) bitem[it] = c_blur_items[lane + 64 * it];
-    // rBRIEF: this lane's 8 tests (word wd = lane + 64 wd), pattern points as floats
-    float ppx[8], ppy[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int m = (q >> 1) * 64 + lane, e = q & 1;
-        ppx[q] = (float)c_pattern[4 * m + 2 * e];
-        ppy[q] = (float)c_pattern[4 * m + 2 * e + 1];
-    }
 
     // output index g (level-major, as the reference concatenates levels) -> level, keypoint.
     // The wave's indices are consecutive, so past the frame's total the rest are too.
