@@ -1161,6 +1161,12 @@ constexpr int kRawD = 13;                             // dwords loaded per raw r
 constexpr int kRawP = 64;                             // LDS row pitch (bytes): 4 rows per 64-lane DMA
 constexpr int kRawRows = 44;                          // 43 rows used
 constexpr int kRawSlots = kRawRows * kRawP / 4;
+// LDS row slot of raw row r (an involution).  With a 16-dword pitch, rows 2 apart share their
+// banks; swapping rows 4k + 2 and 4k + 3 puts the even (odd) rows of consecutive row pairs on
+// alternate bank halves, which halves the horizontal pass's bank conflicts (208 -> 112 LDS cycles
+// per keypoint, tools/diag model).  The DMA applies it per lane for free: slot 4t + q holds row
+// 4t + (q ^ (q >> 1)).
+__host__ __device__ constexpr int raw_slot(int r) { return r ^ ((r >> 1) & 1); }
 constexpr int kTCols = 40, kTP = 22;                  // row-blurred, transposed: [col][row pairs], 22 dwords/col
 constexpr int kDescPerWave = 4;                       // keypoints per wave (lane state set up once per wave)
 
@@ -1339,7 +1345,9 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
             const uint8_t* ub = (const uint8_t*)(s0 & ~(uintptr_t)3);   // wave-uniform, aligned
             sb = (int)(s0 & 3);
             sp = pitch & 3;
-            const int rr = lane >> 4, kk = min(lane & 15, kRawD - 1);
+            // slot row 4t + (lane >> 4) receives source row 4t + rr (raw_slot); row 43 (slot 42)
+            // repeats row 42
+            const int rr = raw_slot(lane >> 4), kk = min(lane & 15, kRawD - 1);
             const uint32_t off = (uint32_t)((sb + rr * pitch) & ~3) + 4u * kk;
 #pragma unroll
             for (int t = 0; t < kRawRows / 4; ++t) {
@@ -1351,9 +1359,9 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
         } else {
             sb = 0;
             sp = 0;
-            for (int i = lane; i < 43 * kRawP; i += 64) {
-                const int r = i / kRawP, c = i - r * kRawP;
-                const int X = reflect101(cx - 21 + c, w), Y = reflect101(cy - 21 + r, h);
+            for (int i = lane; i < kRawRows * kRawP; i += 64) {
+                const int r = raw_slot(min(i / kRawP, 43)), c = i - (i / kRawP) * kRawP;   // slot -> row
+                const int X = reflect101(cx - 21 + c, w), Y = reflect101(cy - 21 + min(r, 42), h);
                 raw[i] = img[(size_t)Y * pitch + X];
             }
         }
@@ -1374,7 +1382,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
         wave_lds_sync();
 
         // IC_Angle (src/ORBextractor.cc:84-128): integer moments over the disc, any order
-        const int icb0 = ic_row * kRawP + ((csb + ic_row * csp) & 3) + ic_col;
+        const int icb0 = raw_slot(ic_row) * kRawP + ((csb + ic_row * csp) & 3) + ic_col;
         const uint32_t* icq = raw32 + (icb0 >> 2);
         const uint32_t icsh = (uint32_t)(icb0 & 3);
         const uint32_t q0 = icq[0], q1 = icq[1], q2 = icq[2], q3 = icq[3], q4 = icq[4];
@@ -1401,7 +1409,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * rp + e;
                 const uint32_t sh = (uint32_t)((csb + r * csp) & 3);
-                const uint32_t* rr = raw32 + r * (kRawP / 4) + cg;
+                const uint32_t* rr = raw32 + raw_slot(r) * (kRawP / 4) + cg;
                 const uint32_t W0 = rr[0], W1 = rr[1], W2 = rr[2], W3 = rr[3];
                 const uint32_t R0 = __builtin_amdgcn_alignbyte(W1, W0, sh);
                 const uint32_t R1 = __builtin_amdgcn_alignbyte(W2, W1, sh);
