@@ -213,6 +213,14 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
             L.xtab_off = (int)xt.size();
             L.ytab_off = (int)yt.size();
             resize_tables(prev_w, prev_h, L.w, L.h, xt, yt);
+            L.pyr_win = 1;
+            for (int g0 = 0; g0 < L.w; g0 += 4) {   // k_pyramid_level's byte window per 4-column group
+                const int first = xt[L.xtab_off + g0].x & 0xFFFF;
+                for (int k = 0; k < 4; ++k) {
+                    const int x = xt[L.xtab_off + std::min(g0 + k, L.w - 1)].x;
+                    if ((x & 0xFFFF) < first || (x >> 16) - first > 7) L.pyr_win = 0;
+                }
+            }
         }
         prev_w = L.w;
         prev_h = L.h;

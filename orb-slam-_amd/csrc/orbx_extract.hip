@@ -38,13 +38,25 @@ __device__ __forceinline__ const uint8_t* level_base(const FramePtrs& P, const G
     return P.pyr + (size_t)f * P.pyr_fstride + G->lv[l].pyr_off;
 }
 
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ ushort2_t as_us2(uint32_t v)
+{
+    ushort2_t r;
+    r.x = (unsigned short)(v & 0xFFFF);
+    r.y = (unsigned short)(v >> 16);
+    return r;
+}
+
 // ---------------------------------------------------------------------------
 // K1: level l from level l-1, cv::resize INTER_LINEAR u8 fixed point
 // (11-bit coefficients, 22-bit vertical rounding) — SURVEY.md A.2.
 // Coefficient tables are built on the host exactly like OpenCV builds them.
 // ---------------------------------------------------------------------------
 constexpr int kPyrRows = 8;
+constexpr int kPyrLd = 8;   // staged dwords in flight per thread
 
+template <bool kWin>
 __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
                                                        const int2* __restrict__ xtab,
                                                        const int2* __restrict__ ytab)
@@ -71,17 +83,34 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
         (const __attribute__((address_space(1))) uint8_t*)((uintptr_t)src & ~(uintptr_t)3);
     const uint32_t o0 = (uint32_t)((uintptr_t)src & 3) + (uint32_t)sy0 * (uint32_t)spitch;
     const float inv_nd = 1.0f / (float)nd;
-    for (int i = threadIdx.x; i < nrows * nd; i += 256) {
-        const int r = (int)(((float)i + 0.5f) * inv_nd), k = i - __mul24(r, nd);
-        const uint32_t o = o0 + __umul24((uint32_t)r, (uint32_t)spitch) + 4u * (uint32_t)k;
-        const __attribute__((address_space(1))) uint32_t* ap =
-            (const __attribute__((address_space(1))) uint32_t*)(base + (o & ~3u));
-        // the second dword is needed only if some of its bytes belong to the row; an aligned
-        // dword that starts inside the row cannot run past the (4-byte aligned) buffer end
-        const uint32_t sh = o & 3u;
-        const bool tail = sh == 0 || 4 * k + 4 - (int)sh >= sw;
-        const uint32_t lo = ap[0], hi = tail ? 0u : ap[1];
-        s_src[r * nd + k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    // kPyrLd dwords per thread in flight: every load of a batch is issued before the first is used
+    // (one dependent load per dword left each thread waiting ~14 HBM latencies per block at level 1)
+    const int total = nrows * nd;
+    for (int i0 = threadIdx.x; i0 < total; i0 += 256 * kPyrLd) {
+        uint32_t lo[kPyrLd], hi[kPyrLd], sh[kPyrLd];
+        int dst[kPyrLd];
+#pragma unroll
+        for (int u = 0; u < kPyrLd; ++u) {
+            const int i = i0 + 256 * u;
+            dst[u] = -1;
+            if (i < total) {
+                const int r = (int)(((float)i + 0.5f) * inv_nd), k = i - __mul24(r, nd);
+                const uint32_t o = o0 + __umul24((uint32_t)r, (uint32_t)spitch) + 4u * (uint32_t)k;
+                const __attribute__((address_space(1))) uint32_t* ap =
+                    (const __attribute__((address_space(1))) uint32_t*)(base + (o & ~3u));
+                // the second dword is needed only if some of its bytes belong to the row; an aligned
+                // dword that starts inside the row cannot run past the (4-byte aligned) buffer end, so a
+                // tail re-reads the first (alignbyte by 0 ignores it, and bytes past the row are never read)
+                sh[u] = o & 3u;
+                const bool tail = sh[u] == 0 || 4 * k + 4 - (int)sh[u] >= sw;
+                lo[u] = ap[0];
+                hi[u] = ap[tail ? 0 : 1];
+                dst[u] = r * nd + k;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kPyrLd; ++u)
+            if (dst[u] >= 0) s_src[dst[u]] = __builtin_amdgcn_alignbyte(hi[u], lo[u], sh[u]);
     }
     __syncthreads();
     const uint8_t* S = (const uint8_t*)s_src;
@@ -105,6 +134,42 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
             x1[k] = (int)((uint32_t)xt.x >> 16);
             a0[k] = (uint32_t)xt.y & 0xFFFFu;
             a1[k] = (uint32_t)xt.y >> 16;
+        }
+        if constexpr (kWin) {
+            // The group's 8 taps lie in the 8 bytes from x0[0] (LevelGeom::pyr_win, checked on the host):
+            // per source row three dword reads, realigned to x0[0] by two alignbytes; each column's tap
+            // pair is one v_perm into a u16 pair and one v_dot2_u32_u16 with (a0, a1)
+            const uint32_t wb = (uint32_t)(x0[0] & ~3), wo = (uint32_t)(x0[0] & 3);
+            uint32_t sel[4], ak[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                sel[k] = (uint32_t)(x0[k] - x0[0]) | 0x0C00u | ((uint32_t)(x1[k] - x0[0]) << 16) | 0x0C000000u;
+                ak[k] = a0[k] | (a1[k] << 16);
+            }
+            auto hrow = [&](const uint8_t* row, uint32_t h[4]) {
+                const uint32_t* q = (const uint32_t*)(row + wb);
+                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+                const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, wo), e1 = __builtin_amdgcn_alignbyte(d2, d1, wo);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    h[k] = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(e1, e0, sel[k])), as_us2(ak[k]), 0u,
+                                                  false);
+            };
+            for (int rr = 0; rr < dyn; ++rr) {
+                const int2 yt = ytab[D.ytab_off + dy0 + rr];
+                const uint32_t b0 = (uint32_t)yt.y & 0xFFFFu, b1 = (uint32_t)yt.y >> 16;
+                uint32_t h0[4], h1[4];
+                hrow(S + ((yt.x & 0xFFFF) - sy0) * srow, h0);
+                hrow(S + ((int)((uint32_t)yt.x >> 16) - sy0) * srow, h1);
+                uint32_t packed = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t v = (__umul24(h0[k], b0) + __umul24(h1[k], b1) + (1u << 21)) >> 22;
+                    packed |= min(v, 255u) << (8 * k);
+                }
+                *reinterpret_cast<uint32_t*>(drow0 + (size_t)rr * D.pitch + dx0) = packed;
+            }
+            continue;
         }
         for (int rr = 0; rr < dyn; ++rr) {
             const int2 yt = ytab[D.ytab_off + dy0 + rr];
@@ -131,9 +196,13 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         const int h = g.lv[l].h;
         // source rows per block: kPyrRows * (src/dst scale) + 2, bounded by the level ratio
         const int srows = (kPyrRows * g.lv[l - 1].h + g.lv[l].h - 1) / g.lv[l].h + 2;
-        const size_t smem = (size_t)srows * (((g.lv[l - 1].w + 3) >> 2) * 4);
+        // + 8 bytes: the window path's third dword of a group at the end of the last row
+        const size_t smem = (size_t)srows * (((g.lv[l - 1].w + 3) >> 2) * 4) + 8;
         dim3 grid(1, (h + kPyrRows - 1) / kPyrRows, batch);
-        hipLaunchKernelGGL(k_pyramid_level, grid, dim3(256), smem, s, b.geom, p, l, b.xtab, b.ytab);
+        if (g.lv[l].pyr_win)
+            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), smem, s, b.geom, p, l, b.xtab, b.ytab);
+        else
+            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(256), smem, s, b.geom, p, l, b.xtab, b.ytab);
     }
 }
 
@@ -1236,15 +1305,6 @@ __device__ __forceinline__ int wave_sum(int v)
            __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
 }
 
-typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ ushort2_t as_us2(uint32_t v)
-{
-    ushort2_t r;
-    r.x = (unsigned short)(v & 0xFFFF);
-    r.y = (unsigned short)(v >> 16);
-    return r;
-}
 
 // Sample coordinates as float bits: fl + 1.5 * 2^23 rounds fl to the nearest integer, ties to even
 // (one f32 addition into [2^23, 2^24), whose ulp is 1; the magic number is even, so the tie parity

@@ -41,6 +41,7 @@ struct LevelGeom {
     float inv_scale;          // mvInvScaleFactor[l]
     float patch_size;         // (float)(int)(PATCH_SIZE * scale)
     int roi_mw, roi_mh;       // largest FAST cell ROI of this level
+    int pyr_win;              // 1: every 4-column group's taps lie in 8 bytes from its first tap (K1 window path)
 };
 
 struct Geometry {
