@@ -152,6 +152,11 @@ struct orbx_handle {
     uint8_t* h_pin = nullptr;   // pinned staging: image in, count + keypoints + descriptors out
     int* h_status = nullptr;    // pinned status word (a pageable D2H copy can stall on other streams' work)
     size_t pin_bytes = 0;
+    // the host path's stream work (H2D image, the extraction kernels, D2H results and status) as one
+    // captured hipGraph, replayed while the buffers it was captured with stay the same
+    hipGraphExec_t host_graph = nullptr;
+    std::vector<const void*> graph_key;
+    bool graph_failed = false;
 
     // last batch (for pyramid / debug readback)
     FramePtrs last{};
@@ -345,11 +350,32 @@ ExtractBufs bufs(orbx_handle* h)
     return b;
 }
 
+// the extraction's stream work alone (no host state): also what the host path's graph captures
+void enqueue_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoint* kps, uint8_t* desc, int* counts,
+                      int cap, hipStream_t s)
+{
+    const Geometry& g = h->geom;
+    ExtractBufs b = bufs(h);
+    hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
+    hipMemsetAsync(h->d_status, 0, sizeof(int), s);
+    launch_pyramid(g, b, P, batch, s);
+    launch_fast(g, b, P, batch, s);
+    launch_quadtree(g, b, counts, batch, s);
+    launch_describe(g, b, P, kps, desc, cap, batch, s);
+}
+
 orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoint* kps, uint8_t* desc,
                          int* counts, int cap, hipStream_t s)
 {
     const Geometry& g = h->geom;
     ExtractBufs b = bufs(h);
+    if (!h->timing) {
+        enqueue_pipeline(h, P, batch, kps, desc, counts, cap, s);
+        h->last = P;
+        h->last_batch = batch;
+        std::fill(h->level_cached.begin(), h->level_cached.end(), false);
+        return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+    }
     hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
     hipMemsetAsync(h->d_status, 0, sizeof(int), s);
     hipEvent_t* ev = nullptr;
@@ -377,12 +403,28 @@ orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_key
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
-orbx_status status_from_device(orbx_handle* h, hipStream_t s)
+bool ensure_status_word(orbx_handle* h)
 {
     if (!h->h_status && hipHostMalloc((void**)&h->h_status, 64, hipHostMallocDefault) != hipSuccess) {
         h->h_status = nullptr;
-        return ORBX_ENOMEM;
+        return false;
     }
+    return true;
+}
+
+// after the status word's D2H copy is queued on s: wait, then map it
+orbx_status status_after_copy(orbx_handle* h, hipStream_t s)
+{
+    if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    const int st = *h->h_status;
+    if (st & kStatusCapOverflow) return ORBX_ENOSPC;
+    if (st) return ORBX_EDEVICE;
+    return ORBX_OK;
+}
+
+orbx_status status_from_device(orbx_handle* h, hipStream_t s)
+{
+    if (!ensure_status_word(h)) return ORBX_ENOMEM;
     if (hipMemcpyAsync(h->h_status, h->d_status, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess)
         return ORBX_EDEVICE;
     if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
@@ -444,6 +486,7 @@ void orbx_destroy(orbx_handle* h)
     dfree(h->d_counts);
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
+    if (h->host_graph) hipGraphExecDestroy(h->host_graph);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -507,18 +550,57 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
         if (hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
         h->pin_bytes = pin_need;
     }
+    if (!ensure_status_word(h)) return ORBX_ENOMEM;
     for (int r = 0; r < rows; ++r) std::memcpy(h->h_pin + (size_t)r * cols, img + (size_t)r * step, (size_t)cols);
     hipStream_t s = own_stream(h);
-    hipMemcpy2DAsync(h->d_img, pitch, h->h_pin, cols, cols, rows, hipMemcpyHostToDevice, s);
     FramePtrs P{h->d_img, need, pitch, h->d_pyr, (size_t)h->geom.pyr_bytes};
-    st = run_pipeline(h, P, 1, h->d_kps, h->d_desc, h->d_counts, ocap, s);
-    if (st != ORBX_OK) return st;
-    // one round trip: count, status and the whole output capacity come back together
     int* pc = (int*)(h->h_pin + img_b);
-    hipMemcpyAsync(pc, h->d_counts, sizeof(int), hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(h->h_pin + kp_off, h->d_kps, sizeof(orbx_keypoint) * (size_t)ocap, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(h->h_pin + ds_off, h->d_desc, (size_t)ocap * 32, hipMemcpyDeviceToHost, s);
-    if ((st = status_from_device(h, s)) != ORBX_OK) return st;
+    // H2D image, the kernels, then one round trip: count, status and the whole output capacity together
+    auto enqueue = [&]() {
+        hipMemcpy2DAsync(h->d_img, pitch, h->h_pin, cols, cols, rows, hipMemcpyHostToDevice, s);
+        enqueue_pipeline(h, P, 1, h->d_kps, h->d_desc, h->d_counts, ocap, s);
+        hipMemcpyAsync(pc, h->d_counts, sizeof(int), hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(h->h_pin + kp_off, h->d_kps, sizeof(orbx_keypoint) * (size_t)ocap, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(h->h_pin + ds_off, h->d_desc, (size_t)ocap * 32, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(h->h_status, h->d_status, sizeof(int), hipMemcpyDeviceToHost, s);
+    };
+    // Replayed as a hipGraph: one submission instead of ~17 (launch overhead is most of a 640x480 frame's
+    // latency).  The graph is re-captured when any buffer or size it holds changes.
+    const std::vector<const void*> key = {(const void*)h->h_pin, h->h_status, h->d_img, h->d_kps, h->d_desc,
+                                          h->d_counts, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
+                                          h->d_spill_node, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
+                                          h->d_cells, h->d_xtab, h->d_ytab, (const void*)(uintptr_t)rows,
+                                          (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
+    bool launched = false;
+    if (!h->graph_failed && !getenv("ORBX_NO_GRAPH")) {
+        if (h->host_graph && h->graph_key != key) {
+            hipGraphExecDestroy(h->host_graph);
+            h->host_graph = nullptr;
+        }
+        if (!h->host_graph) {
+            hipGraph_t graph = nullptr;
+            bool ok = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess;
+            if (ok) {
+                enqueue();
+                ok = hipStreamEndCapture(s, &graph) == hipSuccess && graph;
+            }
+            ok = ok && hipGraphInstantiate(&h->host_graph, graph, nullptr, nullptr, 0) == hipSuccess;
+            if (graph) hipGraphDestroy(graph);
+            if (!ok) {
+                (void)hipGetLastError();
+                h->host_graph = nullptr;
+                h->graph_failed = true;   // direct launches from now on
+            }
+            h->graph_key = key;
+        }
+        launched = h->host_graph && hipGraphLaunch(h->host_graph, s) == hipSuccess;
+    }
+    if (!launched) enqueue();
+    if (hipGetLastError() != hipSuccess) return ORBX_EDEVICE;
+    h->last = P;
+    h->last_batch = 1;
+    std::fill(h->level_cached.begin(), h->level_cached.end(), false);
+    if ((st = status_after_copy(h, s)) != ORBX_OK) return st;
     const int n = *pc;
     if (n > cap) return ORBX_ENOSPC;
     if (n > 0) {
