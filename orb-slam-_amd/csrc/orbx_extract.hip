@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
                                                     const Cell* __restrict__ cells,
                                                     uint32_t* __restrict__ slots,
                                                     int* __restrict__ cell_counts,
-                                                    int cb, int ce, int rw, int rh)
+                                                    int cb, int ce, int rw, int rh, int cpw)
 {
     // cells [cb, ce); per-wave LDS sized from the group's largest cell ROI (rw x rh)
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
@@ -373,8 +373,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
-    const int c0 = cb + ((lb - f * gridDim.x) * kFastWaves + wave) * kCellsPerWave;
-    const int c1 = min(c0 + kCellsPerWave, ce);
+    const int c0 = cb + ((lb - f * gridDim.x) * kFastWaves + wave) * cpw;
+    const int c1 = min(c0 + cpw, ce);
     if (c0 >= c1) return;   // wave-uniform; no block barriers below
     uint32_t* tile = (uint32_t*)(s_fast + (size_t)wave * fast_wave_bytes(rw, rh));
     uint8_t* map = (uint8_t*)(tile + (size_t)rh * kTileP);
@@ -567,7 +567,9 @@ void fast_groups(Geometry& g)
 
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
-    const int per_block = kFastWaves * kCellsPerWave;
+    // small batches (the per-frame host path) are latency-bound: one cell per wave, 3x the waves
+    const int cpw = batch <= kLatencyMaxBatch ? 1 : kCellsPerWave;
+    const int per_block = kFastWaves * cpw;
     for (int i = 0; i < g.fast_groups; ++i) {
         const int cb = g.fast_cb[i], ce = g.fast_cb[i + 1];
         if (ce <= cb) continue;
@@ -575,7 +577,7 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
         const size_t smem = kFastWaves * fast_wave_bytes(g.fast_rw[i], g.fast_rh[i]);
         hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         hipLaunchKernelGGL(k_fast_cells, grid, dim3(64 * kFastWaves), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
-                           cb, ce, g.fast_rw[i], g.fast_rh[i]);
+                           cb, ce, g.fast_rw[i], g.fast_rh[i], cpw);
     }
 }
 
@@ -1339,7 +1341,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
                                                const uint32_t* __restrict__ qt_out,
                                                const int* __restrict__ qt_cnt,
                                                orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                               int cap, int* __restrict__ status)
+                                               int cap, int* __restrict__ status, int kpw)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][kRawSlots];
     __shared__ __attribute__((aligned(16))) uint32_t s_rowT[4][kTCols * kTP];
@@ -1351,7 +1353,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
     uint32_t* raw32 = s_raw[wave];
     uint8_t* raw = (uint8_t*)raw32;
     uint32_t* rowT = s_rowT[wave];
-    const int g0 = (bx * 4 + wave) * kDescPerWave;
+    const int g0 = (bx * 4 + wave) * kpw;
 
     // ---- keypoint-independent lane state (c_desc_lanes), loaded once for the wave's keypoints ----
     const int icv = lane >> 1, ich = lane & 1;
@@ -1432,7 +1434,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
     bool nvalid = lookup(g0, nl, npk);
     if (nvalid) fill(nl, npk, sb, sp);
 #pragma unroll 1
-    for (int jj = 0; jj < kDescPerWave && nvalid; ++jj) {
+    for (int jj = 0; jj < kpw && nvalid; ++jj) {
         const int oidx = g0 + jj, l = nl;
         const uint32_t pk = npk;
         const int csb = sb, csp = sp;
@@ -1485,7 +1487,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
             for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
         }
         wave_lds_sync();   // raw is free: start the next keypoint's patch, it lands under BRIEF
-        nvalid = jj + 1 < kDescPerWave && lookup(oidx + 1, nl, npk);
+        nvalid = jj + 1 < kpw && lookup(oidx + 1, nl, npk);
         if (nvalid) fill(nl, npk, sb, sp);
 
         // rBRIEF with the reference's contracted FMAs; blur evaluated at each sample point
@@ -1532,9 +1534,11 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
 void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, orbx_keypoint* kps,
                      uint8_t* desc, int cap, int batch, hipStream_t s)
 {
-    dim3 grid((g.out_per_frame + 4 * kDescPerWave - 1) / (4 * kDescPerWave), batch);
+    // small batches (the per-frame host path) are latency-bound: one keypoint per wave
+    const int kpw = batch <= kLatencyMaxBatch ? 1 : kDescPerWave;
+    dim3 grid((g.out_per_frame + 4 * kpw - 1) / (4 * kpw), batch);
     hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, s, b.geom, p, b.qt_out, b.qt_cnt, kps, desc, cap,
-                       b.status);
+                       b.status, kpw);
 }
 
 }  // namespace orbx

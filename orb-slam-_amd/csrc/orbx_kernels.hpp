@@ -57,6 +57,7 @@ size_t quadtree_smem_bytes(const Geometry& g);
 // smaller frames keep 16)
 constexpr long long kQtBigArea = 1000000;
 constexpr int kQtMergedMaxBatch = 8;   // batches up to this size run all levels in one launch
+constexpr int kLatencyMaxBatch = 8;    // batches up to this size: FAST one cell per wave, describe one keypoint per wave
 // Workgroup size and keypoints per thread of level l's quadtree: level 0 holds most candidates
 // (KITTI ~6,800), level 1 ~2,700, levels >= 2 a few hundred.  Measured per launch (KITTI, 192 frames):
 // fewer waves per workgroup on the small levels does not shorten them (one wave for levels 3-7:

@@ -13,7 +13,7 @@ for f in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].replace("void ", "")[:40]))
 for f in glob.glob(d + "/**/*memory_copy_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy " + r.get("Direction", "")[:20]))
+        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy " + r.get("Direction", "").replace("MEMORY_COPY_", "")))
 ev.sort()
 # one call = from a H2D copy to the next H2D copy; report the last 5 calls' timelines and per-name averages
 starts = [i for i, e in enumerate(ev) if "HOST_TO_DEVICE" in e[2] or "H2D" in e[2] or "HostToDevice" in e[2]]
