@@ -145,9 +145,7 @@ struct orbx_handle {
     uint8_t* d_img = nullptr;
     size_t img_bytes = 0;
     int img_pitch = 0;
-    orbx_keypoint* d_kps = nullptr;
-    uint8_t* d_desc = nullptr;
-    int* d_counts = nullptr;
+    uint8_t* d_out = nullptr;   // [keypoints ocap (64-byte rounded)][descriptors ocap x 32], one D2H copy
     int single_cap = 0;
     uint8_t* h_pin = nullptr;   // pinned staging: image in, count + keypoints + descriptors out
     int* h_status = nullptr;    // pinned status word (a pageable D2H copy can stall on other streams' work)
@@ -325,7 +323,7 @@ orbx_status ensure_batch(orbx_handle* h, int batch)
     if (!dalloc(h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h->d_slots, (size_t)g.slots_per_frame * B) ||
         !dalloc(h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h->d_spill, (size_t)g.spill_per_frame * B) ||
         !dalloc(h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h->d_qt_out, (size_t)g.out_per_frame * B) ||
-        !dalloc(h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h->d_status, 1)) {
+        !dalloc(h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h->d_status, 16)) {
         h->batch_cap = 0;
         return ORBX_ENOMEM;
     }
@@ -356,8 +354,12 @@ void enqueue_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoi
 {
     const Geometry& g = h->geom;
     ExtractBufs b = bufs(h);
-    hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
-    hipMemsetAsync(h->d_status, 0, sizeof(int), s);
+    if (counts == h->d_status + 1 && batch == 1) {   // the host path: status and count in one memset
+        hipMemsetAsync(h->d_status, 0, 2 * sizeof(int), s);
+    } else {
+        hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
+        hipMemsetAsync(h->d_status, 0, sizeof(int), s);
+    }
     launch_pyramid(g, b, P, batch, s);
     launch_fast(g, b, P, batch, s);
     launch_quadtree(g, b, counts, batch, s);
@@ -410,16 +412,6 @@ bool ensure_status_word(orbx_handle* h)
         return false;
     }
     return true;
-}
-
-// after the status word's D2H copy is queued on s: wait, then map it
-orbx_status status_after_copy(orbx_handle* h, hipStream_t s)
-{
-    if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
-    const int st = *h->h_status;
-    if (st & kStatusCapOverflow) return ORBX_ENOSPC;
-    if (st) return ORBX_EDEVICE;
-    return ORBX_OK;
 }
 
 orbx_status status_from_device(orbx_handle* h, hipStream_t s)
@@ -481,9 +473,7 @@ void orbx_destroy(orbx_handle* h)
     dfree(h->d_qt_cnt);
     dfree(h->d_status);
     dfree(h->d_img);
-    dfree(h->d_kps);
-    dfree(h->d_desc);
-    dfree(h->d_counts);
+    dfree(h->d_out);
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
     if (h->host_graph) hipGraphExecDestroy(h->host_graph);
@@ -534,14 +524,16 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
         h->img_bytes = need;
     }
     const int ocap = h->geom.out_per_frame;
+    // device results [keypoints ocap][descriptors ocap x 32] mirror the pinned block from kp_off, and the
+    // frame's count sits in the status block's second word: two D2H copies (status + count, results)
+    const size_t kp_b = ((size_t)ocap * sizeof(orbx_keypoint) + 63) & ~(size_t)63;
     if (ocap > h->single_cap) {
-        if (!dalloc(h->d_kps, ocap) || !dalloc(h->d_desc, (size_t)ocap * 32) || !dalloc(h->d_counts, 1))
-            return ORBX_ENOMEM;
+        if (!dalloc(h->d_out, kp_b + (size_t)ocap * 32)) return ORBX_ENOMEM;
         h->single_cap = ocap;
     }
-    // pinned staging: [image rows x cols][count][keypoints ocap][descriptors ocap x 32]
+    // pinned staging: [image rows x cols][status, count][keypoints ocap][descriptors ocap x 32]
     const size_t img_b = ((size_t)rows * cols + 63) & ~(size_t)63;
-    const size_t kp_off = img_b + 64, ds_off = kp_off + (((size_t)ocap * sizeof(orbx_keypoint) + 63) & ~(size_t)63);
+    const size_t kp_off = img_b + 64, ds_off = kp_off + kp_b;
     const size_t pin_need = ds_off + (size_t)ocap * 32;
     if (pin_need > h->pin_bytes) {
         if (h->h_pin) hipHostFree(h->h_pin);
@@ -550,24 +542,23 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
         if (hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
         h->pin_bytes = pin_need;
     }
-    if (!ensure_status_word(h)) return ORBX_ENOMEM;
     for (int r = 0; r < rows; ++r) std::memcpy(h->h_pin + (size_t)r * cols, img + (size_t)r * step, (size_t)cols);
     hipStream_t s = own_stream(h);
     FramePtrs P{h->d_img, need, pitch, h->d_pyr, (size_t)h->geom.pyr_bytes};
-    int* pc = (int*)(h->h_pin + img_b);
-    // H2D image, the kernels, then one round trip: count, status and the whole output capacity together
+    int* phdr = (int*)(h->h_pin + img_b);   // [0] status, [1] count
+    int* d_count = h->d_status + 1;
+    orbx_keypoint* d_kps = (orbx_keypoint*)h->d_out;
+    uint8_t* d_desc = h->d_out + kp_b;
+    // H2D image, the kernels, then one round trip: status, count and the whole output capacity
     auto enqueue = [&]() {
         hipMemcpy2DAsync(h->d_img, pitch, h->h_pin, cols, cols, rows, hipMemcpyHostToDevice, s);
-        enqueue_pipeline(h, P, 1, h->d_kps, h->d_desc, h->d_counts, ocap, s);
-        hipMemcpyAsync(pc, h->d_counts, sizeof(int), hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(h->h_pin + kp_off, h->d_kps, sizeof(orbx_keypoint) * (size_t)ocap, hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(h->h_pin + ds_off, h->d_desc, (size_t)ocap * 32, hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(h->h_status, h->d_status, sizeof(int), hipMemcpyDeviceToHost, s);
+        enqueue_pipeline(h, P, 1, d_kps, d_desc, d_count, ocap, s);
+        hipMemcpyAsync(phdr, h->d_status, 2 * sizeof(int), hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(h->h_pin + kp_off, h->d_out, kp_b + (size_t)ocap * 32, hipMemcpyDeviceToHost, s);
     };
     // Replayed as a hipGraph: one submission instead of ~17 (launch overhead is most of a 640x480 frame's
     // latency).  The graph is re-captured when any buffer or size it holds changes.
-    const std::vector<const void*> key = {(const void*)h->h_pin, h->h_status, h->d_img, h->d_kps, h->d_desc,
-                                          h->d_counts, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
+    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
                                           h->d_spill_node, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
                                           h->d_cells, h->d_xtab, h->d_ytab, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
@@ -600,8 +591,10 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     h->last = P;
     h->last_batch = 1;
     std::fill(h->level_cached.begin(), h->level_cached.end(), false);
-    if ((st = status_after_copy(h, s)) != ORBX_OK) return st;
-    const int n = *pc;
+    if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    if (phdr[0] & kStatusCapOverflow) return ORBX_ENOSPC;
+    if (phdr[0]) return ORBX_EDEVICE;
+    const int n = phdr[1];
     if (n > cap) return ORBX_ENOSPC;
     if (n > 0) {
         std::memcpy(kps, h->h_pin + kp_off, sizeof(orbx_keypoint) * (size_t)n);
