@@ -61,6 +61,25 @@ W, H, NFEAT, NLEVELS, SCALE, INI, MINTH = 1241, 376, 2000, 8, 1.2, 20, 7
 WINDOW, NNRATIO = 100, 0.9
 
 
+def copy_bandwidth(dev, nbytes: int = 1 << 30, reps: int = 10):
+    """Achievable HBM bandwidth on this GPU: a device-to-device copy of a 1 GiB buffer (read + write bytes
+    per second), the practical ceiling beside the 8 TB/s spec peak."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    return gbs
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -445,6 +464,12 @@ def main():
         out["roofline_pipelined"] = out["roofline"]
         out["roofline"] = dict(roofline(iso), timing="isolated one-stream pass after the timed region "
                                                         "(same batches); see roofline_pipelined")
+    try:   # after the timed region; not part of `value`
+        cbw = copy_bandwidth(dev)
+        out["roofline"]["hbm_copy_GBps"] = round(cbw, 1)
+        out["roofline"]["frac_of_copy"] = round(out["roofline"]["achieved"] / cbw, 5)
+    except Exception:
+        pass
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(seq, args.cpu_seconds)
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
