@@ -299,7 +299,10 @@ class ORBextractor:
 
     def __call__(self, image, mask=None):
         """operator()(image, mask, keypoints, descriptors); mask ignored like the reference."""
-        img = np.ascontiguousarray(image, dtype=np.uint8)
+        img = np.asarray(image)
+        # a cv::Mat ROI keeps its parent's step: rows with unit-stride pixels pass through as they are
+        if img.dtype != np.uint8 or img.ndim != 2 or img.strides[1] != 1 or img.strides[0] < img.shape[1]:
+            img = np.ascontiguousarray(img, dtype=np.uint8)
         if img.size == 0:
             return np.zeros(0, KEYPOINT_DTYPE), None
         rows, cols = img.shape

@@ -136,6 +136,49 @@ def test_other_params(orbref, cuda):
         assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "params %s" % ((nfeat, scale, nl),))
 
 
+def test_host_graph_recapture_and_direct_launches(orbref, cuda):
+    """The host path replays a captured hipGraph per handle (orbx_api.hip orbx_extract).  Alternating image
+    sizes on one handle re-captures it (buffers and launch shapes change), a strided image goes through the
+    same staging, and ORBX_NO_GRAPH=1 (direct launches) gives identical results."""
+    import os
+    import orbx_synth
+    ex = _extractor(1000)
+    p = orbref.make_params(1000, 1.2, 8, 20, 7)
+    imgs = [orbx_synth.gen_image(31, 640, 480), orbx_synth.gen_image(32, 320, 240),
+            orbx_synth.gen_image(33, 752, 480)]
+    refs = [orbref.extract(im, p, want_pyramid=False) for im in imgs]
+    for rnd in range(2):
+        for i in (0, 1, 2, 0):
+            kps, desc = ex(imgs[i])
+            assert_same_keypoints(kps, refs[i].keypoints, desc, refs[i].descriptors, "graph rnd%d img%d" % (rnd, i))
+    wide = np.zeros((480, 700), np.uint8)
+    wide[:, 30:670] = imgs[0]
+    view = wide[:, 30:670]   # step 700, not contiguous
+    kps, desc = ex(view)
+    assert_same_keypoints(kps, refs[0].keypoints, desc, refs[0].descriptors, "strided")
+    os.environ["ORBX_NO_GRAPH"] = "1"
+    try:
+        for i in (2, 0):
+            kps, desc = ex(imgs[i])
+            assert_same_keypoints(kps, refs[i].keypoints, desc, refs[i].descriptors, "direct img%d" % i)
+    finally:
+        del os.environ["ORBX_NO_GRAPH"]
+
+
+def test_pyramid_without_byte_window(orbref, cuda):
+    """Scale factors above ~2.3 put a 4-column group's taps more than 8 bytes apart, so the pyramid kernel
+    takes its per-byte path instead of the byte window (LevelGeom::pyr_win)."""
+    import orbx_synth
+    img = orbx_synth.gen_image(41, 640, 480)
+    for scale, nl in [(2.5, 2), (2.0, 3)]:
+        ex = _extractor(600, scale, nl, 20, 7)
+        kps, desc = ex(img)
+        ref = orbref.extract(img, orbref.make_params(600, scale, nl, 20, 7))
+        assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "scale %.1f" % scale)
+        for l in range(nl):
+            assert np.array_equal(ex.mvImagePyramid[l], ref.pyramid[l]), "scale %.1f level %d" % (scale, l)
+
+
 def test_search_for_initialization(orbref, cuda):
     import torch
     import orbx
