@@ -69,7 +69,10 @@ int orbx_capacity(const orbx_handle* h, int rows, int cols);
  * (include/ORBextractor.h:58-61, src/ORBextractor.cc:1248-1334).
  * Host image in, host keypoints/descriptors out (desc: cap x 32 bytes, row i
  * belongs to kps[i]).  Synchronous on the handle's stream.  Mask is ignored,
- * as in the reference. */
+ * as in the reference.  The call's device work (upload, kernels, result copies)
+ * is replayed as one hipGraph captured on the first call for an image size and
+ * re-captured when the size changes; ORBX_NO_GRAPH=1 in the environment, or a
+ * failed capture, falls back to direct launches with identical results. */
 orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols, size_t step,
                          orbx_keypoint* kps, int cap, uint8_t* desc, int* n_out);
 
