@@ -62,7 +62,15 @@ orbx_status orbx_get_tables(const orbx_handle* h, int* nlevels, float* scale_fac
                             float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
                             int* features_per_level);
 
-/* Per-frame keypoint capacity the extractor may need (nfeatures + slack per level). */
+/* Per-frame keypoint capacity the extractor may need (nfeatures + slack per level).
+ * -1 (and ORBX_EINVAL from the extract calls) for a geometry the kernels do not run:
+ *   - a level narrower or shorter than one 30-px FAST cell inside its border (the
+ *     reference divides by zero there, src/ORBextractor.cc:941-949);
+ *   - a level whose quadtree region is less than half as wide as it is tall (nIni = 0,
+ *     :650);
+ *   - a level keypoint budget past the quadtree's LDS node arrays (about 90 bytes per node
+ *     in a 160 KB workgroup: roughly 1,700 keypoints per level, e.g. 8,000 features at 8
+ *     levels and scale 1.2, or 1,700 with a single level). */
 int orbx_capacity(const orbx_handle* h, int rows, int cols);
 
 /* Replaces ORBextractor::operator()(image, mask, keypoints, descriptors)
