@@ -462,6 +462,10 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
     }
 }
 
+// level-0 keypoints per frame the SearchForInitialization greedy pass keeps in LDS in its common launch:
+// 1792 keeps the workgroup under 80 KB (two per CU; the extractor's levels hold at most ~1,700)
+constexpr int kSiLdsCap = 1792;
+
 struct SgLayout {
     size_t top, cnt, ang1, ang2, mdist, m21, m12, bin, wmax, wmin, total;
 };
@@ -497,13 +501,22 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
                                                    const uint32_t* __restrict__ gkeys,
                                                    const float2* __restrict__ gxy, const int* __restrict__ gn,
                                                    const int* __restrict__ qcnt, const uint4* __restrict__ qtop,
-                                                   int* __restrict__ m12_out, int* __restrict__ nm_out)
+                                                   int* __restrict__ m12_out, int* __restrict__ nm_out, int lcap,
+                                                   int skip_small)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #ifdef ORBX_SI_PROF
     const long long pt0 = clock64();
 #endif
-    const SgLayout Ly = sg_layout(cap);
+    // The LDS arrays hold level-0 keypoints only (queries of F1, candidates of F2), sized lcap.  A pair whose
+    // level-0 counts exceed lcap is left to a second launch sized for cap (skip_small: that launch skips the
+    // pairs the first one took), so the common launch fits two workgroups per CU.
+    {
+        const int a0 = gn[2 * pa[blockIdx.x]], b0 = gn[2 * pb[blockIdx.x]];
+        const bool small = a0 <= kSiLdsCap && b0 <= kSiLdsCap;
+        if (skip_small ? small : !small) return;
+    }
+    const SgLayout Ly = sg_layout(lcap);
     uint4* top = (uint4*)(smem + Ly.top);
     int* cnt = (int*)(smem + Ly.cnt);
     float* ang1 = (float*)(smem + Ly.ang1);
@@ -517,8 +530,7 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
     __shared__ int s_hist[32];
     const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int fa = pa[pair], fb = pb[pair];
-    const int n1 = min(counts[fa], cap), n2 = min(counts[fb], cap);
-    const int n10 = gn[2 * fa], ng = gn[2 * fb + 1];
+    const int n10 = gn[2 * fa], ng = gn[2 * fb + 1], n20 = gn[2 * fb];   // level-0 counts
     int* out = m12_out + (size_t)pair * cap;
     const orbx_keypoint* k1 = kps + (size_t)fa * cap;
     const orbx_keypoint* k2 = kps + (size_t)fb * cap;
@@ -531,13 +543,13 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
         cnt[n10 + tid] = 0;
         top[n10 + tid] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     }
-    for (int i = tid; i < n2; i += 256) {
+    for (int i = tid; i < n20; i += 256) {   // candidates are F2's level-0 keypoints
         mdist[i] = 0xFFFF;   // INT_MAX: larger than any distance
         m21[i] = -1;
         wmax[i] = wmin[i] = 0;
         ang2[i] = k2[i].angle;
     }
-    for (int i = tid; i < n1; i += 256) {
+    for (int i = tid; i < n10; i += 256) {
         m12[i] = -1;
         bin[i] = -1;
     }
@@ -560,7 +572,7 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
     // The rounds reach the fixed point where every lane's decision follows from the ones
     // before it, which is the sequential result.  A step that needs a full scan ends the
     // chunk's exact prefix: it is replayed on its own with the wave.
-    const int n2c = max(n2 - 1, 0);
+    const int n2c = max(n20 - 1, 0);
     float2* pv = prev ? prev + (size_t)pair * cap : nullptr;
     auto decide = [&](const uint32_t (&e)[SI_TOPK], const uint32_t (&md)[SI_TOPK], int c, int& bi, int& bd,
                       bool& scan) -> bool {
@@ -779,7 +791,7 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
     }
     int nmatches = 0;
     for (int i = lane; i < cap; i += 64) {
-        const int v = i < n1 ? (int)m12[i] : -1;
+        const int v = i < n10 ? (int)m12[i] : -1;
         out[i] = v;
         nmatches += v >= 0;
         if (pv && v >= 0) pv[i] = make_float2(k2[v].x, k2[v].y);   // update vbPrevMatched (:580-584)
@@ -827,10 +839,16 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     const int qsplit = std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
     hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, G,
                        window, (const float2*)prev, gkeys, gxy, gn, qcnt, qtop);
-    const size_t gsmem = sg_layout(cap).total;
-    hipFuncSetAttribute((const void*)k_si_greedy, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gsmem);
+    const int lcap = std::min(cap, kSiLdsCap);
+    const size_t gsmem = sg_layout(lcap).total;
+    hipFuncSetAttribute((const void*)k_si_greedy, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)sg_layout(cap).total);
     hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), gsmem, s, kps, desc, counts, cap, pa, pb, G, window,
-                       nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm);
+                       nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm, lcap, 0);
+    if (cap > kSiLdsCap)   // pairs with more level-0 keypoints than the first launch's arrays hold
+        hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), sg_layout(cap).total, s, kps, desc, counts, cap, pa,
+                           pb, G, window, nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm,
+                           cap, 1);
 }
 
 }  // namespace orbx

@@ -1,5 +1,7 @@
 """Phase cycle counts of k_si_greedy (build liborbx with -DORBX_SI_PROF first)."""
 import sys, os
+if os.environ.get("ORBX_LIB") is None and os.path.exists(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "orb-slam-_amd", "build_prof_si", "liborbx.so")):
+    os.environ["ORBX_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "orb-slam-_amd", "build_prof_si", "liborbx.so")
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "orb-slam-_amd"))
 import numpy as np, torch
 import orbx, orbx_synth
