@@ -224,3 +224,70 @@ def test_host_edge_cases(orbref, cuda):
     with pytest.raises(orbx.OrbxError) as e:
         m.SearchForInitialization((big, np.zeros((5000, 32), np.uint8)), (k, d, (640, 480)), _xy(big), 100)
     assert e.value.code == orbx.ENOSPC
+
+
+def _synthetic_level0(n, seed, shift=(0.0, 0.0), base=None, W=1241, H=376):
+    """n level-0 keypoints (random positions, angles) with random descriptors; with `base`, the same points
+    moved by `shift` plus noise and the descriptors with a few flipped bits, so most have a true match."""
+    import orbx
+    rng = np.random.default_rng(seed)
+    k = np.zeros(n, orbx.KEYPOINT_DTYPE)
+    if base is None:
+        k["x"] = rng.uniform(20, W - 20, n).astype(np.float32)
+        k["y"] = rng.uniform(20, H - 20, n).astype(np.float32)
+        k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+        d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    else:
+        bk, bd = base
+        k["x"] = (bk["x"] + shift[0] + rng.normal(0, 0.7, n)).astype(np.float32)
+        k["y"] = (bk["y"] + shift[1] + rng.normal(0, 0.7, n)).astype(np.float32)
+        k["angle"] = ((bk["angle"] + rng.normal(3, 2, n)) % 360).astype(np.float32)
+        d = bd.copy()
+        for _ in range(3):   # ~3 flipped bits per descriptor
+            idx = rng.integers(0, 256, n)
+            d[np.arange(n), idx // 8] ^= (1 << (idx % 8)).astype(np.uint8)
+    k["size"], k["response"], k["octave"], k["class_id"] = 31.0, 1.0, 0, -1
+    return k, d
+
+
+def test_more_level0_keypoints_than_the_common_launch_holds(orbref, cuda):
+    """The greedy pass keeps up to 1792 level-0 keypoints per frame in LDS in its common launch (two
+    workgroups per CU); a pair with more goes to a second, full-size launch.  One device call with a
+    2400-keypoint pair and a 500-keypoint pair runs both launches; the host entry with 2400 runs the second."""
+    import torch
+    import orbx
+    W_, H_ = 1241, 376
+    ka, da = _synthetic_level0(2400, 1)
+    kb, db = _synthetic_level0(2400, 2, shift=(6.0, -2.0), base=(ka, da))
+    kc, dc = _synthetic_level0(500, 3)
+    kd, dd = _synthetic_level0(500, 4, shift=(-9.0, 4.0), base=(kc, dc))
+    frames = [(ka, da), (kb, db), (kc, dc), (kd, dd)]
+    cap = 2400
+    kp = np.zeros((4, cap, 7), np.int32)
+    ds = np.zeros((4, cap, 32), np.uint8)
+    for f, (k, d) in enumerate(frames):
+        kp[f, :len(k)] = k.view(np.int32).reshape(-1, 7)
+        ds[f, :len(k)] = d
+    tk, td = torch.from_numpy(kp).to(cuda), torch.from_numpy(ds).to(cuda)
+    tc = torch.tensor([len(k) for k, _ in frames], dtype=torch.int32, device=cuda)
+    pa = torch.tensor([0, 2], dtype=torch.int32, device=cuda)
+    pb = torch.tensor([1, 3], dtype=torch.int32, device=cuda)
+    m = orbx.ORBmatcher(0.9, True)
+    prev = np.zeros((2, cap, 2), np.float32)
+    prev[0, :2400] = _xy(ka)
+    prev[1, :500] = _xy(kc)
+    pv = torch.from_numpy(prev).to(cuda)
+    dm12, dnm = m.search_for_initialization_batch(tk, td, tc, pa, pb, H_, W_, 100, bounds=(0.0, W_, 0.0, H_),
+                                                  prev_matched=pv)
+    torch.cuda.synchronize()
+    dm12, dnm, pv = dm12.cpu().numpy(), dnm.cpu().numpy(), pv.cpu().numpy()
+    for p, (a, b) in enumerate([(0, 1), (2, 3)]):
+        n = len(frames[a][0])
+        want = orbref.search_for_initialization(frames[a][0], frames[a][1], frames[b][0], frames[b][1], W_, H_,
+                                                prev_xy=prev[p, :n])
+        assert want[0] > n // 4, "pair %d: only %d oracle matches" % (p, want[0])
+        _check("device pair %d" % p, int(dnm[p]), dm12[p, :n], pv[p, :n], want)
+    got_prev = _xy(ka)
+    n, m12 = m.SearchForInitialization((ka, da), (kb, db, (W_, H_)), got_prev, 100)
+    want = orbref.search_for_initialization(ka, da, kb, db, W_, H_, prev_xy=_xy(ka))
+    _check("host 2400", n, m12, got_prev, want)
