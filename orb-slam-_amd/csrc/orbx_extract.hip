@@ -361,6 +361,19 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch& F, uint32_t* til
     }
 }
 
+#ifdef ORBX_FAST_PROF
+// per-phase cycle sums of all FAST waves: staging commit, map clear, pass 1, pass 2, NMS, output, cells
+__device__ unsigned long long g_fast_prof[8];
+#define FP_STAMP(k)                          \
+    do {                                     \
+        const long long t1_ = clock64();     \
+        fp_acc[k] += t1_ - fp_t;             \
+        fp_t = t1_;                          \
+    } while (0)
+#else
+#define FP_STAMP(k) ((void)0)
+#endif
+
 __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                     const Cell* __restrict__ cells,
                                                     uint32_t* __restrict__ slots,
@@ -380,6 +393,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
     uint8_t* map = (uint8_t*)(tile + (size_t)rh * kTileP);
     uint16_t* list = (uint16_t*)(map + ((((size_t)(rh - 4) * (rw - 4)) + 3) & ~(size_t)3));
     const int tq = min(G->ini_th, G->min_th);
+#ifdef ORBX_FAST_PROF
+    long long fp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long fp_t = clock64();
+#endif
 
     // ROI -> LDS: aligned dword loads (alignbyte realigns rows of any pitch; the ROI ends >= 16
     // px before the level's right edge, so the 8-byte read stays in the row), 4 packed pixels
@@ -405,6 +422,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
         const int rw = C.roi_w, rh = C.roi_h;
         const int dw = rw - 6, dh = rh - 6;
         const Cell Cc = C;
+        FP_STAMP(7);
         fast_commit(F, tile);
         for (int i0 = 64 * kFastLd; i0 < S.ntot; i0 += 64 * kFastLd) {   // ROIs beyond 6 passes
             FastPrefetch R;
@@ -413,8 +431,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
         }
         const int W2 = dw + 2;
         const int mapn = W2 * (dh + 2);
+        FP_STAMP(0);
         for (int i = lane; i < (mapn + 3) >> 2; i += 64) ((uint32_t*)map)[i] = 0u;
         wave_lds_sync();
+        FP_STAMP(1);
         if (c + 1 < c1) {   // prefetch the next cell (registers only; lands under the passes below)
             C = cells[c + 1];
             S = cell_src(C);
@@ -437,34 +457,32 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
         const int col = lane & ((1 << cw_shift) - 1);
         const int rstep = 64 >> cw_shift;
         int row = lane >> cw_shift;
-        const uint32_t* tp = tile + __mul24(row + 3, kTileP) + col + 3;
-        const int tpstep = __mul24(rstep, kTileP);
+        // every lane tests a pixel, branch-free: reads are clamped into the detection window and the
+        // window mask is and-ed into the ballot
+        const int ccol = min(col, dw - 1) + 3;
         int n1 = 0;
         for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {   // two row steps per trip: more LDS reads in flight
-            const bool ina = col < dw && row < dh && fast_compass(tp, kTileP, tq);
-            const bool inb = col < dw && row + rstep < dh && fast_compass(tp + tpstep, kTileP, tq);
+            const uint32_t* tpa = tile + __mul24(min(row, dh - 1) + 3, kTileP) + ccol;
+            const uint32_t* tpb = tile + __mul24(min(row + rstep, dh - 1) + 3, kTileP) + ccol;
+            const bool ina = (col < dw) & (row < dh) & fast_compass(tpa, kTileP, tq);
+            const bool inb = (col < dw) & (row + rstep < dh) & fast_compass(tpb, kTileP, tq);
             const unsigned long long ma = __ballot(ina), mb = __ballot(inb);
             if (ina) list[n1 + lanes_below(ma)] = (uint16_t)((row << 8) | col);
             n1 += __popcll(ma);
             if (inb) list[n1 + lanes_below(mb)] = (uint16_t)(((row + rstep) << 8) | col);
             n1 += __popcll(mb);
             row += 2 * rstep;
-            tp += 2 * tpstep;
         }
         wave_lds_sync();
+        FP_STAMP(2);
         int n2 = 0;
         for (int j0 = 0; j0 < n1; j0 += 128) {   // two list entries per lane per trip
             const int ja = j0 + lane, jb = ja + 64;
-            int ka = 0, kb = 0, sa = 0, sb = 0;
-            if (ja < n1) {
-                ka = list[ja];
-                sa = fast_strength(tile + __mul24((ka >> 8) + 3, kTileP) + ((ka & 0xFF) + 3), kTileP);
-            }
-            if (jb < n1) {
-                kb = list[jb];
-                sb = fast_strength(tile + __mul24((kb >> 8) + 3, kTileP) + ((kb & 0xFF) + 3), kTileP);
-            }
-            const bool ina = ja < n1 && sa > tq, inb = jb < n1 && sb > tq;
+            // branch-free: lanes past the list re-test its last entry, masked out below
+            const int ka = list[min(ja, n1 - 1)], kb = list[min(jb, n1 - 1)];
+            const int sa = fast_strength(tile + __mul24((ka >> 8) + 3, kTileP) + ((ka & 0xFF) + 3), kTileP);
+            const int sb = fast_strength(tile + __mul24((kb >> 8) + 3, kTileP) + ((kb & 0xFF) + 3), kTileP);
+            const bool ina = (ja < n1) & (sa > tq), inb = (jb < n1) & (sb > tq);
             if (ina) map[__mul24((ka >> 8) + 1, W2) + (ka & 0xFF) + 1] = (uint8_t)sa;
             if (inb) map[__mul24((kb >> 8) + 1, W2) + (kb & 0xFF) + 1] = (uint8_t)sb;
             const unsigned long long ma = __ballot(ina), mb = __ballot(inb);
@@ -476,6 +494,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
         }
         wave_lds_sync();
 
+        FP_STAMP(3);
         // NMS at iniThFAST over the list; survivors remembered per round (rounds <= 57)
         const int rounds = (n2 + 63) >> 6;
         unsigned long long keepmask = 0;
@@ -505,6 +524,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
             }
         }
 
+        FP_STAMP(4);
         uint32_t* out = slots + (size_t)f * G->slots_per_frame + Cc.slot_base;
         const int xr0 = Cc.roi_x0 + 3 - kMinBorder, yr0 = Cc.roi_y0 + 3 - kMinBorder;
         int base = 0;
@@ -522,8 +542,29 @@ __global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__
         }
         if (lane == 0) *out_count = base;
         wave_lds_sync();   // tile, map and list are rewritten by the next cell
+        FP_STAMP(5);
+#ifdef ORBX_FAST_PROF
+        fp_acc[6] += 1;
+#endif
     }
+#ifdef ORBX_FAST_PROF
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_fast_prof[k], (unsigned long long)fp_acc[k]);
+#endif
 }
+#ifdef ORBX_FAST_PROF
+}  // namespace orbx
+extern "C" int orbx_debug_fast_prof(unsigned long long* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(orbx::g_fast_prof), sizeof(orbx::g_fast_prof)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(orbx::g_fast_prof), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+namespace orbx {
+#endif
 
 // LDS per CU on gfx950: the occupancy a FAST launch's per-wave tiles allow
 constexpr size_t kLdsPerCu = 160 * 1024;
