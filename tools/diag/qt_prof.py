@@ -2,7 +2,7 @@
 orb-slam-_amd/build_prof/liborbx.so compiled with -DORBX_QT_PROF), KITTI 192-frame batch, one stream."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["ORBX_LIB"] = os.path.join(ROOT, "orb-slam-_amd", "build_prof", "liborbx.so")
+os.environ["ORBX_LIB"] = os.path.join(ROOT, "orb-slam-_amd", sys.argv[1] if len(sys.argv) > 1 else "build_prof", "liborbx.so")
 sys.path[:0] = [os.path.join(ROOT, "orb-slam-_amd")]
 import numpy as np, torch, orbx, orbx_synth
 dev = torch.device("cuda", 0)
