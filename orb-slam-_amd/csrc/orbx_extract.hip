@@ -770,7 +770,8 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
                                                    uint32_t* __restrict__ spill,
                                                    uint32_t* __restrict__ spill_node,
                                                    uint32_t* __restrict__ qt_out, int* __restrict__ qt_cnt,
-                                                   int* __restrict__ frame_counts, int* __restrict__ status)
+                                                   int* __restrict__ frame_counts, int* __restrict__ status,
+                                                   int lcap, int cellcap)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int l = level0 + blockIdx.x, f = blockIdx.y;
@@ -779,8 +780,8 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
     const long long qt_t0 = clock64();
 #endif
     const LevelGeom& LG = G->lv[l];
-    const int lcap = G->lcap;
-    const QtLayout Ly = qt_layout(lcap, G->max_cells_level);
+    // lcap / cellcap: node-list and cell capacity of this launch's levels (qt_launch)
+    const QtLayout Ly = qt_layout(lcap, cellcap);
     uint32_t* scan = (uint32_t*)(smem + Ly.scan);
     int16_t* rect = (int16_t*)(smem + Ly.rect);
     uint32_t* cntb = (uint32_t*)(smem + Ly.cnt);
@@ -1201,11 +1202,21 @@ __global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* 
 
 template <int NT, int KPT>
 static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, int l0, int nl, int batch,
-                      size_t smem, hipStream_t s)
+                      size_t, hipStream_t s)
 {
+    // LDS sized for the levels of this launch: a level's list never holds more than cap + 3 nodes (phase 1
+    // stops before L + 3 * expandable exceeds N, phase 2 once L >= N; cap >= max(N + 2, 4 * nIni)), so the
+    // coarse levels' workgroups take less LDS than level 0's and more of them fit on a CU
+    int lcap = 8, cellcap = 1;
+    for (int l = l0; l < l0 + nl; ++l) {
+        lcap = std::max(lcap, g.lv[l].cap + 4);
+        cellcap = std::max(cellcap, g.lv[l].ncells);
+    }
+    const size_t smem = qt_layout(lcap, cellcap).total;
     hipFuncSetAttribute((const void*)k_quadtree<NT, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_quadtree<NT, KPT>), dim3(nl, batch), dim3(NT), smem, s, l0, b.geom, b.cells, b.slots,
-                       b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status);
+                       b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status, lcap,
+                       cellcap);
 }
 
 #ifdef ORBX_QT_PROF
