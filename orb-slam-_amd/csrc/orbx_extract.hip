@@ -763,7 +763,21 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 }
 
 template <int QT_NT, int QT_KPT>
-__global__ __launch_bounds__(QT_NT) void k_quadtree(int level0, const Geometry* __restrict__ G,
+#ifndef ORBX_QT0_WPE
+#define ORBX_QT0_WPE 4
+#endif
+#ifndef ORBX_QT1_WPE
+#define ORBX_QT1_WPE 1
+#endif
+#ifndef ORBX_QT2_WPE
+#define ORBX_QT2_WPE 1
+#endif
+// Minimum waves per SIMD (HIP's second __launch_bounds__ argument), i.e. a VGPR budget: the level-0
+// workgroup at 4 (128 VGPRs, 7 dwords spilled) instead of the compiler's 172 lets two workgroups share a
+// CU, so a 384-frame launch runs all frames at once (106 -> 68 us) and finds room beside describe sooner.
+__global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WPE
+                                    : (QT_NT == 512 && QT_KPT == 8) ? ORBX_QT1_WPE
+                                    : (QT_NT == 256) ? ORBX_QT2_WPE : 1) void k_quadtree(int level0, const Geometry* __restrict__ G,
                                                    const Cell* __restrict__ cells,
                                                    const uint32_t* __restrict__ slots,
                                                    const int* __restrict__ cell_counts,
