@@ -374,7 +374,10 @@ __device__ unsigned long long g_fast_prof[8];
 #define FP_STAMP(k) ((void)0)
 #endif
 
-__global__ __launch_bounds__(256) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
+#ifndef ORBX_FAST_WPE
+#define ORBX_FAST_WPE 1
+#endif
+__global__ __launch_bounds__(256, ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                     const Cell* __restrict__ cells,
                                                     uint32_t* __restrict__ slots,
                                                     int* __restrict__ cell_counts,
@@ -767,14 +770,18 @@ template <int QT_NT, int QT_KPT>
 #define ORBX_QT0_WPE 4
 #endif
 #ifndef ORBX_QT1_WPE
-#define ORBX_QT1_WPE 1
+#define ORBX_QT1_WPE 5
 #endif
 #ifndef ORBX_QT2_WPE
-#define ORBX_QT2_WPE 1
+#define ORBX_QT2_WPE 6
 #endif
-// Minimum waves per SIMD (HIP's second __launch_bounds__ argument), i.e. a VGPR budget: the level-0
-// workgroup at 4 (128 VGPRs, 7 dwords spilled) instead of the compiler's 172 lets two workgroups share a
-// CU, so a 384-frame launch runs all frames at once (106 -> 68 us) and finds room beside describe sooner.
+// Minimum waves per SIMD (HIP's second __launch_bounds__ argument), i.e. a VGPR budget per template:
+//   <512,16> (level 0) 4: 128 VGPRs (7 dwords spilled) instead of the compiler's 172, so two workgroups
+//            share a CU and a 384-frame launch runs every frame at once: 106 -> 68 us;
+//   <512,8>  (level 1) 5: 96 VGPRs (5 spilled) instead of 128: 43.8 -> 42.5 us;
+//   <256,4>  (levels 2-7) 6: 80 VGPRs (3 spilled) instead of 100: 88 -> 70 us.
+// Smaller workgroups also find room beside describe's sooner under the pipeline (+1.5% frames/s together).
+// FAST at 5 (94 VGPRs, no spill) measured slower (485 -> 495 us) and keeps the compiler's choice.
 __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WPE
                                     : (QT_NT == 512 && QT_KPT == 8) ? ORBX_QT1_WPE
                                     : (QT_NT == 256) ? ORBX_QT2_WPE : 1) void k_quadtree(int level0, const Geometry* __restrict__ G,

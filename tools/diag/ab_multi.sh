@@ -12,7 +12,7 @@ for L in default "$@"; do
   head -8 gpurun_out/abm_${L}_ks.txt
   cd $R
 done
-for i in 1 2; do
+for i in $(seq 1 ${ABN:-2}); do
   for L in default "$@"; do
     if [ $L = default ]; then unset ORBX_LIB; else export ORBX_LIB=$R/orb-slam-_amd/$L/liborbx.so; fi
     timeout -k 10 300 python bench.py --no-cpu --host-steps 0 --iso-steps 0 > gpurun_out/abm.json || exit 1
