@@ -10,6 +10,7 @@
 
 #include <algorithm>
 
+#include <type_traits>
 #include "orbx_kernels.hpp"
 
 namespace orbx {
@@ -377,6 +378,14 @@ __device__ __forceinline__ bool si_in_window(const uint32_t* keys, const float2*
     return fabsf(p.x - w.x) < w.r && fabsf(p.y - w.y) < w.r;
 }
 
+// F2 level-0 keypoints whose grid keys, positions and descriptors k_si_build stages in LDS (22 KB per
+// workgroup); a pair with more reads them from global memory instead
+constexpr int kSiBuildLds = 512;
+
+__host__ __device__ inline size_t si_build_xy_off() { return ((size_t)kSiBuildLds * 4 + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t si_build_desc_off() { return si_build_xy_off() + (size_t)kSiBuildLds * 8; }
+size_t si_build_smem_bytes() { return si_build_desc_off() + (size_t)kSiBuildLds * 32; }
+
 __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* __restrict__ kps,
                                                           const uint8_t* __restrict__ desc, int cap,
                                                           const int* __restrict__ pa, const int* __restrict__ pb,
@@ -389,77 +398,104 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
     const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave: uniform
     const int fa = pa[pair], fb = pb[pair];
     const int n10 = gn[2 * fa], ng = gn[2 * fb + 1];
-    uint32_t* keys = (uint32_t*)smem;
-    float2* xy = (float2*)(smem + (((size_t)cap * 4 + 15) & ~(size_t)15));
+    const uint8_t* d2 = desc + (size_t)fb * cap * 32;
     __shared__ int colstart[kGridCols + 1];
-    for (int g = tid; g < ng; g += SI_BUILD_NT) {
-        keys[g] = gkeys[(size_t)fb * cap + g];
-        xy[g] = gxy[(size_t)fb * cap + g];
+    // the window scans read F2's grid keys, positions and descriptors once per candidate per query: in LDS
+    // when they fit (one L2 round trip per candidate otherwise dominated the kernel)
+    const bool staged = ng <= kSiBuildLds;   // block-uniform
+    uint32_t* skeys = (uint32_t*)smem;
+    float2* sxy = (float2*)(smem + si_build_xy_off());
+    ulonglong2* sdesc = (ulonglong2*)(smem + si_build_desc_off());
+    if (staged) {
+        for (int g = tid; g < ng; g += SI_BUILD_NT) {
+            const uint32_t key = gkeys[(size_t)fb * cap + g];
+            skeys[g] = key;
+            sxy[g] = gxy[(size_t)fb * cap + g];
+            const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)(key & 0xFFFF) * 32);
+            sdesc[2 * g] = b[0];
+            sdesc[2 * g + 1] = b[1];
+        }
+        __syncthreads();
     }
-    __syncthreads();
+    const uint32_t* keys = staged ? (const uint32_t*)skeys : gkeys + (size_t)fb * cap;
+    const float2* xy = staged ? (const float2*)sxy : gxy + (size_t)fb * cap;
     si_colstart(keys, ng, colstart, tid, SI_BUILD_NT);
     __syncthreads();
     const orbx_keypoint* k1 = kps + (size_t)fa * cap;
     const uint8_t* d1 = desc + (size_t)fa * cap * 32;
-    const uint8_t* d2 = desc + (size_t)fb * cap * 32;
     const float2* pv = prev ? prev + (size_t)pair * cap : nullptr;
     const int nwaves = gridDim.y * (SI_BUILD_NT / 64);
-    for (int i1 = blockIdx.y * (SI_BUILD_NT / 64) + wave; i1 < n10; i1 += nwaves) {
-        const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
-        const ulonglong2 a0 = a[0], a1 = a[1];
-        // window centre vbPrevMatched[i1] (src/ORBmatcher.cc:456-460); F1's own keypoint when not given
-        const float2 c = pv ? pv[i1] : make_float2(k1[i1].x, k1[i1].y);
-        const SiWindow w = si_window(keys, ng, c, (float)window, G, colstart);
-        // lane-local 4 smallest (Hamming << 16 | visit position), with their i2
-        uint32_t hk[SI_TOPK], hi2[SI_TOPK];
+    auto scan_queries = [&](auto staged_tag) {
+        constexpr bool kStaged = decltype(staged_tag)::value;
+        const uint32_t* K = kStaged ? (const uint32_t*)skeys : keys;
+        const float2* XY = kStaged ? (const float2*)sxy : xy;
+        for (int i1 = blockIdx.y * (SI_BUILD_NT / 64) + wave; i1 < n10; i1 += nwaves) {
+            const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
+            const ulonglong2 a0 = a[0], a1 = a[1];
+            // window centre vbPrevMatched[i1] (src/ORBmatcher.cc:456-460); F1's own keypoint when not given
+            const float2 c = pv ? pv[i1] : make_float2(k1[i1].x, k1[i1].y);
+            const SiWindow w = si_window(K, ng, c, (float)window, G, colstart);
+            // lane-local 4 smallest (Hamming << 16 | visit position), with their i2
+            uint32_t hk[SI_TOPK], hi2[SI_TOPK];
 #pragma unroll
-        for (int q = 0; q < SI_TOPK; ++q) hk[q] = hi2[q] = 0xFFFFFFFFu;
-        int count = 0;
-        for (int g0 = w.lo; g0 < w.hi; g0 += 64) {
-            int i2 = 0;
-            const bool in = si_in_window(keys, xy, w, g0 + lane, i2);
-            const unsigned long long m = __ballot(in);
-            if (in) {
-                const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)i2 * 32);
-                const int d = ham256(a0, a1, b[0], b[1]);
-                const int pos = count + lanes_below_u64(m);
-                uint32_t k = ((uint32_t)d << 16) | (uint32_t)pos, v = (uint32_t)i2;
+            for (int q = 0; q < SI_TOPK; ++q) hk[q] = hi2[q] = 0xFFFFFFFFu;
+            int count = 0;
+            for (int g0 = w.lo; g0 < w.hi; g0 += 64) {
+                int i2 = 0;
+                const int g = g0 + lane;
+                const bool in = si_in_window(K, XY, w, g, i2);
+                const unsigned long long m = __ballot(in);
+                if (in) {
+                    int d;
+                    if constexpr (kStaged) {
+                        d = ham256(a0, a1, sdesc[2 * g], sdesc[2 * g + 1]);
+                    } else {
+                        const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)i2 * 32);
+                        d = ham256(a0, a1, b[0], b[1]);
+                    }
+                    const int pos = count + lanes_below_u64(m);
+                    uint32_t k = ((uint32_t)d << 16) | (uint32_t)pos, v = (uint32_t)i2;
 #pragma unroll
-                for (int q = 0; q < SI_TOPK; ++q) {   // sorted insert
-                    if (k < hk[q]) {
-                        const uint32_t tk = hk[q], tv = hi2[q];
-                        hk[q] = k;
-                        hi2[q] = v;
-                        k = tk;
-                        v = tv;
+                    for (int q = 0; q < SI_TOPK; ++q) {   // sorted insert
+                        if (k < hk[q]) {
+                            const uint32_t tk = hk[q], tv = hi2[q];
+                            hk[q] = k;
+                            hi2[q] = v;
+                            k = tk;
+                            v = tv;
+                        }
                     }
                 }
+                count += __popcll(m);
             }
-            count += __popcll(m);
-        }
-        // wave merge: keys are unique (visit positions), so one lane pops per round
-        uint32_t top[SI_TOPK];
+            // wave merge: keys are unique (visit positions), so one lane pops per round
+            uint32_t top[SI_TOPK];
 #pragma unroll
-        for (int q = 0; q < SI_TOPK; ++q) {
-            const uint32_t kmin = wave_min_u32(hk[0]);
-            const unsigned long long wm = __ballot(hk[0] == kmin);
-            const int wl = wm ? (int)__builtin_ctzll(wm) : 0;
-            const uint32_t i2 = (uint32_t)__builtin_amdgcn_readlane((int)hi2[0], wl);
-            top[q] = kmin == 0xFFFFFFFFu ? 0xFFFFFFFFu : ((kmin & 0xFFFF0000u) | i2);
-            if (kmin != 0xFFFFFFFFu && hk[0] == kmin) {
+            for (int q = 0; q < SI_TOPK; ++q) {
+                const uint32_t kmin = wave_min_u32(hk[0]);
+                const unsigned long long wm = __ballot(hk[0] == kmin);
+                const int wl = wm ? (int)__builtin_ctzll(wm) : 0;
+                const uint32_t i2 = (uint32_t)__builtin_amdgcn_readlane((int)hi2[0], wl);
+                top[q] = kmin == 0xFFFFFFFFu ? 0xFFFFFFFFu : ((kmin & 0xFFFF0000u) | i2);
+                if (kmin != 0xFFFFFFFFu && hk[0] == kmin) {
 #pragma unroll
-                for (int r = 0; r + 1 < SI_TOPK; ++r) {
-                    hk[r] = hk[r + 1];
-                    hi2[r] = hi2[r + 1];
+                    for (int r = 0; r + 1 < SI_TOPK; ++r) {
+                        hk[r] = hk[r + 1];
+                        hi2[r] = hi2[r + 1];
+                    }
+                    hk[SI_TOPK - 1] = hi2[SI_TOPK - 1] = 0xFFFFFFFFu;
                 }
-                hk[SI_TOPK - 1] = hi2[SI_TOPK - 1] = 0xFFFFFFFFu;
+            }
+            if (lane == 0) {
+                qtop[(size_t)pair * cap + i1] = make_uint4(top[0], top[1], top[2], top[3]);
+                qcnt[(size_t)pair * cap + i1] = count;
             }
         }
-        if (lane == 0) {
-            qtop[(size_t)pair * cap + i1] = make_uint4(top[0], top[1], top[2], top[3]);
-            qcnt[(size_t)pair * cap + i1] = count;
-        }
-    }
+    };
+    if (staged)
+        scan_queries(std::true_type{});
+    else
+        scan_queries(std::false_type{});
 }
 
 // level-0 keypoints per frame the SearchForInitialization greedy pass keeps in LDS in its common launch:
@@ -834,7 +870,7 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     int p2 = 1;
     while (p2 < cap) p2 <<= 1;
     hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)p2 * 4, s, kps, counts, cap, G, gkeys, gxy, gn);
-    const size_t bsmem = (((size_t)cap * 4 + 15) & ~(size_t)15) + (size_t)cap * 8;
+    const size_t bsmem = si_build_smem_bytes();
     // query slices per pair: about 8 waves per SIMD over the chip, at least 4 queries per wave
     const int qsplit = std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
     hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, G,
