@@ -501,6 +501,7 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
 // level-0 keypoints per frame the SearchForInitialization greedy pass keeps in LDS in its common launch:
 // 1792 keeps the workgroup under 80 KB (two per CU; the extractor's levels hold at most ~1,700)
 constexpr int kSiLdsCap = 1792;
+constexpr int kSiGreedySmall = 512;   // the common tier: KITTI / EuRoC / TUM frames keep <= ~440 level-0 keypoints
 
 struct SgLayout {
     size_t top, cnt, ang1, ang2, mdist, m21, m12, bin, wmax, wmin, total;
@@ -538,19 +539,19 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
                                                    const float2* __restrict__ gxy, const int* __restrict__ gn,
                                                    const int* __restrict__ qcnt, const uint4* __restrict__ qtop,
                                                    int* __restrict__ m12_out, int* __restrict__ nm_out, int lcap,
-                                                   int skip_small)
+                                                   int tier_lo)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #ifdef ORBX_SI_PROF
     const long long pt0 = clock64();
 #endif
-    // The LDS arrays hold level-0 keypoints only (queries of F1, candidates of F2), sized lcap.  A pair whose
-    // level-0 counts exceed lcap is left to a second launch sized for cap (skip_small: that launch skips the
-    // pairs the first one took), so the common launch fits two workgroups per CU.
+    // The LDS arrays hold level-0 keypoints only (queries of F1, candidates of F2), sized lcap.  Pairs are
+    // tiered by their larger level-0 count: this launch takes the pairs in (tier_lo, lcap], launches sized
+    // for the larger tiers take the rest (launch_search_init), so the common launch's workgroups stay small
+    // (22 KB for up to 512 level-0 keypoints) and find room beside the extractor's under the pipeline.
     {
-        const int a0 = gn[2 * pa[blockIdx.x]], b0 = gn[2 * pb[blockIdx.x]];
-        const bool small = a0 <= kSiLdsCap && b0 <= kSiLdsCap;
-        if (skip_small ? small : !small) return;
+        const int n0 = max(gn[2 * pa[blockIdx.x]], gn[2 * pb[blockIdx.x]]);
+        if (n0 <= tier_lo || n0 > lcap) return;
     }
     const SgLayout Ly = sg_layout(lcap);
     uint4* top = (uint4*)(smem + Ly.top);
@@ -875,16 +876,19 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     const int qsplit = std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
     hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, G,
                        window, (const float2*)prev, gkeys, gxy, gn, qcnt, qtop);
-    const int lcap = std::min(cap, kSiLdsCap);
-    const size_t gsmem = sg_layout(lcap).total;
     hipFuncSetAttribute((const void*)k_si_greedy, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)sg_layout(cap).total);
-    hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), gsmem, s, kps, desc, counts, cap, pa, pb, G, window,
-                       nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm, lcap, 0);
-    if (cap > kSiLdsCap)   // pairs with more level-0 keypoints than the first launch's arrays hold
-        hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), sg_layout(cap).total, s, kps, desc, counts, cap, pa,
-                           pb, G, window, nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm,
-                           cap, 1);
+    // tiers by level-0 count: up to 512 (22 KB per workgroup), up to kSiLdsCap (two workgroups per CU), cap;
+    // a launch whose tier holds no pair costs a few microseconds (its workgroups return at once)
+    const int tiers[3] = {std::min(cap, kSiGreedySmall), std::min(cap, kSiLdsCap), cap};
+    int lo = -1;
+    for (int t = 0; t < 3; ++t) {
+        if (tiers[t] <= lo) continue;
+        hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), sg_layout(tiers[t]).total, s, kps, desc, counts, cap,
+                           pa, pb, G, window, nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm,
+                           tiers[t], lo);
+        lo = tiers[t];
+    }
 }
 
 }  // namespace orbx
