@@ -1312,7 +1312,17 @@ constexpr int kRawSlots = kRawRows * kRawP / 4;
 // 4t + (q ^ (q >> 1)).
 __host__ __device__ constexpr int raw_slot(int r) { return r ^ ((r >> 1) & 1); }
 constexpr int kTCols = 40, kTP = 22;                  // row-blurred, transposed: [col][row pairs], 22 dwords/col
-constexpr int kDescPerWave = 4;                       // keypoints per wave (lane state set up once per wave)
+#ifndef ORBX_DESC_KPW
+#define ORBX_DESC_KPW 4
+#endif
+constexpr int kDescPerWave = ORBX_DESC_KPW;           // keypoints per wave (lane state set up once per wave)
+#ifndef ORBX_DESC_WAVES
+#define ORBX_DESC_WAVES 1
+#endif
+// waves per describe workgroup: one, so a workgroup's LDS (6.3 KB) frees as soon as its own keypoints are done
+// and no wave waits on slower siblings (4 waves: 863 us per 384 frames, 2: 815, 1: 768; pipelined 169.1k ->
+// 176.4k frames/s)
+constexpr int kDescWaves = ORBX_DESC_WAVES;
 
 // Horizontal-pass items (row pair rp << 8 | column group cg) that BRIEF can read: a sample
 // (18 + xx, 18 + yy) has |(x, y)| <= 18.39 before rounding (the pattern's largest radius), so a
@@ -1410,14 +1420,14 @@ __device__ __forceinline__ uint32_t blur_acc(const uint32_t* rowT, uint32_t by, 
     return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
 }
 
-__global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
+__global__ __launch_bounds__(64 * kDescWaves) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
                                                const uint32_t* __restrict__ qt_out,
                                                const int* __restrict__ qt_cnt,
                                                orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                int cap, int* __restrict__ status, int kpw)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_raw[4][kRawSlots];
-    __shared__ __attribute__((aligned(16))) uint32_t s_rowT[4][kTCols * kTP];
+    __shared__ __attribute__((aligned(16))) uint32_t s_raw[kDescWaves][kRawSlots];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rowT[kDescWaves][kTCols * kTP];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x, bx = lb - f * gridDim.x;
@@ -1426,7 +1436,7 @@ __global__ __launch_bounds__(256) void k_describe(const Geometry* __restrict__ G
     uint32_t* raw32 = s_raw[wave];
     uint8_t* raw = (uint8_t*)raw32;
     uint32_t* rowT = s_rowT[wave];
-    const int g0 = (bx * 4 + wave) * kpw;
+    const int g0 = (bx * kDescWaves + wave) * kpw;
 
     // ---- keypoint-independent lane state (c_desc_lanes), loaded once for the wave's keypoints ----
     const int icv = lane >> 1, ich = lane & 1;
@@ -1609,8 +1619,8 @@ void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p
 {
     // small batches (the per-frame host path) are latency-bound: one keypoint per wave
     const int kpw = batch <= kLatencyMaxBatch ? 1 : kDescPerWave;
-    dim3 grid((g.out_per_frame + 4 * kpw - 1) / (4 * kpw), batch);
-    hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, s, b.geom, p, b.qt_out, b.qt_cnt, kps, desc, cap,
+    dim3 grid((g.out_per_frame + kDescWaves * kpw - 1) / (kDescWaves * kpw), batch);
+    hipLaunchKernelGGL(k_describe, grid, dim3(64 * kDescWaves), 0, s, b.geom, p, b.qt_out, b.qt_cnt, kps, desc, cap,
                        b.status, kpw);
 }
 
