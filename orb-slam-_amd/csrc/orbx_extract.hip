@@ -53,11 +53,18 @@ __device__ __forceinline__ ushort2_t as_us2(uint32_t v)
 // (11-bit coefficients, 22-bit vertical rounding) — SURVEY.md A.2.
 // Coefficient tables are built on the host exactly like OpenCV builds them.
 // ---------------------------------------------------------------------------
-constexpr int kPyrRows = 8;
+#ifndef ORBX_PYR_ROWS
+#define ORBX_PYR_ROWS 8
+#endif
+#ifndef ORBX_PYR_NT
+#define ORBX_PYR_NT 256
+#endif
+constexpr int kPyrRows = ORBX_PYR_ROWS;
+constexpr int kPyrNT = ORBX_PYR_NT;   // threads per pyramid workgroup
 constexpr int kPyrLd = 8;   // staged dwords in flight per thread
 
 template <bool kWin>
-__global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
+__global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
                                                        const int2* __restrict__ xtab,
                                                        const int2* __restrict__ ytab)
 {
@@ -86,12 +93,12 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
     // kPyrLd dwords per thread in flight: every load of a batch is issued before the first is used
     // (one dependent load per dword left each thread waiting ~14 HBM latencies per block at level 1)
     const int total = nrows * nd;
-    for (int i0 = threadIdx.x; i0 < total; i0 += 256 * kPyrLd) {
+    for (int i0 = threadIdx.x; i0 < total; i0 += kPyrNT * kPyrLd) {
         uint32_t lo[kPyrLd], hi[kPyrLd], sh[kPyrLd];
         int dst[kPyrLd];
 #pragma unroll
         for (int u = 0; u < kPyrLd; ++u) {
-            const int i = i0 + 256 * u;
+            const int i = i0 + kPyrNT * u;
             dst[u] = -1;
             if (i < total) {
                 const int r = (int)(((float)i + 0.5f) * inv_nd), k = i - __mul24(r, nd);
@@ -119,7 +126,7 @@ __global__ __launch_bounds__(256) void k_pyramid_level(const Geometry* __restric
     // reused for the block's rows
     const int q = (D.w + 3) >> 2;
     uint8_t* drow0 = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy0 * D.pitch;
-    for (int g = threadIdx.x; g < q; g += 256) {
+    for (int g = threadIdx.x; g < q; g += kPyrNT) {
         const int dx0 = g * 4;
         // every product fits a 24 x 24 -> 32-bit multiply (v_mul_u32_u24, full rate; the compiler
         // otherwise emits the quarter-rate v_mul_lo_u32 for h * b).  The two taps keep separate
@@ -200,9 +207,9 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         const size_t smem = (size_t)srows * (((g.lv[l - 1].w + 3) >> 2) * 4) + 8;
         dim3 grid(1, (h + kPyrRows - 1) / kPyrRows, batch);
         if (g.lv[l].pyr_win)
-            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(256), smem, s, b.geom, p, l, b.xtab, b.ytab);
+            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(kPyrNT), smem, s, b.geom, p, l, b.xtab, b.ytab);
         else
-            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(256), smem, s, b.geom, p, l, b.xtab, b.ytab);
+            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(kPyrNT), smem, s, b.geom, p, l, b.xtab, b.ytab);
     }
 }
 
