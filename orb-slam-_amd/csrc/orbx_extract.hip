@@ -1427,7 +1427,10 @@ __device__ __forceinline__ uint32_t blur_acc(const uint32_t* rowT, uint32_t by, 
     return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
 }
 
-__global__ __launch_bounds__(64 * kDescWaves) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
+#ifndef ORBX_DESC_WPE
+#define ORBX_DESC_WPE 1
+#endif
+__global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
                                                const uint32_t* __restrict__ qt_out,
                                                const int* __restrict__ qt_cnt,
                                                orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
