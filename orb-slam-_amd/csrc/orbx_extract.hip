@@ -1492,10 +1492,14 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         const int w = G->lv[l].w, h = G->lv[l].h;
         int pitch;
         const uint8_t* img = level_base(P, G, f, l, pitch);
-        if (cx >= 21 && cy >= 21 && cy + 21 < h && cx + 31 <= w) {
+        // Interior keypoints, and right-border ones whose 43 columns are all inside the level (cx + 21 < w):
+        // those read up to 9 bytes past the row end, which land in the next row of the same level (cy + 22 < h)
+        // and only feed blurred columns BRIEF never samples (|x| <= 18 + the 3-tap reach).  About 2/3 of the
+        // 6.5% of KITTI keypoints the reflect-101 byte path took before (13% of the describe launch).
+        if (cx >= 21 && cy >= 21 && cy + 21 < h && (cx + 31 <= w || (cx + 21 < w && cy + 22 < h))) {
             // DMA instruction t moves rows 4t..4t+3 (lane = 16 * row + dword; dwords 13..15
-            // repeat dword 12, row 43 repeats row 42).  Each row's aligned dwords end at or
-            // before column cx+30 < w and start at or after the 4-byte aligned allocation.
+            // repeat dword 12, row 43 repeats row 42).  Each row's aligned dwords start at or after the
+            // 4-byte aligned allocation.
             const uintptr_t s0 = (uintptr_t)(img + (size_t)(cy - 21) * pitch + (cx - 21));
             const uint8_t* ub = (const uint8_t*)(s0 & ~(uintptr_t)3);   // wave-uniform, aligned
             sb = (int)(s0 & 3);
