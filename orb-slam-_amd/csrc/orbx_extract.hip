@@ -1518,10 +1518,19 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         } else {
             sb = 0;
             sp = 0;
-            for (int i = lane; i < kRawRows * kRawP; i += 64) {
-                const int r = raw_slot(min(i / kRawP, 43)), c = i - (i / kRawP) * kRawP;   // slot -> row
-                const int X = reflect101(cx - 21 + c, w), Y = reflect101(cy - 21 + min(r, 42), h);
-                raw[i] = img[(size_t)Y * pitch + X];
+            // reflect-101 bytes, lane = column of a 64-byte slot row: the column reflection once per lane, the
+            // row's per slot (wave-uniform), and 11 slots' loads in flight before their LDS stores
+            static_assert(kRawP == 64 && kRawRows % 11 == 0, "one lane per slot column, 11-slot batches");
+            const uint8_t* col = img + reflect101(cx - 21 + lane, w);
+            for (int s0 = 0; s0 < kRawRows; s0 += 11) {
+                uint8_t v[11];
+#pragma unroll
+                for (int u = 0; u < 11; ++u) {
+                    const int r = raw_slot(min(s0 + u, 43));   // slot -> row; row 43 repeats row 42
+                    v[u] = col[(size_t)reflect101(cy - 21 + min(r, 42), h) * pitch];
+                }
+#pragma unroll
+                for (int u = 0; u < 11; ++u) raw[(s0 + u) * kRawP + lane] = v[u];
             }
         }
     };
