@@ -68,9 +68,10 @@ orbx_status orbx_get_tables(const orbx_handle* h, int* nlevels, float* scale_fac
  *     reference divides by zero there, src/ORBextractor.cc:941-949);
  *   - a level whose quadtree region is less than half as wide as it is tall (nIni = 0,
  *     :650);
- *   - a level keypoint budget past the quadtree's LDS node arrays (about 90 bytes per node
- *     in a 160 KB workgroup: roughly 1,700 keypoints per level, e.g. 8,000 features at 8
- *     levels and scale 1.2, or 1,700 with a single level). */
+ *   - an image side above 4096 pixels (12-bit packed keypoint coordinates).
+ * Any keypoint budget runs: a level whose quadtree node list outgrows a workgroup's LDS
+ * (about 1,700 keypoints, e.g. Tracking's 2 * nFeatures initialisation extractor at 4,000
+ * features, src/Tracking.cc:133) keeps its node arrays in device memory instead. */
 int orbx_capacity(const orbx_handle* h, int rows, int cols);
 
 /* Replaces ORBextractor::operator()(image, mask, keypoints, descriptors)
@@ -219,8 +220,8 @@ typedef struct {
  * Tracking::MonocularInitialization keeps it across attempts (src/Tracking.cc:599-602, 639-644);
  * NULL = F1's own keypoint positions (the first attempt), not written.
  * Outputs: d_matches12[p*cap + i1] (-1 = none) and d_nmatches[p] (the return value).
- * cap <= 32767, and the greedy pass's LDS (about 43 * cap bytes) must fit one workgroup
- * (ORBX_ENOSPC otherwise).  Asynchronous on `stream`. */
+ * cap <= 32767.  Pairs with more level-0 keypoints than one workgroup's LDS holds for the greedy
+ * pass (about 43 bytes each, ~3,800) run it from device memory.  Asynchronous on `stream`. */
 orbx_status orbm_search_for_initialization_device(const orbx_keypoint* d_kps, const uint8_t* d_desc,
                                                   const int* d_counts, int nframes, int cap, const int* d_pair_a,
                                                   const int* d_pair_b, int npairs, const orbm_grid* grid,

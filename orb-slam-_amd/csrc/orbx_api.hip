@@ -137,6 +137,7 @@ struct orbx_handle {
     int* d_cell_counts = nullptr;
     uint32_t* d_spill = nullptr;
     uint32_t* d_spill_node = nullptr;
+    uint8_t* d_qt_nodes = nullptr;
     uint32_t* d_qt_out = nullptr;
     int* d_qt_cnt = nullptr;
     int* d_status = nullptr;
@@ -291,9 +292,10 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     g.pyr_bytes = (pyr + 255) & ~255LL;
     int spill = 0;
     g.qt_kpt0 = (long long)rows * cols > kQtBigArea ? 24 : 16;
+    // node lists too large for a workgroup's LDS run from global memory (any budget the reference takes)
+    if (!qt_prepare(g)) return ORBX_EINVAL;
     for (int l = 0; l < t.nlevels; ++l) spill += std::max(0, g.lv[l].slot_cap - qt_regcap(g, l));
     g.spill_per_frame = std::max(spill, 1);
-    if (lcap >= 65535 || quadtree_smem_bytes(g) > 160 * 1024) return ORBX_EINVAL;
 
     // once per image size: the tables go up on the handle's own stream (never the legacy null stream)
     if (!dalloc(h->d_geom, 1) || !dalloc(h->d_cells, cells.size()) || !dalloc(h->d_xtab, xt.size()) ||
@@ -323,7 +325,8 @@ orbx_status ensure_batch(orbx_handle* h, int batch)
     if (!dalloc(h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h->d_slots, (size_t)g.slots_per_frame * B) ||
         !dalloc(h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h->d_spill, (size_t)g.spill_per_frame * B) ||
         !dalloc(h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h->d_qt_out, (size_t)g.out_per_frame * B) ||
-        !dalloc(h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h->d_status, 16)) {
+        !dalloc(h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h->d_status, 16) ||
+        !dalloc(h->d_qt_nodes, (size_t)g.qtg_per_frame * B)) {
         h->batch_cap = 0;
         return ORBX_ENOMEM;
     }
@@ -342,6 +345,7 @@ ExtractBufs bufs(orbx_handle* h)
     b.cell_counts = h->d_cell_counts;
     b.spill = h->d_spill;
     b.spill_node = h->d_spill_node;
+    b.qt_nodes = h->d_qt_nodes;
     b.qt_out = h->d_qt_out;
     b.qt_cnt = h->d_qt_cnt;
     b.status = h->d_status;
@@ -469,6 +473,7 @@ void orbx_destroy(orbx_handle* h)
     dfree(h->d_cell_counts);
     dfree(h->d_spill);
     dfree(h->d_spill_node);
+    dfree(h->d_qt_nodes);
     dfree(h->d_qt_out);
     dfree(h->d_qt_cnt);
     dfree(h->d_status);
@@ -559,7 +564,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     // Replayed as a hipGraph: one submission instead of ~17 (launch overhead is most of a 640x480 frame's
     // latency).  The graph is re-captured when any buffer or size it holds changes.
     const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
-                                          h->d_spill_node, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
+                                          h->d_spill_node, h->d_qt_nodes, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
                                           h->d_cells, h->d_xtab, h->d_ytab, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
     bool launched = false;
@@ -1291,7 +1296,6 @@ orbx_status orbm_search_for_initialization_device(const orbx_keypoint* d_kps, co
         return ORBX_EINVAL;
     if (npairs == 0) return ORBX_OK;
     if (!d_pair_a || !d_pair_b || !d_matches12 || !d_nmatches) return ORBX_EINVAL;
-    if (search_init_smem_bytes(cap) > 160 * 1024) return ORBX_ENOSPC;
     hipStream_t s = (hipStream_t)stream;
     void* scratch = nullptr;
     if (hipMallocAsync(&scratch, search_init_scratch_bytes(nframes, npairs, cap), s) != hipSuccess)
@@ -1333,7 +1337,6 @@ orbx_status orbm_search_for_initialization(int device, const orbx_keypoint* kps1
     for (int i = 0; i < n1; ++i) matches12[i] = -1;
     if (n2 == 0) return ORBX_OK;   // every GetFeaturesInArea is empty
     const int cap = std::max(n1, n2);
-    if (search_init_smem_bytes(cap) > 160 * 1024) return ORBX_ENOSPC;
     HostCall c(device);
     const int meta[4] = {n1, n2, 0, 1};   // counts[2], pair (0, 1)
     const size_t om = c.in(meta, sizeof(meta));

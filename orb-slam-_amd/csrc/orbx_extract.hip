@@ -660,7 +660,6 @@ __device__ unsigned long long g_qt_prof[16][16];
 #else
 #define QT_STAMP(slot, t0) ((void)0)
 #endif
-constexpr uint16_t kNone = 0xFFFF;
 
 // Inclusive wave64 prefix sum with DPP: row shifts within each 16-lane row, then row broadcasts
 // (lane 15 into row 1 and 3, lane 31 into rows 2 and 3).  Six dependent VALU steps of a few cycles
@@ -719,7 +718,8 @@ struct QtLayout {
     size_t scan, rect, cnt, srank, npos, snode, smx, smy, ccnt, cpos, vprev, vnew, skey, best, wsum, sh, total;
 };
 
-__host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap)
+// ixb: bytes per node index (2 with the node arrays in LDS, 4 in global memory)
+__host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap, int ixb = 2)
 {
     QtLayout L;
     size_t o = 0;
@@ -734,15 +734,15 @@ __host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap)
     L.scan = take(sizeof(uint32_t) * scan_n);
     L.rect = take(sizeof(int16_t) * 4 * 2 * lcap);   // [2 buffers][4 coords][lcap]
     L.cnt = take(sizeof(uint32_t) * 2 * lcap);
-    L.srank = take(sizeof(uint16_t) * lcap);
-    L.npos = take(sizeof(uint16_t) * lcap);
-    L.snode = take(sizeof(uint16_t) * lcap);
+    L.srank = take((size_t)ixb * lcap);
+    L.npos = take((size_t)ixb * lcap);
+    L.snode = take((size_t)ixb * lcap);
     L.smx = take(sizeof(int16_t) * lcap);
     L.smy = take(sizeof(int16_t) * lcap);
     L.ccnt = take(sizeof(uint32_t) * 4 * lcap);
-    L.cpos = take(sizeof(uint16_t) * 4 * lcap);
-    L.vprev = take(sizeof(uint16_t) * lcap);
-    L.vnew = take(sizeof(uint16_t) * lcap);
+    L.cpos = take((size_t)ixb * 4 * lcap);
+    L.vprev = take((size_t)ixb * lcap);
+    L.vnew = take((size_t)ixb * lcap);
     L.skey = take(sizeof(uint32_t) * (p2 + 4));   // + padding to whole 16-byte groups (rank sort)
     L.best = take(sizeof(unsigned long long) * lcap);
     L.wsum = take(sizeof(uint32_t) * (QT_NW + 1));
@@ -751,10 +751,16 @@ __host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap)
     return L;
 }
 
-size_t quadtree_smem_bytes(const Geometry& g) { return qt_layout(g.lcap, g.max_cells_level).total; }
+// LDS of a global-node workgroup: the wave totals and the shared scalars only
+constexpr size_t kQtGlobWsum = 0, kQtGlobSh = 64, kQtGlobSmem = 128;
+// Largest LDS node layout a workgroup takes (the CU's 160 KiB); larger lists run from global memory.
+// The LDS form packs a keypoint's child slot (4 * lcap) beside its node index in one 32-bit word.
+constexpr size_t kQtLdsMax = 160 * 1024;
+constexpr int kQtLdsMaxList = 16383;
 
 // shared scalar slots
-enum { SH_N = 0, SH_L, SH_PHASE, SH_M, SH_DONE, SH_KK, SH_ERR, SH_S, SH_C, SH_NEWL };
+// SH_BIG: some phase-2 node holds more than 0xFFFF keys, so the packed (size, creation) sort key overflows
+enum { SH_N = 0, SH_L, SH_PHASE, SH_M, SH_DONE, SH_KK, SH_ERR, SH_S, SH_C, SH_NEWL, SH_BIG };
 
 // ctr[key] += 1 for every lane with key >= 0, one LDS atomic per run of equal keys in consecutive
 // lanes.  Lanes hold consecutive candidates (cell order), which are spatial neighbours and mostly fall
@@ -772,7 +778,7 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
     }
 }
 
-template <int QT_NT, int QT_KPT>
+template <int QT_NT, int QT_KPT, bool kG>
 #ifndef ORBX_QT0_WPE
 #define ORBX_QT0_WPE 4
 #endif
@@ -789,7 +795,13 @@ template <int QT_NT, int QT_KPT>
 //   <256,4>  (levels 2-7) 6: 80 VGPRs (3 spilled) instead of 100: 88 -> 70 us.
 // Smaller workgroups also find room beside describe's sooner under the pipeline (+1.5% frames/s together).
 // FAST at 5 (94 VGPRs, no spill) measured slower (485 -> 495 us) and keeps the compiler's choice.
-__global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WPE
+//
+// kG: the node arrays live in the level's global region (LevelGeom::qtg_off) instead of LDS, with 32-bit
+// node indices, for budgets whose node list outgrows a workgroup's LDS (e.g. Tracking's
+// 2 * nFeatures initialisation extractor, src/Tracking.cc:133, at 4000 features).  The algorithm and its
+// order of operations are the same; only the wave totals and the shared scalars stay in LDS.
+__global__ __launch_bounds__(QT_NT, kG ? 1
+                                    : (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WPE
                                     : (QT_NT == 512 && QT_KPT == 8) ? ORBX_QT1_WPE
                                     : (QT_NT == 256) ? ORBX_QT2_WPE : 1) void k_quadtree(int level0, const Geometry* __restrict__ G,
                                                    const Cell* __restrict__ cells,
@@ -797,10 +809,15 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
                                                    const int* __restrict__ cell_counts,
                                                    uint32_t* __restrict__ spill,
                                                    uint32_t* __restrict__ spill_node,
+                                                   uint8_t* __restrict__ gnodes,
                                                    uint32_t* __restrict__ qt_out, int* __restrict__ qt_cnt,
                                                    int* __restrict__ frame_counts, int* __restrict__ status,
                                                    int lcap, int cellcap)
 {
+    // node index type; kNoneI marks "no node" (and compares above every valid rank)
+    using Ix = typename std::conditional<kG, uint32_t, uint16_t>::type;
+    constexpr Ix kNoneI = (Ix)~(Ix)0;
+    constexpr uint32_t kPosMask = kG ? 0xFFFFFFFFu : 0xFFFFu;   // node position bits of a keypoint's node word
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int l = level0 + blockIdx.x, f = blockIdx.y;
     const int tid = threadIdx.x;
@@ -809,23 +826,25 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
 #endif
     const LevelGeom& LG = G->lv[l];
     // lcap / cellcap: node-list and cell capacity of this launch's levels (qt_launch)
-    const QtLayout Ly = qt_layout(lcap, cellcap);
-    uint32_t* scan = (uint32_t*)(smem + Ly.scan);
-    int16_t* rect = (int16_t*)(smem + Ly.rect);
-    uint32_t* cntb = (uint32_t*)(smem + Ly.cnt);
-    uint16_t* srank = (uint16_t*)(smem + Ly.srank);
-    uint16_t* npos = (uint16_t*)(smem + Ly.npos);
-    uint16_t* snode = (uint16_t*)(smem + Ly.snode);
-    int16_t* smx = (int16_t*)(smem + Ly.smx);
-    int16_t* smy = (int16_t*)(smem + Ly.smy);
-    uint32_t* ccnt = (uint32_t*)(smem + Ly.ccnt);
-    uint16_t* cpos = (uint16_t*)(smem + Ly.cpos);
-    uint16_t* vprev = (uint16_t*)(smem + Ly.vprev);
-    uint16_t* vnew = (uint16_t*)(smem + Ly.vnew);
-    uint32_t* skey = (uint32_t*)(smem + Ly.skey);
-    unsigned long long* best = (unsigned long long*)(smem + Ly.best);
-    uint32_t* wsum = (uint32_t*)(smem + Ly.wsum);
-    int* sh = (int*)(smem + Ly.sh);
+    const QtLayout Ly = qt_layout(lcap, cellcap, (int)sizeof(Ix));
+    uint8_t* nb = smem;
+    if constexpr (kG) nb = gnodes + (size_t)f * G->qtg_per_frame + LG.qtg_off;
+    uint32_t* scan = (uint32_t*)(nb + Ly.scan);
+    int16_t* rect = (int16_t*)(nb + Ly.rect);
+    uint32_t* cntb = (uint32_t*)(nb + Ly.cnt);
+    Ix* srank = (Ix*)(nb + Ly.srank);
+    Ix* npos = (Ix*)(nb + Ly.npos);
+    Ix* snode = (Ix*)(nb + Ly.snode);
+    int16_t* smx = (int16_t*)(nb + Ly.smx);
+    int16_t* smy = (int16_t*)(nb + Ly.smy);
+    uint32_t* ccnt = (uint32_t*)(nb + Ly.ccnt);
+    Ix* cpos = (Ix*)(nb + Ly.cpos);
+    Ix* vprev = (Ix*)(nb + Ly.vprev);
+    Ix* vnew = (Ix*)(nb + Ly.vnew);
+    uint32_t* skey = (uint32_t*)(nb + Ly.skey);
+    unsigned long long* best = (unsigned long long*)(nb + Ly.best);
+    uint32_t* wsum = (uint32_t*)(smem + (kG ? kQtGlobWsum : Ly.wsum));
+    int* sh = (int*)(smem + (kG ? kQtGlobSh : Ly.sh));
     // rect buffers: [buf][coord][lcap], coord 0..3 = x0, x1, y0, y1
     auto R = [&](int buf, int coord) { return rect + (size_t)(buf * 4 + coord) * lcap; };
 
@@ -860,10 +879,12 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
     // fit there, every thread copies whole cells into it (a cell's candidates are contiguous in its
     // slots) and then reads its own indices, instead of a binary search over the cells plus a
     // dependent cell-table load per candidate.
-    uint32_t* stage = (uint32_t*)(smem + Ly.rect);
+    uint32_t* stage = (uint32_t*)(nb + Ly.rect);
     // (small levels keep the search: their few hundred candidates spread over few cells, and a
-    // thread's serial copy of a whole cell costs more there than the lanes' parallel searches)
-    const bool staged = n >= 1024 && (size_t)n * 4 <= Ly.wsum - Ly.rect;   // block-uniform; wsum / sh untouched
+    // thread's serial copy of a whole cell costs more there than the lanes' parallel searches;
+    // a global region is sized to stage the level's every candidate slot, qt_prepare)
+    const bool staged = kG ? (long long)n * 4 <= LG.qtg_bytes - (long long)Ly.rect
+                           : n >= 1024 && (size_t)n * 4 <= Ly.wsum - Ly.rect;   // block-uniform; wsum / sh untouched
     if (staged) {
         for (int c = tid; c < ncl; c += QT_NT) {
             const int base = (int)scan[c], cnt = (c + 1 < ncl ? (int)scan[c + 1] : n) - base;
@@ -933,7 +954,7 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
     if (tid == 0) {
         int L = 0;
         for (int i = 0; i < nIni; ++i) {
-            npos[i] = kNone;
+            npos[i] = kNoneI;
             if (ccnt[i] > 0) {
                 if (L < lcap) {
                     R(0, 0)[L] = (int16_t)(int)(hX * (float)i);
@@ -942,7 +963,7 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
                     R(0, 3)[L] = (int16_t)LG.qh;
                     cntb[L] = ccnt[i];
                 }
-                npos[i] = (uint16_t)L;
+                npos[i] = (Ix)L;
                 ++L;
             }
         }
@@ -950,6 +971,7 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
         sh[SH_L] = L;
         sh[SH_PHASE] = 1;
         sh[SH_DONE] = 0;
+        sh[SH_BIG] = 0;
         sh[SH_ERR] = L > lcap ? kStatusListOverflow : 0;
         if (L > lcap) sh[SH_DONE] = 1;
     }
@@ -987,12 +1009,12 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
             for (int p = tid; p < L; p += QT_NT) {
                 if (cntc[p] > 1) {
                     const int s = (int)scan[p];
-                    srank[p] = (uint16_t)s;
-                    snode[s] = (uint16_t)p;
+                    srank[p] = (Ix)s;
+                    snode[s] = (Ix)p;
                 } else {
-                    srank[p] = kNone;
+                    srank[p] = kNoneI;
                 }
-                npos[p] = (uint16_t)(p - (int)scan[p]);   // rank among non-split nodes
+                npos[p] = (Ix)(p - (int)scan[p]);   // rank among non-split nodes
             }
         } else {
             // phase 2: sort vPrev by (size, creation) descending and split from the front.  The keys
@@ -1001,25 +1023,48 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
             // 16-byte reads, with one barrier in place of a bitonic network's log2(m)^2 / 2 stages.
             m = sh[SH_M];
             const int m4 = (m + 3) >> 2;
-            for (int k = tid; k < 4 * m4; k += QT_NT)
-                skey[k] = k < m ? ((cntc[vprev[k]] << 16) | (uint32_t)k) : 0u;   // 0: below every key
-            for (int p = tid; p < L; p += QT_NT) srank[p] = kNone;
+            for (int k = tid; k < 4 * m4; k += QT_NT) {
+                uint32_t key = 0u;   // 0: below every key
+                if (k < m) {
+                    const uint32_t c = cntc[vprev[k]];
+                    key = (c << 16) | (uint32_t)k;
+                    if (c > 0xFFFFu) sh[SH_BIG] = 1;   // the packed key would wrap (reset at the round's end)
+                }
+                skey[k] = key;
+            }
+            for (int p = tid; p < L; p += QT_NT) srank[p] = kNoneI;
             __syncthreads();
 #ifdef ORBX_QT_PROF
             long long qs = 0;
             if (threadIdx.x == 0) qs = clock64();
 #endif
-            const uint4* k4 = (const uint4*)skey;
-            for (int k = tid; k < m; k += QT_NT) {
-                const uint32_t key = skey[k];
-                int j = 0;
-                for (int i4 = 0; i4 < m4; ++i4) {
-                    const uint4 v = k4[i4];
-                    j += (int)(v.x > key) + (int)(v.y > key) + (int)(v.z > key) + (int)(v.w > key);
+            if (sh[SH_BIG] == 0 && m <= 0x10000) {   // block-uniform
+                const uint4* k4 = (const uint4*)skey;
+                for (int k = tid; k < m; k += QT_NT) {
+                    const uint32_t key = skey[k];
+                    int j = 0;
+                    for (int i4 = 0; i4 < m4; ++i4) {
+                        const uint4 v = k4[i4];
+                        j += (int)(v.x > key) + (int)(v.y > key) + (int)(v.z > key) + (int)(v.w > key);
+                    }
+                    const int p = vprev[k];
+                    srank[p] = (Ix)j;
+                    snode[j] = (Ix)p;
                 }
-                const int p = vprev[k];
-                srank[p] = (uint16_t)j;
-                snode[j] = (uint16_t)p;
+            } else {
+                // a node of more than 0xFFFF keys (huge levels with small budgets) or more than 2^16
+                // candidates: the same order, compared as (size, creation) pairs
+                for (int k = tid; k < m; k += QT_NT) {
+                    const uint32_t c = cntc[vprev[k]];
+                    int j = 0;
+                    for (int k2 = 0; k2 < m; ++k2) {
+                        const uint32_t c2 = cntc[vprev[k2]];
+                        j += (int)(c2 > c || (c2 == c && k2 > k));
+                    }
+                    const int p = vprev[k];
+                    srank[p] = (Ix)j;
+                    snode[j] = (Ix)p;
+                }
             }
 #ifdef ORBX_QT_PROF
             if (threadIdx.x == 0) atomicAdd(&g_qt_prof[l][4], (unsigned long long)(clock64() - qs));
@@ -1042,9 +1087,12 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
         __syncthreads();
         // a keypoint's child slot 4 * split rank + quadrant is kept in the upper half of its node word
         // for the relabel below (the lower half is the node's list position)
+        // (kG: node words hold the full position, and the relabel below recomputes the child slot;
+        // srank, smx and smy stay unchanged until then)
         auto child_key = [&](uint32_t k, uint32_t d) {
-            const int s = srank[d & 0xFFFF];
-            if (s == kNone) return -1;
+            const Ix sx = srank[d & kPosMask];
+            if (sx == kNoneI) return -1;
+            const int s = (int)sx;
             const int x = (int)(k & 0xFFF), y = (int)((k >> 12) & 0xFFF);
             return 4 * s + (x >= smx[s] ? 1 : 0) + (y >= smy[s] ? 2 : 0);
         };
@@ -1053,13 +1101,13 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
             if (wave_i0 + r * QT_NT >= n) break;   // wave-uniform
             const int i = tid + r * QT_NT;
             const int key = i < n ? child_key(kp[r], nd[r]) : -1;
-            nd[r] = (nd[r] & 0xFFFFu) | ((uint32_t)(key + 1) << 16);
+            if constexpr (!kG) nd[r] = (nd[r] & 0xFFFFu) | ((uint32_t)(key + 1) << 16);
             wave_run_add(ccnt, key);
         }
         for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) {
             uint32_t& d = fspill_node[i - QT_NT * QT_KPT];
             const int key = child_key(fspill[i - QT_NT * QT_KPT], d);
-            d = (d & 0xFFFFu) | ((uint32_t)(key + 1) << 16);
+            if constexpr (!kG) d = (d & 0xFFFFu) | ((uint32_t)(key + 1) << 16);
             if (key >= 0) atomicAdd(&ccnt[key], 1u);
         }
         __syncthreads();
@@ -1088,10 +1136,10 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
             __syncthreads();
             kk = sh[SH_KK];
             // non-split rank of every current node
-            for (int p = tid; p < L; p += QT_NT) scan[p] = (srank[p] != kNone && srank[p] < kk) ? 1u : 0u;
+            for (int p = tid; p < L; p += QT_NT) scan[p] = (srank[p] != kNoneI && (int)srank[p] < kk) ? 1u : 0u;
             __syncthreads();
             block_scan_excl<QT_NT>(scan, L, wsum);
-            for (int p = tid; p < L; p += QT_NT) npos[p] = (uint16_t)(p - (int)scan[p]);
+            for (int p = tid; p < L; p += QT_NT) npos[p] = (Ix)(p - (int)scan[p]);
             __syncthreads();
         }
 #ifdef ORBX_QT_PROF
@@ -1125,11 +1173,11 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
             for (int q = 3; q >= 0; --q) {
                 const uint32_t c = ccnt[4 * s + q];
                 if (c == 0) {
-                    cpos[4 * s + q] = kNone;
+                    cpos[4 * s + q] = kNoneI;
                     continue;
                 }
                 const int np = pos0 + j++;
-                cpos[4 * s + q] = (uint16_t)np;
+                cpos[4 * s + q] = (Ix)np;
                 nx0[np] = (int16_t)((q & 1) ? mx : x0);
                 nx1[np] = (int16_t)((q & 1) ? x1 : mx);
                 ny0[np] = (int16_t)((q & 2) ? my : y0);
@@ -1138,10 +1186,10 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
             }
         }
         for (int p = tid; p < L; p += QT_NT) {
-            const bool split = srank[p] != kNone && srank[p] < kk;
+            const bool split = srank[p] != kNoneI && (int)srank[p] < kk;
             if (!split) {
-                const int np = Ctot + npos[p];
-                npos[p] = (uint16_t)np;
+                const int np = Ctot + (int)npos[p];
+                npos[p] = (Ix)np;
                 nx0[np] = cx0[p];
                 nx1[np] = cx1[p];
                 ny0[np] = cy0[p];
@@ -1158,11 +1206,12 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
         __syncthreads();
         const int nexp = (int)block_scan_excl<QT_NT>(scan, 4 * kk, wsum);
         for (int e = tid; e < 4 * kk; e += QT_NT)
-            if (ccnt[e] > 1) vnew[scan[e]] = cpos[e];
+            if (ccnt[e] > 1) vnew[scan[e]] = cpos[e];   // (Ix)
         // relabel keypoints with their new list position
-        visit([&](uint32_t&, uint32_t& d, int) {
-            const int ck = (int)(d >> 16) - 1;   // child slot from the count pass, -1 if the node was not a candidate
-            d = (ck >= 0 && (ck >> 2) < kk) ? cpos[ck] : npos[d & 0xFFFF];
+        visit([&](uint32_t& k, uint32_t& d, int) {
+            // child slot from the count pass, -1 if the node was not a candidate
+            const int ck = kG ? child_key(k, d) : (int)(d >> 16) - 1;
+            d = (ck >= 0 && (ck >> 2) < kk) ? (uint32_t)cpos[ck] : (uint32_t)npos[d & kPosMask];
         });
         __syncthreads();
 #ifdef ORBX_QT_PROF
@@ -1179,6 +1228,7 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
                 }
             }
             sh[SH_M] = nexp;
+            sh[SH_BIG] = 0;
         }
         // vnew -> vprev for the next round
         for (int e = tid; e < nexp; e += QT_NT) vprev[e] = vnew[e];
@@ -1228,23 +1278,94 @@ __global__ __launch_bounds__(QT_NT, (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WP
     }
 }
 
-template <int NT, int KPT>
-static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, int l0, int nl, int batch,
-                      size_t, hipStream_t s)
+template <int NT, int KPT, bool kG>
+static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
+                      hipStream_t s)
 {
-    // LDS sized for the levels of this launch: a level's list never holds more than cap + 3 nodes (phase 1
-    // stops before L + 3 * expandable exceeds N, phase 2 once L >= N; cap >= max(N + 2, 4 * nIni)), so the
-    // coarse levels' workgroups take less LDS than level 0's and more of them fit on a CU
-    int lcap = 8, cellcap = 1;
-    for (int l = l0; l < l0 + nl; ++l) {
-        lcap = std::max(lcap, g.lv[l].cap + 4);
-        cellcap = std::max(cellcap, g.lv[l].ncells);
+    const size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap).total;
+    hipFuncSetAttribute((const void*)k_quadtree<NT, KPT, kG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL((k_quadtree<NT, KPT, kG>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
+                       b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt, frame_counts,
+                       b.status, q.lcap, q.cellcap);
+}
+
+// Launch groups.  A group's node capacity is the largest cap + 4 of its levels: a level's list never holds
+// more than cap + 3 nodes (phase 1 stops before L + 3 * expandable exceeds N, phase 2 once L >= N;
+// cap >= max(N + 2, 4 * nIni)), so the coarse levels' workgroups take less LDS than level 0's and more of
+// them fit on a CU.
+int qt_plan(const Geometry& g, int batch, QtGroup* out)
+{
+    auto caps = [&](QtGroup& q) {
+        q.lcap = 8;
+        q.cellcap = 1;
+        for (int l = q.l0; l < q.l0 + q.nl; ++l) {
+            q.lcap = std::max(q.lcap, g.lv[l].cap + 4);
+            q.cellcap = std::max(q.cellcap, g.lv[l].ncells);
+        }
+    };
+    bool anyg = false;
+    for (int l = 0; l < g.nlevels; ++l) anyg |= g.lv[l].qt_glob != 0;
+    // Small batches (the per-frame host path): one launch of the level-0 kernel over every level, so
+    // the levels run concurrently instead of as dependent launches (latency, not throughput).
+    // A level run with more register capacity than qt_regcap(g, l) spills less than its region holds.
+    if (batch <= kQtMergedMaxBatch && !anyg) {
+        QtGroup q{0, g.nlevels, 512, g.qt_kpt0, 0, 0, 0};
+        caps(q);
+        if (qt_layout(q.lcap, q.cellcap).total <= kQtLdsMax) {
+            out[0] = q;
+            return 1;
+        }
     }
-    const size_t smem = qt_layout(lcap, cellcap).total;
-    hipFuncSetAttribute((const void*)k_quadtree<NT, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL((k_quadtree<NT, KPT>), dim3(nl, batch), dim3(NT), smem, s, l0, b.geom, b.cells, b.slots,
-                       b.cell_counts, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts, b.status, lcap,
-                       cellcap);
+    // one launch per run of consecutive levels with the same configuration; the launched template is
+    // exactly qt_nt / qt_kpt, which size the spill regions
+    int n = 0;
+    for (int l0 = 0; l0 < g.nlevels;) {
+        const int nt = qt_nt(g, l0), kpt = qt_kpt(g, l0), gl = g.lv[l0].qt_glob;
+        int l1 = l0 + 1;
+        while (l1 < g.nlevels && qt_nt(g, l1) == nt && qt_kpt(g, l1) == kpt && g.lv[l1].qt_glob == gl) ++l1;
+        QtGroup q{l0, l1 - l0, nt, kpt, gl, 0, 0};
+        caps(q);
+        out[n++] = q;
+        l0 = l1;
+    }
+    return n;
+}
+
+bool qt_prepare(Geometry& g)
+{
+    // a level's own node list decides; a group whose shared capacity outgrows LDS moves to global too
+    for (int l = 0; l < g.nlevels; ++l) {
+        const int lc = g.lv[l].cap + 4;
+        g.lv[l].qt_glob = lc > kQtLdsMaxList || qt_layout(lc, g.lv[l].ncells).total > kQtLdsMax;
+        g.lv[l].qtg_off = g.lv[l].qtg_bytes = 0;
+    }
+    QtGroup grp[kQtMaxGroups];
+    for (;;) {
+        const int ng = qt_plan(g, 1 << 30, grp);
+        bool moved = false;
+        for (int i = 0; i < ng; ++i) {
+            if (grp[i].glob || qt_layout(grp[i].lcap, grp[i].cellcap).total <= kQtLdsMax) continue;
+            for (int l = grp[i].l0; l < grp[i].l0 + grp[i].nl; ++l) g.lv[l].qt_glob = 1;
+            moved = true;
+        }
+        if (moved) continue;
+        // global regions: the group's node layout with 32-bit indices, or room to stage every candidate
+        // slot of the level (the gather reads them in index order from there), whichever is larger
+        long long off = 0;
+        for (int i = 0; i < ng; ++i) {
+            if (!grp[i].glob) continue;
+            const QtLayout Ly = qt_layout(grp[i].lcap, grp[i].cellcap, 4);
+            for (int l = grp[i].l0; l < grp[i].l0 + grp[i].nl; ++l) {
+                long long bytes = std::max((long long)Ly.total, (long long)Ly.rect + 4LL * g.lv[l].slot_cap);
+                bytes = (bytes + 255) & ~255LL;
+                g.lv[l].qtg_off = off;
+                g.lv[l].qtg_bytes = bytes;
+                off += bytes;
+            }
+        }
+        g.qtg_per_frame = off;
+        return true;
+    }
 }
 
 #ifdef ORBX_QT_PROF
@@ -1263,29 +1384,15 @@ namespace orbx {
 
 void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s)
 {
-    const size_t smem = quadtree_smem_bytes(g);
-    // Small batches (the per-frame host path): one launch of the level-0 kernel over every level, so
-    // the levels run concurrently instead of as dependent launches (latency, not throughput).
-    // A level run with more register capacity than qt_regcap(g, l) spills less than its region holds.
-    if (batch <= kQtMergedMaxBatch) {
-        if (g.qt_kpt0 == 24)
-            qt_launch<512, 24>(g, b, frame_counts, 0, g.nlevels, batch, smem, s);
-        else
-            qt_launch<512, 16>(g, b, frame_counts, 0, g.nlevels, batch, smem, s);
-        return;
-    }
-    // one launch per run of consecutive levels with the same configuration; the launched template is
-    // exactly qt_nt / qt_kpt, which size the spill regions
-    for (int l0 = 0; l0 < g.nlevels;) {
-        const int nt = qt_nt(g, l0), kpt = qt_kpt(g, l0);
-        int l1 = l0 + 1;
-        while (l1 < g.nlevels && qt_nt(g, l1) == nt && qt_kpt(g, l1) == kpt) ++l1;
-        const int nl = l1 - l0;
-        if (nt == 512 && kpt == 24) qt_launch<512, 24>(g, b, frame_counts, l0, nl, batch, smem, s);
-        else if (nt == 512 && kpt == 16) qt_launch<512, 16>(g, b, frame_counts, l0, nl, batch, smem, s);
-        else if (nt == 512) qt_launch<512, 8>(g, b, frame_counts, l0, nl, batch, smem, s);
-        else qt_launch<256, 4>(g, b, frame_counts, l0, nl, batch, smem, s);
-        l0 = l1;
+    QtGroup grp[kQtMaxGroups];
+    const int ng = qt_plan(g, batch, grp);
+    for (int i = 0; i < ng; ++i) {
+        const QtGroup& q = grp[i];
+        if (q.glob) qt_launch<kQtGlobNT, kQtGlobKPT, true>(g, b, frame_counts, q, batch, s);
+        else if (q.nt == 512 && q.kpt == 24) qt_launch<512, 24, false>(g, b, frame_counts, q, batch, s);
+        else if (q.nt == 512 && q.kpt == 16) qt_launch<512, 16, false>(g, b, frame_counts, q, batch, s);
+        else if (q.nt == 512) qt_launch<512, 8, false>(g, b, frame_counts, q, batch, s);
+        else qt_launch<256, 4, false>(g, b, frame_counts, q, batch, s);
     }
 }
 

@@ -42,6 +42,10 @@ struct LevelGeom {
     float patch_size;         // (float)(int)(PATCH_SIZE * scale)
     int roi_mw, roi_mh;       // largest FAST cell ROI of this level
     int pyr_win;              // 1: every 4-column group's taps lie in 8 bytes from its first tap (K1 window path)
+    // K3 node arrays: in LDS (qt_glob 0), or, for budgets whose node list outgrows a workgroup's LDS,
+    // in a per-(frame, level) global region of qtg_bytes at qtg_off inside the frame's node block
+    int qt_glob;
+    long long qtg_off, qtg_bytes;
 };
 
 struct Geometry {
@@ -61,6 +65,7 @@ struct Geometry {
     int lcap;                 // quadtree list capacity (max level cap + slack)
     int qt_kpt0;              // level-0 quadtree keypoints per thread (16, or 24 for large frames)
     long long pyr_bytes;      // bytes per frame for levels 1..L-1
+    long long qtg_per_frame;  // K3 global node block per frame (0: every level's node list fits LDS)
     int umax[16];
     LevelGeom lv[kMaxLevels];
 };

@@ -26,6 +26,7 @@ struct ExtractBufs {
     int* cell_counts;           // [B][ncells]
     uint32_t* spill;            // [B][spill_per_frame] quadtree overflow (packed kp)
     uint32_t* spill_node;       // [B][spill_per_frame]
+    uint8_t* qt_nodes;          // [B][qtg_per_frame] K3 node arrays of the levels whose list outgrows LDS
     uint32_t* qt_out;           // [B][out_per_frame] retained keypoints (level coords)
     int* qt_cnt;                // [B][nlevels]
     int* status;                // device error word (bit flags)
@@ -49,7 +50,16 @@ enum : int {
     kStatusCapOverflow = 4,
 };
 
-size_t quadtree_smem_bytes(const Geometry& g);
+// K3 launch plan: runs of consecutive levels sharing a kernel configuration.  glob: the node arrays
+// live in global memory (ExtractBufs::qt_nodes) because lcap nodes need more LDS than a workgroup has.
+struct QtGroup {
+    int l0, nl, nt, kpt, glob, lcap, cellcap;
+};
+constexpr int kQtMaxGroups = kMaxLevels + 1;
+int qt_plan(const Geometry& g, int batch, QtGroup* out);   // returns the group count
+// host: decides qt_glob per level and lays out the per-frame global node block (qtg_*); false if a
+// level cannot be run at all
+bool qt_prepare(Geometry& g);
 // quadtree workgroup size and keypoints held in registers per thread at level l (the rest spill
 // to global): level 0 holds most candidates, levels >= 2 a few hundred
 // (level 0: 16 per thread, or 24 for frames above kQtBigArea pixels, whose level-0 candidates
@@ -63,8 +73,16 @@ constexpr int kLatencyMaxBatch = 8;    // batches up to this size: FAST one cell
 // fewer waves per workgroup on the small levels does not shorten them (one wave for levels 3-7:
 // 70 us against 84 us for 256 threads on levels 2-7 together, plus a separate level-2 launch), since
 // a split round is a chain of dependent LDS steps whatever the workgroup size.
-__host__ __device__ inline int qt_nt(const Geometry& g, int l) { return l >= 2 ? 256 : 512; }
-__host__ __device__ inline int qt_kpt(const Geometry& g, int l) { return l == 0 ? g.qt_kpt0 : (l == 1 ? 8 : 4); }
+// Levels whose node list runs from global memory (LevelGeom::qt_glob) take one configuration.
+constexpr int kQtGlobNT = 512, kQtGlobKPT = 8;
+__host__ __device__ inline int qt_nt(const Geometry& g, int l)
+{
+    return g.lv[l].qt_glob ? kQtGlobNT : (l >= 2 ? 256 : 512);
+}
+__host__ __device__ inline int qt_kpt(const Geometry& g, int l)
+{
+    return g.lv[l].qt_glob ? kQtGlobKPT : (l == 0 ? g.qt_kpt0 : (l == 1 ? 8 : 4));
+}
 __host__ __device__ inline int qt_regcap(const Geometry& g, int l) { return qt_nt(g, l) * qt_kpt(g, l); }
 
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
@@ -80,7 +98,6 @@ void launch_best2_csr(const uint8_t* q, int nq, const uint8_t* t, const int* ptr
                       int* bi, int* b1, int* b2, hipStream_t s);
 void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, uint16_t* out, hipStream_t s);
 size_t search_init_scratch_bytes(int nframes, int npairs, int cap);
-size_t search_init_smem_bytes(int cap);   // k_si_greedy's LDS (must fit 160 KiB)
 // prev: [npairs][cap] float2 vbPrevMatched (window centres in, matched F2 positions out) or NULL
 void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int nframes, int cap,
                         const int* pa, const int* pb, int npairs, const orbm_grid& G, int window, float nnratio,

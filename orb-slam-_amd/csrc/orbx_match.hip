@@ -530,6 +530,10 @@ __host__ __device__ inline SgLayout sg_layout(int cap)
     return L;
 }
 
+// kG: the per-pair arrays live in a global region (gbuf, sg_stride bytes per pair) instead of LDS, for frames
+// with more level-0 keypoints than a workgroup's LDS holds (about 3,800; e.g. Tracking's 2 * nFeatures
+// initialisation extractor at 1080p and beyond).  Same algorithm; the histogram stays in LDS.
+template <bool kG>
 __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restrict__ kps,
                                                    const uint8_t* __restrict__ desc, const int* __restrict__ counts,
                                                    int cap, const int* __restrict__ pa, const int* __restrict__ pb,
@@ -539,9 +543,9 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
                                                    const float2* __restrict__ gxy, const int* __restrict__ gn,
                                                    const int* __restrict__ qcnt, const uint4* __restrict__ qtop,
                                                    int* __restrict__ m12_out, int* __restrict__ nm_out, int lcap,
-                                                   int tier_lo)
+                                                   int tier_lo, uint8_t* __restrict__ gbuf, size_t sg_stride)
 {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_lds[];
 #ifdef ORBX_SI_PROF
     const long long pt0 = clock64();
 #endif
@@ -554,6 +558,8 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
         if (n0 <= tier_lo || n0 > lcap) return;
     }
     const SgLayout Ly = sg_layout(lcap);
+    uint8_t* smem = smem_lds;
+    if constexpr (kG) smem = gbuf + (size_t)blockIdx.x * sg_stride;
     uint4* top = (uint4*)(smem + Ly.top);
     int* cnt = (int*)(smem + Ly.cnt);
     float* ang1 = (float*)(smem + Ly.ang1);
@@ -846,12 +852,26 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
 #endif
 }
 
-size_t search_init_scratch_bytes(int nframes, int npairs, int cap)
+// largest level-0 count whose greedy-pass arrays fit a workgroup's 160 KiB of LDS; larger frames take the
+// global-array launch (k_si_greedy<true>)
+static int si_lds_max_cap()
 {
-    return (size_t)nframes * cap * (4 + 8) + (size_t)nframes * 2 * 4 + (size_t)npairs * cap * (4 + 16) + 64 * 6;
+    static const int c = [] {
+        int v = 32767;
+        while (v > 1 && sg_layout(v).total > 160 * 1024 - 256) v -= 16;   // + the static histogram
+        return v;
+    }();
+    return c;
 }
 
-size_t search_init_smem_bytes(int cap) { return sg_layout(cap).total; }
+static size_t si_global_stride(int cap) { return (sg_layout(cap).total + 255) & ~(size_t)255; }
+
+size_t search_init_scratch_bytes(int nframes, int npairs, int cap)
+{
+    size_t b = (size_t)nframes * cap * (4 + 8) + (size_t)nframes * 2 * 4 + (size_t)npairs * cap * (4 + 16) + 64 * 7;
+    if (cap > si_lds_max_cap()) b += (size_t)npairs * si_global_stride(cap);
+    return b;
+}
 
 void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int* counts, int nframes, int cap,
                         const int* pa, const int* pb, int npairs, const orbm_grid& G, int window, float nnratio,
@@ -876,18 +896,26 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     const int qsplit = std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
     hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, G,
                        window, (const float2*)prev, gkeys, gxy, gn, qcnt, qtop);
-    hipFuncSetAttribute((const void*)k_si_greedy, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)sg_layout(cap).total);
-    // tiers by level-0 count: up to 512 (22 KB per workgroup), up to kSiLdsCap (two workgroups per CU), cap;
-    // a launch whose tier holds no pair costs a few microseconds (its workgroups return at once)
-    const int tiers[3] = {std::min(cap, kSiGreedySmall), std::min(cap, kSiLdsCap), cap};
+    const int ldscap = std::min(cap, si_lds_max_cap());
+    hipFuncSetAttribute((const void*)k_si_greedy<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)sg_layout(ldscap).total);
+    // tiers by level-0 count: up to 512 (22 KB per workgroup), up to kSiLdsCap (two workgroups per CU), the
+    // LDS maximum, then cap from global memory; a launch whose tier holds no pair costs a few microseconds
+    // (its workgroups return at once)
+    const int tiers[3] = {std::min(cap, kSiGreedySmall), std::min(cap, kSiLdsCap), ldscap};
     int lo = -1;
     for (int t = 0; t < 3; ++t) {
         if (tiers[t] <= lo) continue;
-        hipLaunchKernelGGL(k_si_greedy, dim3(npairs), dim3(256), sg_layout(tiers[t]).total, s, kps, desc, counts, cap,
-                           pa, pb, G, window, nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm,
-                           tiers[t], lo);
+        hipLaunchKernelGGL(k_si_greedy<false>, dim3(npairs), dim3(256), sg_layout(tiers[t]).total, s, kps, desc,
+                           counts, cap, pa, pb, G, window, nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt,
+                           qtop, m12, nm, tiers[t], lo, (uint8_t*)nullptr, (size_t)0);
         lo = tiers[t];
+    }
+    if (cap > lo) {
+        uint8_t* gbuf = carve((size_t)npairs * si_global_stride(cap));
+        hipLaunchKernelGGL(k_si_greedy<true>, dim3(npairs), dim3(256), 0, s, kps, desc, counts, cap, pa, pb, G, window,
+                           nnratio, check_ori, (float2*)prev, gkeys, gxy, gn, qcnt, qtop, m12, nm, cap, lo, gbuf,
+                           si_global_stride(cap));
     }
 }
 

@@ -219,11 +219,20 @@ def test_host_edge_cases(orbref, cuda):
     with pytest.raises(orbx.OrbxError) as e:
         m.SearchForInitialization((bad, d), (k, d, (640, 480)), _xy(k), 100)
     assert e.value.code == orbx.EINVAL
-    # more keypoints than the greedy pass's LDS holds: ENOSPC, not a failed launch
+    # more keypoints than the greedy pass's LDS holds (device-memory form), all in one grid cell with equal
+    # descriptors: every query sees the same 3 candidates at distance 0
     big = np.zeros(5000, orbx.KEYPOINT_DTYPE)
+    big["x"], big["y"], big["size"], big["class_id"] = 11.0, 12.0, 31.0, -1
+    bd = np.zeros((5000, 32), np.uint8)
+    got_prev = _xy(big)
+    n, m12 = m.SearchForInitialization((big, bd), (k, d, (640, 480)), got_prev, 100)
+    want = orbref.search_for_initialization(big, bd, k, d, 640, 480, prev_xy=_xy(big))
+    _check("host 5000 x 3", n, m12, got_prev, want)
+    # past the int16 match vectors: EINVAL
     with pytest.raises(orbx.OrbxError) as e:
-        m.SearchForInitialization((big, np.zeros((5000, 32), np.uint8)), (k, d, (640, 480)), _xy(big), 100)
-    assert e.value.code == orbx.ENOSPC
+        huge = np.zeros(40000, orbx.KEYPOINT_DTYPE)
+        m.SearchForInitialization((huge, np.zeros((40000, 32), np.uint8)), (k, d, (640, 480)), _xy(huge), 100)
+    assert e.value.code == orbx.EINVAL
 
 
 def _synthetic_level0(n, seed, shift=(0.0, 0.0), base=None, W=1241, H=376):
@@ -252,42 +261,47 @@ def _synthetic_level0(n, seed, shift=(0.0, 0.0), base=None, W=1241, H=376):
 
 def test_more_level0_keypoints_than_the_common_launch_holds(orbref, cuda):
     """The greedy pass keeps up to 1792 level-0 keypoints per frame in LDS in its common launch (two
-    workgroups per CU); a pair with more goes to a second, full-size launch.  One device call with a
-    2400-keypoint pair and a 500-keypoint pair runs both launches; the host entry with 2400 runs the second."""
+    workgroups per CU); a pair with more goes to a launch sized for the LDS maximum (~3,800), and past that to
+    a launch whose arrays live in device memory.  One device call with a 6000-, a 2400- and a 500-keypoint
+    pair runs all of them; the host entry with 2400 and 6000 runs the last two."""
     import torch
     import orbx
-    W_, H_ = 1241, 376
-    ka, da = _synthetic_level0(2400, 1)
-    kb, db = _synthetic_level0(2400, 2, shift=(6.0, -2.0), base=(ka, da))
-    kc, dc = _synthetic_level0(500, 3)
-    kd, dd = _synthetic_level0(500, 4, shift=(-9.0, 4.0), base=(kc, dc))
-    frames = [(ka, da), (kb, db), (kc, dc), (kd, dd)]
-    cap = 2400
-    kp = np.zeros((4, cap, 7), np.int32)
-    ds = np.zeros((4, cap, 32), np.uint8)
+    W_, H_ = 1920, 1080
+    ka, da = _synthetic_level0(2400, 1, W=W_, H=H_)
+    kb, db = _synthetic_level0(2400, 2, shift=(6.0, -2.0), base=(ka, da), W=W_, H=H_)
+    kc, dc = _synthetic_level0(500, 3, W=W_, H=H_)
+    kd, dd = _synthetic_level0(500, 4, shift=(-9.0, 4.0), base=(kc, dc), W=W_, H=H_)
+    ke, de = _synthetic_level0(6000, 5, W=W_, H=H_)
+    kf, df = _synthetic_level0(6000, 6, shift=(3.0, 5.0), base=(ke, de), W=W_, H=H_)
+    frames = [(ka, da), (kb, db), (kc, dc), (kd, dd), (ke, de), (kf, df)]
+    cap = 6000
+    kp = np.zeros((6, cap, 7), np.int32)
+    ds = np.zeros((6, cap, 32), np.uint8)
     for f, (k, d) in enumerate(frames):
         kp[f, :len(k)] = k.view(np.int32).reshape(-1, 7)
         ds[f, :len(k)] = d
     tk, td = torch.from_numpy(kp).to(cuda), torch.from_numpy(ds).to(cuda)
     tc = torch.tensor([len(k) for k, _ in frames], dtype=torch.int32, device=cuda)
-    pa = torch.tensor([0, 2], dtype=torch.int32, device=cuda)
-    pb = torch.tensor([1, 3], dtype=torch.int32, device=cuda)
+    pa = torch.tensor([0, 2, 4], dtype=torch.int32, device=cuda)
+    pb = torch.tensor([1, 3, 5], dtype=torch.int32, device=cuda)
     m = orbx.ORBmatcher(0.9, True)
-    prev = np.zeros((2, cap, 2), np.float32)
+    prev = np.zeros((3, cap, 2), np.float32)
     prev[0, :2400] = _xy(ka)
     prev[1, :500] = _xy(kc)
+    prev[2, :6000] = _xy(ke)
     pv = torch.from_numpy(prev).to(cuda)
     dm12, dnm = m.search_for_initialization_batch(tk, td, tc, pa, pb, H_, W_, 100, bounds=(0.0, W_, 0.0, H_),
                                                   prev_matched=pv)
     torch.cuda.synchronize()
     dm12, dnm, pv = dm12.cpu().numpy(), dnm.cpu().numpy(), pv.cpu().numpy()
-    for p, (a, b) in enumerate([(0, 1), (2, 3)]):
+    for p, (a, b) in enumerate([(0, 1), (2, 3), (4, 5)]):
         n = len(frames[a][0])
         want = orbref.search_for_initialization(frames[a][0], frames[a][1], frames[b][0], frames[b][1], W_, H_,
                                                 prev_xy=prev[p, :n])
         assert want[0] > n // 4, "pair %d: only %d oracle matches" % (p, want[0])
         _check("device pair %d" % p, int(dnm[p]), dm12[p, :n], pv[p, :n], want)
-    got_prev = _xy(ka)
-    n, m12 = m.SearchForInitialization((ka, da), (kb, db, (W_, H_)), got_prev, 100)
-    want = orbref.search_for_initialization(ka, da, kb, db, W_, H_, prev_xy=_xy(ka))
-    _check("host 2400", n, m12, got_prev, want)
+    for (k1, d1), (k2, d2) in (((ka, da), (kb, db)), ((ke, de), (kf, df))):
+        got_prev = _xy(k1)
+        n, m12 = m.SearchForInitialization((k1, d1), (k2, d2, (W_, H_)), got_prev, 100)
+        want = orbref.search_for_initialization(k1, d1, k2, d2, W_, H_, prev_xy=_xy(k1))
+        _check("host %d" % len(k1), n, m12, got_prev, want)
