@@ -93,8 +93,30 @@ def level_sizes():
     return [(int(np.rint(np.float32(W) * i)), int(np.rint(np.float32(H) * i))) for i in inv]
 
 
+_NATIVE = {"built": None}
+
+
+def native_oracle():
+    """Build the CPU-baseline copy of oracle/orbref.c on this host with -march=native (the reference's own
+    flag) and point orbref at it (ORBREF_LIB).  Parity tests keep the portable
+    x86-64-v3 build; -ffp-contract=off keeps the arithmetic identical.  Returns the flag used."""
+    if _NATIVE["built"] is None:
+        import tempfile
+        out = os.path.join(tempfile.mkdtemp(prefix="orbref_native_"), "liborbref_native.so")
+        try:
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", "NATIVE_OUT=" + out],
+                           check=True, capture_output=True, timeout=120)
+            os.environ["ORBREF_LIB"] = out
+            _NATIVE["built"] = "-O3 -march=native"
+        except Exception as e:   # no compiler: the prebuilt portable copy
+            log("native oracle build failed (%s); CPU baseline uses the x86-64-v3 build" % e)
+            _NATIVE["built"] = "-O3 -march=x86-64-v3 (native build failed)"
+    return _NATIVE["built"]
+
+
 def cpu_baseline(frames: np.ndarray, budget_s: float):
     """Oracle (scalar C restatement of the reference, 1 thread) on a bounded sample."""
+    flags = native_oracle()
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orbref
     p = orbref.make_params(NFEAT, SCALE, NLEVELS, INI, MINTH)
@@ -118,8 +140,8 @@ def cpu_baseline(frames: np.ndarray, budget_s: float):
     except Exception:
         pass
     return {"value": n / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": "oracle/orbref scalar C restatement (-O3 -march=x86-64-v3), frames 0..%d of the config-2 "
-                      "sequence, extract + SearchForInitialization(t-1,t), 1 thread, %.1f s" % (n - 1, dt),
+            "sample": "oracle/orbref scalar C restatement (%s), frames 0..%d of the config-2 "
+                      "sequence, extract + SearchForInitialization(t-1,t), 1 thread, %.1f s" % (flags, n - 1, dt),
             "host_cpu": model or platform.processor(), "host_threads": os.cpu_count()}
 
 
@@ -127,6 +149,7 @@ def cpu_baseline_all_cores(frames: np.ndarray, budget_s: float, threads: int = 1
     """`threads` workers, each with its own contiguous block of the sequence
     (extract + SearchForInitialization within the block), the oracle's C calls release the GIL."""
     import threading
+    flags = native_oracle()
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orbref
     p = orbref.make_params(NFEAT, SCALE, NLEVELS, INI, MINTH)
@@ -152,8 +175,8 @@ def cpu_baseline_all_cores(frames: np.ndarray, budget_s: float, threads: int = 1
         t.join()
     dt = time.perf_counter() - t0
     return {"value": sum(done) / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": "oracle/orbref, %d threads each on its own block of the config-2 sequence, extract + "
-                      "SearchForInitialization(t-1,t), %d frames in %.1f s" % (threads, sum(done), dt)}
+            "sample": "oracle/orbref (%s), %d threads each on its own block of the config-2 sequence, extract + "
+                      "SearchForInitialization(t-1,t), %d frames in %.1f s" % (flags, threads, sum(done), dt)}
 
 
 def main():
@@ -245,12 +268,13 @@ def main():
     for j in range(P):
         exs[j].sync(streams[j])   # raises on device-side overflow
     elapsed = t1 - t0
+    # results of the last timed step, read now: the host-fed leg below reuses the payloads and m12 / nm
+    counts = last_payload[0].counts.cpu().numpy()
+    nmatch = nm[(args.warmup + args.steps - 1) % P].cpu().numpy()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    payload = last_payload[0]
-    nm = nm[(args.warmup + args.steps - 1) % P]
     used = sorted({(args.warmup + k) % P for k in range(args.steps)})
     stage_ms = sum(exs[j].stage_times() for j in used)   # sums over the timed steps (all streams)
     match_ms = sum(a.elapsed_time(b) for a, b in ev_m)
@@ -344,8 +368,6 @@ def main():
         with torch.cuda.stream(streams[j]):
             hands[j].drain()
     torch.cuda.synchronize()
-    counts = payload.counts.cpu().numpy()
-    nmatch = nm.cpu().numpy()
 
     if rank != 0:
         if world > 1:
@@ -418,10 +440,14 @@ def main():
                     ins = sum(per[k]["SQ_INSTS_VALU"] for k in parts)
                     rate = ins / t_launch / 1e9
                     pk, pins, p2 = valu_peak(kname)
-                    r["valu"] = {"insts_per_launch": int(ins), "achieved": round(rate, 1), "peak": pk,
-                                 "unit": "G wave-instr/s", "frac": round(rate / pk, 4),
-                                 "peak_basis": "measured issue rate of %s, 8 waves/SIMD (profiles/r02/valu_rate.json)"
-                                               % pins, "peak_2cycle_ops": p2}
+                    r["valu_issue"] = {
+                        "insts_per_launch": int(ins), "achieved": round(rate, 1), "peak": pk,
+                        "unit": "G wave-instr/s", "frac": round(rate / pk, 4),
+                        "peak_basis": "measured issue rate of %s, 8 waves/SIMD (profiles/r02/valu_rate.json)" % pins,
+                        "peak_2cycle_ops": p2,
+                        "note": "an issue ratio against the rate of the kernel's slowest (4-cycle) dominant "
+                                "instruction: an upper bound on how issue-bound the kernel is, not proof that the "
+                                "VALU pipe is its limiter (DESIGN.md section 6)"}
             except Exception:
                 pass
         return r
@@ -484,8 +510,9 @@ def main():
             nproc = os.cpu_count() or args.cpu_threads
             out["cpu_baseline_nproc_extrapolated"] = {
                 "value": round(allc["value"] / args.cpu_threads * nproc, 1), "unit": "frames/s", "cores": nproc,
-                "kind": "port, extrapolated", "sample": "cpu_baseline_all_cores x %d / %d threads (linear)" % (
-                    nproc, args.cpu_threads)}
+                "kind": "port, extrapolated", "extrapolated": True,
+                "sample": "NOT MEASURED: cpu_baseline_all_cores x %d / %d threads, a linear extrapolation (the box "
+                          "gives one GPU's job a %d-CPU share)" % (nproc, args.cpu_threads, args.cpu_threads)}
             out["speedup_vs_cpu_nproc_extrapolated"] = round(value / out["cpu_baseline_nproc_extrapolated"]["value"], 1)
     print(json.dumps(out), flush=True)
     if world > 1:

@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "liborbref.so")
+# ORBREF_LIB: another build of orbref.c (bench.py's -march=native CPU-baseline copy)
+_LIB_PATH = os.environ.get("ORBREF_LIB") or os.path.join(_HERE, "_build", "liborbref.so")
 _FAITHFUL_PATH = os.path.join(_HERE, "_build", "liborbref_faithful.so")
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -67,6 +68,8 @@ class FeatVec(C.Structure):
 
 
 def build(force: bool = False) -> str:
+    if os.environ.get("ORBREF_LIB"):
+        return _LIB_PATH
     if force or not os.path.exists(_LIB_PATH) or not os.path.exists(_FAITHFUL_PATH):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH

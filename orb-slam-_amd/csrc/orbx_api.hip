@@ -104,14 +104,6 @@ void dfree(T*& p)
     p = nullptr;
 }
 
-template <class T>
-bool dalloc(T*& p, size_t count)
-{
-    dfree(p);
-    if (count == 0) count = 1;
-    return hipMalloc((void**)&p, sizeof(T) * count) == hipSuccess;
-}
-
 }  // namespace
 
 struct orbx_handle {
@@ -167,9 +159,40 @@ struct orbx_handle {
     bool timing = false;
     std::vector<hipEvent_t> ev;
     int ev_used = 0;
+
+    // Buffers only grow, and an outgrown one is retired until orbx_destroy rather than freed:
+    // hipFree / hipHostFree wait for the whole device, which would stall every other stream of the
+    // process (the other extractor and matcher threads).  Capacities (bytes) per live buffer.
+    std::vector<std::pair<const void*, size_t>> caps;
+    std::vector<void*> retired_dev, retired_pin;
 };
 
 namespace {
+
+size_t& cap_of(orbx_handle* h, const void* p)
+{
+    for (auto& c : h->caps)
+        if (c.first == p) return c.second;
+    h->caps.emplace_back(p, 0);
+    return h->caps.back().second;
+}
+
+// p holds at least `count` T afterwards (contents not kept); grows geometrically, never frees
+template <class T>
+bool dalloc(orbx_handle* h, T*& p, size_t count)
+{
+    const size_t bytes = sizeof(T) * (count ? count : 1);
+    if (p && cap_of(h, p) >= bytes) return true;
+    if (p) h->retired_dev.push_back((void*)p);
+    const size_t want = std::max(bytes, p ? cap_of(h, p) + cap_of(h, p) / 2 : bytes);
+    p = nullptr;
+    if (hipMalloc((void**)&p, want) != hipSuccess) {
+        p = nullptr;
+        return false;
+    }
+    cap_of(h, p) = want;
+    return true;
+}
 
 // The handle's own stream serves the synchronous host paths only.  It is created on
 // first use: device-batch users bring their own streams, and every idle stream would
@@ -298,15 +321,22 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     g.spill_per_frame = std::max(spill, 1);
 
     // once per image size: the tables go up on the handle's own stream (never the legacy null stream)
-    if (!dalloc(h->d_geom, 1) || !dalloc(h->d_cells, cells.size()) || !dalloc(h->d_xtab, xt.size()) ||
-        !dalloc(h->d_ytab, yt.size()))
+    if (!dalloc(h, h->d_geom, 1) || !dalloc(h, h->d_cells, cells.size()) || !dalloc(h, h->d_xtab, xt.size()) ||
+        !dalloc(h, h->d_ytab, yt.size()))
         return ORBX_ENOMEM;
-    hipStream_t s = own_stream(h);
-    hipMemcpyAsync(h->d_geom, &g, sizeof(g), hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(h->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice, s);
-    if (!xt.empty()) hipMemcpyAsync(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice, s);
-    if (!yt.empty()) hipMemcpyAsync(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice, s);
-    if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    // on a pooled host-call stream (high priority, orbx_host.hip), so that a handle used only through
+    // orbx_extract_batch_device never creates a stream of its own (each takes one of the process's
+    // few hardware queues); the copies are complete before any later launch on any stream
+    {
+        HostCall c(h->device);
+        hipStream_t s = c.stream();
+        if (!s) return ORBX_EDEVICE;
+        hipMemcpyAsync(h->d_geom, &g, sizeof(g), hipMemcpyHostToDevice, s);
+        hipMemcpyAsync(h->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice, s);
+        if (!xt.empty()) hipMemcpyAsync(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice, s);
+        if (!yt.empty()) hipMemcpyAsync(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice, s);
+        if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    }
     h->geom = g;
     h->cells = std::move(cells);
     h->grows = rows;
@@ -322,11 +352,11 @@ orbx_status ensure_batch(orbx_handle* h, int batch)
     if (batch <= h->batch_cap) return ORBX_OK;
     const Geometry& g = h->geom;
     const size_t B = (size_t)batch;
-    if (!dalloc(h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h->d_slots, (size_t)g.slots_per_frame * B) ||
-        !dalloc(h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h->d_spill, (size_t)g.spill_per_frame * B) ||
-        !dalloc(h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h->d_qt_out, (size_t)g.out_per_frame * B) ||
-        !dalloc(h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h->d_status, 16) ||
-        !dalloc(h->d_qt_nodes, (size_t)g.qtg_per_frame * B)) {
+    if (!dalloc(h, h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h, h->d_slots, (size_t)g.slots_per_frame * B) ||
+        !dalloc(h, h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h, h->d_spill, (size_t)g.spill_per_frame * B) ||
+        !dalloc(h, h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h, h->d_qt_out, (size_t)g.out_per_frame * B) ||
+        !dalloc(h, h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h, h->d_status, 16) ||
+        !dalloc(h, h->d_qt_nodes, (size_t)g.qtg_per_frame * B)) {
         h->batch_cap = 0;
         return ORBX_ENOMEM;
     }
@@ -352,9 +382,21 @@ ExtractBufs bufs(orbx_handle* h)
     return b;
 }
 
-// the extraction's stream work alone (no host state): also what the host path's graph captures
+// the next set of 5 stage-boundary events of a timed handle (orbx_set_timing)
+const hipEvent_t* next_stage_events(orbx_handle* h)
+{
+    if ((size_t)(h->ev_used + 1) * 5 > h->ev.size()) {
+        const size_t old = h->ev.size();
+        h->ev.resize(old + 5 * 64);
+        for (size_t i = old; i < h->ev.size(); ++i) hipEventCreate(&h->ev[i]);
+    }
+    return &h->ev[(size_t)(h->ev_used++) * 5];
+}
+
+// the extraction's stream work alone (no host state): also what the host path's graph captures;
+// ev (timed handles): events recorded at the 5 stage boundaries
 void enqueue_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoint* kps, uint8_t* desc, int* counts,
-                      int cap, hipStream_t s)
+                      int cap, hipStream_t s, const hipEvent_t* ev = nullptr)
 {
     const Geometry& g = h->geom;
     ExtractBufs b = bufs(h);
@@ -363,36 +405,6 @@ void enqueue_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoi
     } else {
         hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
         hipMemsetAsync(h->d_status, 0, sizeof(int), s);
-    }
-    launch_pyramid(g, b, P, batch, s);
-    launch_fast(g, b, P, batch, s);
-    launch_quadtree(g, b, counts, batch, s);
-    launch_describe(g, b, P, kps, desc, cap, batch, s);
-}
-
-orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoint* kps, uint8_t* desc,
-                         int* counts, int cap, hipStream_t s)
-{
-    const Geometry& g = h->geom;
-    ExtractBufs b = bufs(h);
-    if (!h->timing) {
-        enqueue_pipeline(h, P, batch, kps, desc, counts, cap, s);
-        h->last = P;
-        h->last_batch = batch;
-        std::fill(h->level_cached.begin(), h->level_cached.end(), false);
-        return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
-    }
-    hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
-    hipMemsetAsync(h->d_status, 0, sizeof(int), s);
-    hipEvent_t* ev = nullptr;
-    if (h->timing) {
-        if ((size_t)(h->ev_used + 1) * 5 > h->ev.size()) {
-            const size_t old = h->ev.size();
-            h->ev.resize(old + 5 * 64);
-            for (size_t i = old; i < h->ev.size(); ++i) hipEventCreate(&h->ev[i]);
-        }
-        ev = &h->ev[(size_t)h->ev_used * 5];
-        h->ev_used++;
     }
     if (ev) hipEventRecord(ev[0], s);
     launch_pyramid(g, b, P, batch, s);
@@ -403,6 +415,12 @@ orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_key
     if (ev) hipEventRecord(ev[3], s);
     launch_describe(g, b, P, kps, desc, cap, batch, s);
     if (ev) hipEventRecord(ev[4], s);
+}
+
+orbx_status run_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoint* kps, uint8_t* desc,
+                         int* counts, int cap, hipStream_t s)
+{
+    enqueue_pipeline(h, P, batch, kps, desc, counts, cap, s, h->timing ? next_stage_events(h) : nullptr);
     h->last = P;
     h->last_batch = batch;
     std::fill(h->level_cached.begin(), h->level_cached.end(), false);
@@ -464,6 +482,8 @@ void orbx_destroy(orbx_handle* h)
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->h_pin) hipHostFree(h->h_pin);
     if (h->h_status) hipHostFree(h->h_status);
+    for (void* p : h->retired_pin) hipHostFree(p);
+    for (void* p : h->retired_dev) (void)hipFree(p);
     dfree(h->d_geom);
     dfree(h->d_cells);
     dfree(h->d_xtab);
@@ -525,7 +545,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     const int pitch = (cols + 63) & ~63;
     const size_t need = (size_t)pitch * rows;
     if (need > h->img_bytes) {
-        if (!dalloc(h->d_img, need)) return ORBX_ENOMEM;
+        if (!dalloc(h, h->d_img, need)) return ORBX_ENOMEM;
         h->img_bytes = need;
     }
     const int ocap = h->geom.out_per_frame;
@@ -533,19 +553,20 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     // frame's count sits in the status block's second word: two D2H copies (status + count, results)
     const size_t kp_b = ((size_t)ocap * sizeof(orbx_keypoint) + 63) & ~(size_t)63;
     if (ocap > h->single_cap) {
-        if (!dalloc(h->d_out, kp_b + (size_t)ocap * 32)) return ORBX_ENOMEM;
+        if (!dalloc(h, h->d_out, kp_b + (size_t)ocap * 32)) return ORBX_ENOMEM;
         h->single_cap = ocap;
     }
     // pinned staging: [image rows x cols][status, count][keypoints ocap][descriptors ocap x 32]
     const size_t img_b = ((size_t)rows * cols + 63) & ~(size_t)63;
     const size_t kp_off = img_b + 64, ds_off = kp_off + kp_b;
     const size_t pin_need = ds_off + (size_t)ocap * 32;
-    if (pin_need > h->pin_bytes) {
-        if (h->h_pin) hipHostFree(h->h_pin);
+    if (pin_need > h->pin_bytes) {   // retired, not freed (see orbx_handle::caps)
+        if (h->h_pin) h->retired_pin.push_back(h->h_pin);
         h->h_pin = nullptr;
+        const size_t want = std::max(pin_need, h->pin_bytes + h->pin_bytes / 2);
         h->pin_bytes = 0;
-        if (hipHostMalloc((void**)&h->h_pin, pin_need, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
-        h->pin_bytes = pin_need;
+        if (hipHostMalloc((void**)&h->h_pin, want, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
+        h->pin_bytes = want;
     }
     for (int r = 0; r < rows; ++r) std::memcpy(h->h_pin + (size_t)r * cols, img + (size_t)r * step, (size_t)cols);
     hipStream_t s = own_stream(h);
@@ -555,9 +576,11 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     orbx_keypoint* d_kps = (orbx_keypoint*)h->d_out;
     uint8_t* d_desc = h->d_out + kp_b;
     // H2D image, the kernels, then one round trip: status, count and the whole output capacity
+    // a timed handle (orbx_set_timing) launches directly, recording the stage events
+    const hipEvent_t* ev = h->timing ? next_stage_events(h) : nullptr;
     auto enqueue = [&]() {
         hipMemcpy2DAsync(h->d_img, pitch, h->h_pin, cols, cols, rows, hipMemcpyHostToDevice, s);
-        enqueue_pipeline(h, P, 1, d_kps, d_desc, d_count, ocap, s);
+        enqueue_pipeline(h, P, 1, d_kps, d_desc, d_count, ocap, s, ev);
         hipMemcpyAsync(phdr, h->d_status, 2 * sizeof(int), hipMemcpyDeviceToHost, s);
         hipMemcpyAsync(h->h_pin + kp_off, h->d_out, kp_b + (size_t)ocap * 32, hipMemcpyDeviceToHost, s);
     };
@@ -568,7 +591,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
                                           h->d_cells, h->d_xtab, h->d_ytab, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
     bool launched = false;
-    if (!h->graph_failed && !getenv("ORBX_NO_GRAPH")) {
+    if (!ev && !h->graph_failed && !getenv("ORBX_NO_GRAPH")) {
         if (h->host_graph && h->graph_key != key) {
             hipGraphExecDestroy(h->host_graph);
             h->host_graph = nullptr;

@@ -39,6 +39,10 @@ namespace {
 // exit-time teardown.  The pool grows to the largest number of concurrent host calls.
 std::mutex g_pool_mu;
 std::vector<HostCtx*>* g_pool = nullptr;
+// Pinned buffers a context outgrew.  hipHostFree waits for the whole device (every stream), so a
+// growing host call would stall the other threads' work; the buffers are kept until the process
+// ends instead (geometric growth: together less than the final buffer).
+std::vector<uint8_t*>* g_retired = nullptr;
 
 HostCtx* acquire(int device)
 {
@@ -105,7 +109,7 @@ size_t HostCall::in(const void* src, size_t bytes)
     // inputs come first so that one copy uploads them all
     if (outs_started_) st_ = ORBX_EINVAL;
     const size_t off = end_;
-    ins_.push_back({off, bytes, src});
+    ins_.push_back({off, bytes, src, -1});
     end_ = round_up(off + bytes);
     in_end_ = end_;
     return off;
@@ -125,7 +129,11 @@ orbx_status HostCall::prepare()
     const size_t total = std::max(end_, kAlign);
     pin_ = std::min(total, kPinnedMax);
     if (ctx_->pinned_size < pin_) {
-        if (ctx_->pinned) hipHostFree(ctx_->pinned);   // rare: the context only grows
+        if (ctx_->pinned) {   // rare: the context only grows; retired, never freed (see g_retired)
+            std::lock_guard<std::mutex> lk(g_pool_mu);
+            if (!g_retired) g_retired = new std::vector<uint8_t*>();
+            g_retired->push_back(ctx_->pinned);
+        }
         ctx_->pinned = nullptr;
         ctx_->pinned_size = 0;
         const size_t s = grow_to(pin_);
@@ -141,12 +149,26 @@ orbx_status HostCall::prepare()
         ctx_->dbuf_size = s;
         queued_ = true;
     }
-    for (const Block& b : ins_)
+    for (Block& b : ins_) {
         if (b.src && b.bytes && b.off + b.bytes <= pin_) std::memcpy(ctx_->pinned + b.off, b.src, b.bytes);
+        if (!b.src && b.bytes && b.off + b.bytes > pin_) {   // filled through host(): its own staging copy
+            b.stage = (int)staged_.size();
+            staged_.emplace_back(b.bytes);
+        }
+    }
     return ORBX_OK;
 }
 
-uint8_t* HostCall::host(size_t off) const { return ctx_ && off < pin_ ? ctx_->pinned + off : nullptr; }
+uint8_t* HostCall::host(size_t off)
+{
+    if (!ctx_ || st_ != ORBX_OK) return nullptr;
+    for (const Block& b : ins_) {
+        if (b.off != off) continue;
+        if (b.off + b.bytes <= pin_) return ctx_->pinned + off;
+        return b.stage >= 0 ? staged_[(size_t)b.stage].data() : nullptr;
+    }
+    return nullptr;
+}
 
 uint8_t* HostCall::dev(size_t off) const { return ctx_ ? ctx_->dbuf + off : nullptr; }
 
@@ -157,10 +179,12 @@ orbx_status HostCall::upload()
     queued_ = true;
     if (head && hipMemcpyAsync(ctx_->dbuf, ctx_->pinned, head, hipMemcpyHostToDevice, ctx_->stream) != hipSuccess)
         return st_ = ORBX_EDEVICE;
-    for (const Block& b : ins_)   // blocks past the pinned window: straight from the caller's memory
-        if (b.src && b.bytes && b.off + b.bytes > pin_ &&
-            hipMemcpyAsync(ctx_->dbuf + b.off, b.src, b.bytes, hipMemcpyHostToDevice, ctx_->stream) != hipSuccess)
+    for (const Block& b : ins_) {   // blocks past the pinned window: straight from the caller's memory
+        const void* from = b.src ? b.src : b.stage >= 0 ? (const void*)staged_[(size_t)b.stage].data() : nullptr;
+        if (from && b.bytes && b.off + b.bytes > pin_ &&
+            hipMemcpyAsync(ctx_->dbuf + b.off, from, b.bytes, hipMemcpyHostToDevice, ctx_->stream) != hipSuccess)
             return st_ = ORBX_EDEVICE;
+    }
     return ORBX_OK;
 }
 

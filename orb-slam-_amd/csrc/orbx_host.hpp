@@ -50,12 +50,15 @@ struct HostCtx;
 //   size_t a = c.in(src, bytes) ...;         // input blocks (copied at prepare())
 //   size_t o = c.out(bytes) ...;             // device-only blocks (outputs, scratch), after the inputs
 //   c.prepare();                             // size the buffers, fill the pinned inputs
-//   c.host(a) ...                            // optional: patch staged inputs (e.g. device pointers)
+//   c.host(a) ...                            // optional: fill or patch an input block (src NULL or not)
 //   c.upload();                              // H2D of the input prefix on the call's stream
 //   launch ...(c.dev(o), c.stream())
 //   c.fetch(o, dst, bytes) ...; c.finish();  // D2H, stream sync, copy out
 // Blocks are 64-byte aligned.  Blocks inside the pinned window go through pinned memory; larger
-// layouts copy their tail blocks directly from / to the caller's memory.
+// layouts copy their tail blocks directly from / to the caller's memory, or, for an input block
+// without a source (filled through host()), from a host-side staging copy of its own.
+// A context's pinned buffer only grows; a replaced one is retired, not freed (hipHostFree waits for
+// the whole device, which would stall every other thread's stream).
 class HostCall {
 public:
     explicit HostCall(int device);
@@ -69,7 +72,7 @@ public:
     size_t in(const void* src, size_t bytes);
     size_t out(size_t bytes);
     orbx_status prepare();
-    uint8_t* host(size_t off) const;   // pinned copy of an input block (prepare() first)
+    uint8_t* host(size_t off);         // staged copy of the input block at off (prepare() first)
     orbx_status upload();
     uint8_t* dev(size_t off) const;
     template <class T>
@@ -81,6 +84,7 @@ private:
     struct Block {
         size_t off, bytes;
         const void* src;
+        int stage;   // index into staged_ for a source-less block past the pinned window, else -1
     };
     struct Fetch {
         size_t off, bytes;
@@ -93,6 +97,7 @@ private:
     bool outs_started_ = false;
     std::vector<Block> ins_;
     std::vector<Fetch> fetches_;
+    std::vector<std::vector<uint8_t>> staged_;
     size_t pin_ = 0;   // pinned window: blocks ending at or below it are staged through pinned memory
     bool queued_ = false;
 };

@@ -190,3 +190,78 @@ def test_hand_back_of_oracle_payloads(world):
         p.join(180)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True
+
+
+# ---- bench.py's exact hand-back sequencing ------------------------------------------------
+_BP_P, _BP_B, _BP_CAP = 3, 2, 5   # pipeline slots, frames per batch, keypoints per frame
+
+
+def _bench_payload(rank, k):
+    """Deterministic payload bytes of rank `rank`'s global step k."""
+    kb = _BP_B * _BP_CAP * 28
+    db = _BP_B * _BP_CAP * 32
+    n = kb + db + _BP_B * 4
+    v = (np.arange(n, dtype=np.int64) * 131 + rank * 7919 + k * 104729) % 251
+    return torch.from_numpy(v.astype(np.uint8))
+
+
+def _bench_pattern_worker(rank, world, port, steps, q):
+    """Drives HandBack exactly as bench.py's step() does: step k runs on slot k % P, takes the slot's
+    next payload (which orders it after that payload's previous send), fills it and sends it.  Rank 0
+    checks every peer's every batch as soon as its receive is known complete (the slot's payload comes
+    round again two slot-steps later, i.e. global step k - 2P), and the rest after drain()."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "orb-slam-_amd"))
+    import orbx_dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        P = _BP_P
+        hands = [orbx_dist.HandBack(_BP_B, _BP_CAP, torch.device("cpu"), world, rank) for _ in range(P)]
+        seen, bad = set(), []
+
+        def check(recv, kstep):
+            for r in range(1, world):
+                if not torch.equal(recv[r - 1], _bench_payload(r, kstep)):
+                    bad.append((r, kstep))
+                seen.add((r, kstep))
+
+        for k in range(steps):
+            j = k % P
+            hb = hands[j]
+            i = hb.k % 2
+            pl = hb.next_payload()
+            if rank == 0 and hb.k >= 2:
+                check(hb.gatherers[i].recv, k - 2 * P)
+            pl.buf.copy_(_bench_payload(rank, k))
+            hb.send()
+        for hb in hands:
+            hb.drain()
+        if rank == 0:
+            for j, hb in enumerate(hands):
+                for s in (hb.k - 2, hb.k - 1):
+                    if s >= 0:
+                        check(hb.gatherers[s % 2].recv, s * P + j)
+            want = {(r, k) for r in range(1, world) for k in range(steps)}
+            q.put((not bad) and seen == want)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,steps", [(2, 13), (4, 20)])
+def test_hand_back_in_bench_sequence(world, steps):
+    """bench.py's multi-GPU pattern on gloo: P = 3 pipeline slots, each its own double-buffered HandBack,
+    sends interleaved across slots over many steps (a step count that is not a multiple of P); rank 0
+    receives every rank's every batch byte for byte, each in its slot's order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_pattern_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=5) is True

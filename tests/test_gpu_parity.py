@@ -366,3 +366,22 @@ def test_allpairs_config5_full_size(orbref, cuda):
     want_rows = (qb * (n - tb) + (1 - qb) * tb).sum(axis=1)
     assert np.array_equal(rows, want_rows)
     assert (wi >= 0).all() and w1[near].max() <= 40
+
+
+def test_stage_times_cover_host_calls(orbref, cuda):
+    """orbx_set_timing then host-path extracts (orbx_extract, which otherwise replays a captured graph):
+    stage_times sums their stage events, and the timed calls still give the oracle's result."""
+    import orbx_synth
+    ex = _extractor(1000)
+    img = orbx_synth.gen_image(12, 640, 480)
+    ex(img)   # the graph path, untimed
+    ex.set_timing(True)
+    ref = orbref.extract(img, orbref.make_params(1000, 1.2, 8, 20, 7), want_pyramid=False)
+    for _ in range(3):
+        kps, desc = ex(img)
+        assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "timed host call")
+    ms = ex.stage_times()
+    assert ms.shape == (4,) and (ms > 0).all() and ms.sum() < 1000, ms
+    ex.set_timing(False)
+    kps, desc = ex(img)   # back on the graph
+    assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "untimed again")

@@ -185,3 +185,50 @@ def test_host_calls_do_not_wait_for_other_streams(orbref, cuda, where):
             if not running or dt > 0.15:
                 slow.append((rnd, k, round(dt, 3), running))
     assert not slow, "host calls waited for the %s kernel: %s" % (where, slow)
+
+
+@pytest.mark.parametrize("where", ["side_stream", "default_stream"])
+def test_growing_host_calls_do_not_wait_for_other_streams(orbref, cuda, where):
+    """Cold variant: every timed call needs a larger pinned staging buffer or device workspace than any call
+    before it (host matcher contexts and extractor handles only grow: an outgrown buffer is retired, not
+    freed, since hipFree / hipHostFree wait for the whole device).  Only the kernels are warmed, on small
+    inputs; each timed call must still return while the sleeping kernel on the other stream runs, and give
+    the oracle's result."""
+    import torch
+    import orbx
+    import orbx_synth
+    from test_gpu_parity import assert_same_keypoints
+    if not hasattr(torch.cuda, "_sleep"):
+        pytest.skip("torch.cuda._sleep unavailable")
+    ex = orbx.ORBextractor(1000, 1.2, 8, 20, 7)
+    ex(orbx_synth.gen_image(3, 320, 240))   # code objects; a small workspace
+    orbx.allpairs_host(orbx_synth.random_descriptors(8, 1), orbx_synth.random_descriptors(8, 2))
+    per_ms = _spin_cycles_per_ms(cuda)
+    p = orbref.make_params(1000, 1.2, 8, 20, 7)
+    sizes = [(400, 300), (640, 480), (752, 480), (1241, 376), (1280, 720), (1920, 1080)]
+    nq = [600, 2000, 6000, 12000, 30000, 60000]
+    slow = []
+    for k, ((w, h), n) in enumerate(zip(sizes, nq)):
+        img = orbx_synth.gen_image(40 + k, w, h)
+        q = orbx_synth.random_descriptors(n, 10 + k)
+        t = orbx_synth.random_descriptors(n // 2, 20 + k)
+        for j, call in enumerate((lambda: ex(img), lambda: orbx.allpairs_host(q, t))):
+            s = torch.cuda.Stream() if where == "side_stream" else torch.cuda.default_stream()
+            done = torch.cuda.Event()
+            with torch.cuda.stream(s):
+                torch.cuda._sleep(int(per_ms * 400))   # ~0.4 s
+                done.record(s)
+            t0 = time.perf_counter()
+            out = call()
+            dt = time.perf_counter() - t0
+            running = not done.query()
+            s.synchronize()
+            if not running:
+                slow.append((k, j, round(dt, 3)))
+            if j == 0:
+                ref = orbref.extract(img, p, want_pyramid=False)
+                assert_same_keypoints(out[0], ref.keypoints, out[1], ref.descriptors, "%dx%d" % (w, h))
+            elif k < 2:
+                wi, w1, w2 = orbref.allpairs_top2(q[:200], t)
+                assert np.array_equal(out[0][:200], wi) and np.array_equal(out[1][:200], w1)
+    assert not slow, "growing host calls waited for the %s kernel: %s" % (where, slow)
