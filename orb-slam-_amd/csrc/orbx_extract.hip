@@ -222,11 +222,13 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
 // (src/ORBextractor.cc:982-987).  Survivors are emitted row-major, i.e. in
 // OpenCV's emission order.
 // ---------------------------------------------------------------------------
-// The ROI tile holds every pixel x as the f16 pair (1024 + x, 1024 + 255 - x).  Integers in
-// [1024, 2048) are exact f16 values with unit spacing (bit pattern 0x6400 + value - 1024), so
-// packed f16 max/min/sub are exact integer ops on both polarities at once, and gfx950's
-// v_pk_maximum3_f16 / v_pk_minimum3_f16 take three operands: a 9-arc max of x is the
-// "brighter" arc value and, in the other half, 255 - the 9-arc min ("darker").
+// The ROI tile holds every pixel x as the f16 h = 1024 + x (bit pattern 0x6400 | x: integers in
+// [1024, 2048) are exact f16 values with unit spacing), 2 bytes per pixel.  Each ring value enters the
+// arithmetic as the packed pair (h, -h): the compiler folds that into the first packed instruction's
+// source modifiers (op_sel_hi = 0, neg_hi), so it costs nothing, and packed f16 max/min/sub are then exact
+// integer ops on both polarities at once.  gfx950's v_pk_maximum3_f16 / v_pk_minimum3_f16 take three
+// operands: a 9-arc max of the pairs is the "brighter" arc value and, in the other half, minus the 9-arc
+// min ("darker").
 typedef _Float16 fh2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ fh2 as_fh2(uint32_t u) { return __builtin_bit_cast(fh2, u); }
@@ -234,39 +236,59 @@ __device__ __forceinline__ fh2 pmax2(fh2 a, fh2 b) { return __builtin_elementwis
 __device__ __forceinline__ fh2 pmin2(fh2 a, fh2 b) { return __builtin_elementwise_minimum(a, b); }
 __device__ __forceinline__ fh2 pmax3(fh2 a, fh2 b, fh2 c) { return pmax2(pmax2(a, b), c); }
 __device__ __forceinline__ fh2 pmin3(fh2 a, fh2 b, fh2 c) { return pmin2(pmin2(a, b), c); }
-
-// packed tile row pitch in dwords (pixels), a multiple of 4 for 16-byte LDS stores
-__host__ __device__ inline int fast_tile_pitch(int max_roi_w) { return (max_roi_w + 3) & ~3; }
-// per-wave LDS: packed ROI tile + zero-bordered strength map of the detection window + the
-// candidate list (u16 pixel indices)
-__host__ __device__ inline size_t fast_wave_bytes(int max_roi_w, int max_roi_h)
+__device__ __forceinline__ fh2 dup_neg(_Float16 h)
 {
-    const size_t tile = (size_t)4 * max_roi_h * fast_tile_pitch(max_roi_w);
-    const size_t map = (((size_t)(max_roi_h - 4) * (max_roi_w - 4)) + 3) & ~(size_t)3;
-    const size_t list = 2 * (size_t)(max_roi_h - 6) * (max_roi_w - 6);
-    return (tile + map + list + 15) & ~(size_t)15;
+    fh2 r;
+    r.x = h;
+    r.y = -h;
+    return r;
 }
 
-// max(v - minMax, maxMin - v) over the 16 cyclic 9-arcs of the Bresenham ring
-__device__ __forceinline__ int fast_strength(const uint32_t* c, int tp)
+// Tile row pitch in dwords (pixels): a compile-time constant per kernel instantiation, so every ring
+// and neighbour access is one base register plus an immediate LDS offset (no per-access address
+// arithmetic).  40 covers the ROIs of every BASELINE configuration (37-38 px); 68 the 66-px cap.
+__host__ __device__ constexpr int fast_tile_pitch(int max_roi_w) { return max_roi_w <= 40 ? 40 : 68; }
+// per-wave LDS: ROI tile [rh][TP] f16 values, zero-bordered strength map [rh - 4][TP] bytes (the
+// detection window plus a one-pixel frame, at the tile's pitch so a map index is a tile index minus a
+// constant), and the candidate list (u16 tile indices) of the largest window, filled from both ends
+__host__ __device__ inline size_t fast_map_bytes(int rw, int rh)
+{
+    return ((size_t)(rh - 4) * fast_tile_pitch(rw) + 3) & ~(size_t)3;
+}
+__host__ __device__ inline int fast_list_cap(int rw, int rh) { return (rh - 6) * (rw - 6); }
+// Output buffer (packed candidates) of the wave's cells, written to HBM once after its last cell: a global
+// store inside the cell loop would make the next cell's wait for its prefetched ROI (vmcnt counts loads
+// and stores, completed in issue order) wait for the store's round trip as well.
+constexpr int kFastObCap = 128;
+__host__ __device__ inline size_t fast_list_bytes(int rw, int rh) { return (2 * (size_t)fast_list_cap(rw, rh) + 3) & ~(size_t)3; }
+__host__ __device__ inline size_t fast_wave_bytes(int rw, int rh)
+{
+    const size_t tile = (size_t)2 * rh * fast_tile_pitch(rw);
+    return (tile + fast_map_bytes(rw, rh) + fast_list_bytes(rw, rh) + 4 * kFastObCap + 15) & ~(size_t)15;
+}
+
+// max(v - minMax, maxMin - v) over the 16 cyclic 9-arcs of the Bresenham ring of the
+// pixel at tile value c[0]
+template <int TP>
+__device__ __forceinline__ int fast_strength(const _Float16* c)
 {
     fh2 x[16];
-    x[0] = as_fh2(c[3 * tp]);
-    x[1] = as_fh2(c[3 * tp + 1]);
-    x[2] = as_fh2(c[2 * tp + 2]);
-    x[3] = as_fh2(c[tp + 3]);
-    x[4] = as_fh2(c[3]);
-    x[5] = as_fh2(c[-tp + 3]);
-    x[6] = as_fh2(c[-2 * tp + 2]);
-    x[7] = as_fh2(c[-3 * tp + 1]);
-    x[8] = as_fh2(c[-3 * tp]);
-    x[9] = as_fh2(c[-3 * tp - 1]);
-    x[10] = as_fh2(c[-2 * tp - 2]);
-    x[11] = as_fh2(c[-tp - 3]);
-    x[12] = as_fh2(c[-3]);
-    x[13] = as_fh2(c[tp - 3]);
-    x[14] = as_fh2(c[2 * tp - 2]);
-    x[15] = as_fh2(c[3 * tp - 1]);
+    x[0] = dup_neg(c[3 * TP]);
+    x[1] = dup_neg(c[3 * TP + 1]);
+    x[2] = dup_neg(c[2 * TP + 2]);
+    x[3] = dup_neg(c[TP + 3]);
+    x[4] = dup_neg(c[3]);
+    x[5] = dup_neg(c[-TP + 3]);
+    x[6] = dup_neg(c[-2 * TP + 2]);
+    x[7] = dup_neg(c[-3 * TP + 1]);
+    x[8] = dup_neg(c[-3 * TP]);
+    x[9] = dup_neg(c[-3 * TP - 1]);
+    x[10] = dup_neg(c[-2 * TP - 2]);
+    x[11] = dup_neg(c[-TP - 3]);
+    x[12] = dup_neg(c[-3]);
+    x[13] = dup_neg(c[TP - 3]);
+    x[14] = dup_neg(c[2 * TP - 2]);
+    x[15] = dup_neg(c[3 * TP - 1]);
     fh2 m3[16], a[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) m3[k] = pmax3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
@@ -274,37 +296,35 @@ __device__ __forceinline__ int fast_strength(const uint32_t* c, int tp)
     for (int k = 0; k < 16; ++k) a[k] = pmax3(m3[k], m3[(k + 3) & 15], m3[(k + 6) & 15]);
     const fh2 b0 = pmin3(a[0], a[1], a[2]), b1 = pmin3(a[3], a[4], a[5]), b2 = pmin3(a[6], a[7], a[8]);
     const fh2 b3 = pmin3(a[9], a[10], a[11]), b4 = pmin3(a[12], a[13], a[14]);
-    const fh2 mm = pmin3(pmin3(b0, b1, b2), pmin2(b3, b4), a[15]);   // (minMax, 255 - maxMin)
-    const fh2 d = as_fh2(c[0]) - mm;                                  // (v - minMax, maxMin - v)
-    const _Float16 sv = d.x > d.y ? d.x : d.y;
-    return (int)sv;
+    const fh2 mm = pmin3(pmin3(b0, b1, b2), pmin2(b3, b4), a[15]);   // (minMax, -maxMin)
+    const fh2 d = dup_neg(c[0]) - mm;                                 // (v - minMax, maxMin - v)
+    return (int)__builtin_fmaxf16(d.x, d.y);
 }
 
-// Necessary condition for s > t: a 9-arc holds two consecutive compass points
-// (ring positions 0, 4, 8, 12), so some consecutive pair is brighter than v+t or
-// some pair is darker than v-t.
-__device__ __forceinline__ bool fast_compass(const uint32_t* c, int tp, int t)
+// Compass value q of the pixel at c[0]: a 9-arc holds two consecutive compass points (ring positions
+// 0, 4, 8, 12), so s > t needs some consecutive pair brighter than v + t or darker than v - t, i.e.
+// q = max(max pair-min - v, v - min pair-max) > t.  An integer-valued f16.
+template <int TP>
+__device__ __forceinline__ _Float16 fast_compass_q(const _Float16* c)
 {
-    const fh2 a = as_fh2(c[3 * tp]), b = as_fh2(c[3]), d = as_fh2(c[-3 * tp]), e = as_fh2(c[-3]);
-    const fh2 m = pmax2(pmax3(pmin2(a, b), pmin2(b, d), pmin2(d, e)), pmin2(e, a));   // (br, 255 - dk)
-    const fh2 q = m - as_fh2(c[0]);                                                  // (br - v, v - dk)
-    const _Float16 tt = (_Float16)t;
-    return q.x > tt || q.y > tt;
+    const fh2 a = dup_neg(c[3 * TP]), b = dup_neg(c[3]), d = dup_neg(c[-3 * TP]), e = dup_neg(c[-3]);
+    const fh2 m = pmax2(pmax3(pmin2(a, b), pmin2(b, d), pmin2(d, e)), pmin2(e, a));   // (br, -dk)
+    const fh2 q = m - dup_neg(c[0]);                                                 // (br - v, v - dk)
+    return __builtin_fmaxf16(q.x, q.y);   // one v_max_f16 (SDWA high-half operand)
 }
 
-__device__ __forceinline__ bool nms_keep(const uint8_t* m, int p, int W2, int t)
+// strict 3x3 non-maximum suppression on the strength map at threshold t (m[0]: the pixel)
+template <int TP>
+__device__ __forceinline__ bool nms_keep(const uint8_t* m, int t)
 {
-    const int s = m[p];
+    const int s = m[0];
     if (s <= t) return false;
     const int sc = s - 1;
-    const int nb[8] = {m[p - W2 - 1], m[p - W2], m[p - W2 + 1], m[p - 1],
-                       m[p + 1],      m[p + W2 - 1], m[p + W2], m[p + W2 + 1]};
+    const int nb[8] = {m[-TP - 1], m[-TP], m[-TP + 1], m[-1], m[1], m[TP - 1], m[TP], m[TP + 1]};
+    bool keep = true;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int mm = nb[k] > t ? nb[k] - 1 : 0;
-        if (!(sc > mm)) return false;
-    }
-    return true;
+    for (int k = 0; k < 8; ++k) keep &= sc > (nb[k] > t ? nb[k] - 1 : 0);
+    return keep;
 }
 
 // ROI bytes of one cell staged in registers: up to kFastLd aligned dword pairs per lane
@@ -314,11 +334,9 @@ constexpr int kFastLd = 6;
 #define ORBX_FAST_CPW 3
 #endif
 constexpr int kCellsPerWave = ORBX_FAST_CPW;   // cells per wave: the next cell's ROI loads fly under this one's passes
-constexpr int kFastWaves = 1;                  // waves per workgroup: LDS is allocated per wave, not in 4-wave steps
 
 struct FastPrefetch {
-    uint32_t lo[kFastLd], hi[kFastLd], sh[kFastLd];
-    int dst[kFastLd];
+    uint32_t lo[kFastLd], hi[kFastLd];   // placement (row, dword) is recomputed at the commit
 };
 
 struct FastCellSrc {
@@ -327,44 +345,51 @@ struct FastCellSrc {
     float inv_nd;
 };
 
-__device__ __forceinline__ void fast_issue(const FastCellSrc& S, int i0, int lane, int tp, FastPrefetch& F)
+// ROI dword k of row r for flat index i (lane-major passes), at byte offset o from the aligned origin
+__device__ __forceinline__ bool fast_slot(const FastCellSrc& S, int i, int& r, int& k, uint32_t& o)
+{
+    if (i >= S.ntot) return false;
+    r = (int)(((float)i + 0.5f) * S.inv_nd);
+    k = i - __mul24(r, S.nd);
+    o = (uint32_t)((uintptr_t)S.src & 3) + (uint32_t)__mul24(r, S.pitch) + 4u * (uint32_t)k;
+    return true;
+}
+
+__device__ __forceinline__ void fast_issue(const FastCellSrc& S, int i0, int lane, FastPrefetch& F)
 {
     // 32-bit byte offsets from the wave-uniform aligned ROI origin: scalar base + vector offset
     // addressing, no 64-bit address arithmetic per load
     const __attribute__((address_space(1))) uint8_t* base =
         (const __attribute__((address_space(1))) uint8_t*)((uintptr_t)S.src & ~(uintptr_t)3);
-    const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
 #pragma unroll
     for (int u = 0; u < kFastLd; ++u) {
-        const int i = i0 + u * 64 + lane;
-        F.dst[u] = -1;
-        if (i < S.ntot) {
-            const int r = (int)(((float)i + 0.5f) * S.inv_nd), k = i - __mul24(r, S.nd);
-            const uint32_t o = s0 + (uint32_t)__mul24(r, S.pitch) + 4u * (uint32_t)k;
+        int r, k;
+        uint32_t o;
+        if (fast_slot(S, i0 + u * 64 + lane, r, k, o)) {
             const __attribute__((address_space(1))) uint32_t* ap =
                 (const __attribute__((address_space(1))) uint32_t*)(base + (o & ~3u));
             F.lo[u] = ap[0];
             F.hi[u] = ap[1];
-            F.sh[u] = o & 3u;
-            F.dst[u] = __mul24(r, tp) + 4 * k;
         }
     }
 }
 
-__device__ __forceinline__ void fast_commit(const FastPrefetch& F, uint32_t* tile)
+// 4 pixels of ROI row r from column 4k as f16 (0x6400 | x): two v_perm (bytes 0, 1 and 2, 3 of the
+// realigned dword into the low bytes of two halves) and two ors, one 8-byte LDS store
+template <int TP>
+__device__ __forceinline__ void fast_commit(const FastPrefetch& F, const FastCellSrc& S, int i0, int lane,
+                                            _Float16* tile)
 {
 #pragma unroll
     for (int u = 0; u < kFastLd; ++u) {
-        if (F.dst[u] < 0) continue;
-        const uint32_t w = __builtin_amdgcn_alignbyte(F.hi[u], F.lo[u], F.sh[u]);
-        // fast_pack(x) = (0x6400 | x, 0x64FF - x) = 0x64FF6400 ^ (x | x << 16) for a byte x:
-        // one v_perm (byte k of w into bytes 0 and 2, zeros elsewhere) and one xor per pixel
-        uint4 q;
-        q.x = __builtin_amdgcn_perm(0u, w, 0x0C000C00u) ^ 0x64FF6400u;
-        q.y = __builtin_amdgcn_perm(0u, w, 0x0C010C01u) ^ 0x64FF6400u;
-        q.z = __builtin_amdgcn_perm(0u, w, 0x0C020C02u) ^ 0x64FF6400u;
-        q.w = __builtin_amdgcn_perm(0u, w, 0x0C030C03u) ^ 0x64FF6400u;
-        *(uint4*)(tile + F.dst[u]) = q;
+        int r, k;
+        uint32_t o;
+        if (!fast_slot(S, i0 + u * 64 + lane, r, k, o)) continue;
+        const uint32_t w = __builtin_amdgcn_alignbyte(F.hi[u], F.lo[u], o & 3u);
+        uint2 q;
+        q.x = __builtin_amdgcn_perm(0u, w, 0x0C010C00u) | 0x64006400u;
+        q.y = __builtin_amdgcn_perm(0u, w, 0x0C030C02u) | 0x64006400u;
+        *(uint2*)(tile + r * TP + 4 * k) = q;
     }
 }
 
@@ -381,28 +406,62 @@ __device__ unsigned long long g_fast_prof[8];
 #define FP_STAMP(k) ((void)0)
 #endif
 
+__device__ __forceinline__ unsigned long long ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// K2: one wave per workgroup (LDS is granted per wave), cpw consecutive cells per wave.  Per cell
+// (src/ORBextractor.cc:952-1000, cv::FAST on the cell ROI with nonmax suppression, retried at
+// minThFAST when iniThFAST keeps nothing):
+//   pass 1   compass value q of every window pixel; q > iniThFAST lists the pixel at the list's front,
+//            minThFAST < q <= iniThFAST at its back (q <= t implies strength <= t)
+//   pass 2a  exact strength of the front entries into the map (kept if above the lower threshold)
+//   NMS      at iniThFAST over the front entries
+//   pass 2b  only when it kept nothing: strengths of the back entries, then NMS at minThFAST over both
+//   output   kept pixels marked in a per-row bitmask, emitted in row-major order (cv::FAST's order)
+// On the synthetic KITTI sequence about 45% of cells fall back, and the front holds about 2% of the
+// pixels against 26% for both ends, so the fallback-free cells skip most strength evaluations.
 #ifndef ORBX_FAST_WPE
 #define ORBX_FAST_WPE 1
 #endif
-__global__ __launch_bounds__(256, ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
-                                                    const Cell* __restrict__ cells,
-                                                    uint32_t* __restrict__ slots,
-                                                    int* __restrict__ cell_counts,
-                                                    int cb, int ce, int rw, int rh, int cpw)
+template <int TP>
+__global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
+                                                   const Cell* __restrict__ cells, uint32_t* __restrict__ slots,
+                                                   int* __restrict__ cell_counts, int cb, int ce, int rw, int rh,
+                                                   int cpw)
 {
-    // cells [cb, ce); per-wave LDS sized from the group's largest cell ROI (rw x rh)
+    // cells [cb, ce); LDS sized from the group's largest cell ROI (rw x rh)
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
-    const int kTileP = fast_tile_pitch(rw);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
+    const int lane = threadIdx.x;
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
-    const int c0 = cb + ((lb - f * gridDim.x) * kFastWaves + wave) * cpw;
+    const int c0 = cb + (lb - f * gridDim.x) * cpw;
     const int c1 = min(c0 + cpw, ce);
     if (c0 >= c1) return;   // wave-uniform; no block barriers below
-    uint32_t* tile = (uint32_t*)(s_fast + (size_t)wave * fast_wave_bytes(rw, rh));
-    uint8_t* map = (uint8_t*)(tile + (size_t)rh * kTileP);
-    uint16_t* list = (uint16_t*)(map + ((((size_t)(rh - 4) * (rw - 4)) + 3) & ~(size_t)3));
-    const int tq = min(G->ini_th, G->min_th);
+    _Float16* tile = (_Float16*)s_fast;
+    uint8_t* map = (uint8_t*)(tile + (size_t)rh * TP);
+    uint16_t* list = (uint16_t*)(map + fast_map_bytes(rw, rh));
+    uint32_t* obuf = (uint32_t*)((uint8_t*)list + fast_list_bytes(rw, rh));
+    const int lcap = fast_list_cap(rw, rh);
+    uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
+    // lane i: the wave's cell c0 + i -- its candidate count, and for a buffered cell its obuf offset and
+    // slot base; cells [fb0, current) are in obuf
+    int cnt_all = 0, c_off = 0, c_cnt = 0, c_slot = 0;
+    int obn = 0, fb0 = 0;
+    auto flush = [&](int fb1) {
+        for (int i = fb0; i < fb1; ++i) {
+            const int n = __builtin_amdgcn_readlane(c_cnt, i);
+            const int o = __builtin_amdgcn_readlane(c_off, i);
+            uint32_t* out = fslots + __builtin_amdgcn_readlane(c_slot, i);
+            for (int e = lane; e < n; e += 64) out[e] = obuf[o + e];
+        }
+        obn = 0;
+        fb0 = fb1;
+    };
+    // kept-pixel bitmask, one u64 per window row: aliases the tile, which is dead once every strength
+    // of the cell is known
+    unsigned long long* kept = (unsigned long long*)tile;
+    const int t_ini = G->ini_th, t_min = G->min_th;
+    const int t_lo = min(t_ini, t_min);
+    const _Float16 f_hi = (_Float16)t_ini, f_lo = (_Float16)t_lo;
 #ifdef ORBX_FAST_PROF
     long long fp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long fp_t = clock64();
@@ -422,141 +481,216 @@ __global__ __launch_bounds__(256, ORBX_FAST_WPE) void k_fast_cells(const Geometr
         S.inv_nd = 1.0f / (float)S.nd;   // exact row split for ntot < 4096
         return S;
     };
-    Cell C = cells[c0];
+    // the cell descriptor as whole dwords: scalar loads (a 16-bit field read is a vector load, whose
+    // vmcnt wait would also drain every store still in flight)
+    auto load_cell = [&](int ci) {
+        const uint32_t* w = (const uint32_t*)(cells + ci);
+        const uint32_t w0 = w[0], w1 = w[1];
+        Cell r;
+        r.level = (int16_t)(w0 & 0xFFFF);
+        r.roi_w = (int16_t)(w0 >> 16);
+        r.roi_h = (int16_t)(w1 & 0xFFFF);
+        r.pad = 0;
+        r.roi_x0 = (int32_t)w[2];
+        r.roi_y0 = (int32_t)w[3];
+        r.slot_base = (int32_t)w[4];
+        r.slot_cap = (int32_t)w[5];
+        return r;
+    };
+    Cell C = load_cell(c0);
     FastCellSrc S = cell_src(C);
     FastPrefetch F;
-    fast_issue(S, 0, lane, kTileP, F);
+    fast_issue(S, 0, lane, F);
 
 #pragma unroll 1
     for (int c = c0; c < c1; ++c) {
-        const int rw = C.roi_w, rh = C.roi_h;
-        const int dw = rw - 6, dh = rh - 6;
+        const int dw = C.roi_w - 6, dh = C.roi_h - 6;
         const Cell Cc = C;
         FP_STAMP(7);
-        fast_commit(F, tile);
+        fast_commit<TP>(F, S, 0, lane, tile);
         for (int i0 = 64 * kFastLd; i0 < S.ntot; i0 += 64 * kFastLd) {   // ROIs beyond 6 passes
             FastPrefetch R;
-            fast_issue(S, i0, lane, kTileP, R);
-            fast_commit(R, tile);
+            fast_issue(S, i0, lane, R);
+            fast_commit<TP>(R, S, i0, lane, tile);
         }
-        const int W2 = dw + 2;
-        const int mapn = W2 * (dh + 2);
+        const int mapn = (dh + 2) * TP;
         FP_STAMP(0);
         for (int i = lane; i < (mapn + 3) >> 2; i += 64) ((uint32_t*)map)[i] = 0u;
         wave_lds_sync();
         FP_STAMP(1);
         if (c + 1 < c1) {   // prefetch the next cell (registers only; lands under the passes below)
-            C = cells[c + 1];
+            C = load_cell(c + 1);
             S = cell_src(C);
-            fast_issue(S, 0, lane, kTileP, F);
+            fast_issue(S, 0, lane, F);
         }
-        int* out_count = cell_counts + (size_t)f * G->ncells + c;
         if (dw <= 0 || dh <= 0) {
-            if (lane == 0) *out_count = 0;
             wave_lds_sync();
             continue;
         }
 
-        // Pass 1: compass filter at the lower of the two thresholds; survivors listed in
-        // row-major order as (row << 8 | col).  A pass covers 64 / cw rows of cw = 32 or 64
-        // columns, so lanes map to pixels without divisions and ballot order is row-major.
-        // Pass 2: exact strength of the listed pixels into the map; the list keeps those
-        // above the lower threshold (in place: a round writes at or before the entries it
-        // has read).  Only listed pixels can pass either NMS test.
+        // ---- pass 1: a pass covers 64 / cw rows of cw = 32 or 64 columns (row-major lanes); two row
+        // steps per trip.  Lanes outside the window read in-bounds LDS (the tile's slack rows, the map)
+        // and are masked out.  Pixels are named by their window index m = i * TP + j: the pixel's tile
+        // value is tile[m + 3 * TP + 3] and its map byte map[m + TP + 1], so every ring, compass and
+        // neighbour access is (tile or map) + m plus a non-negative immediate offset.
         const int cw_shift = dw <= 32 ? 5 : 6;
         const int col = lane & ((1 << cw_shift) - 1);
         const int rstep = 64 >> cw_shift;
-        int row = lane >> cw_shift;
-        // every lane tests a pixel, branch-free: reads are clamped into the detection window and the
-        // window mask is and-ed into the ballot
-        const int ccol = min(col, dw - 1) + 3;
-        int n1 = 0;
-        for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {   // two row steps per trip: more LDS reads in flight
-            const uint32_t* tpa = tile + __mul24(min(row, dh - 1) + 3, kTileP) + ccol;
-            const uint32_t* tpb = tile + __mul24(min(row + rstep, dh - 1) + 3, kTileP) + ccol;
-            const bool ina = (col < dw) & (row < dh) & fast_compass(tpa, kTileP, tq);
-            const bool inb = (col < dw) & (row + rstep < dh) & fast_compass(tpb, kTileP, tq);
-            const unsigned long long ma = __ballot(ina), mb = __ballot(inb);
-            if (ina) list[n1 + lanes_below(ma)] = (uint16_t)((row << 8) | col);
-            n1 += __popcll(ma);
-            if (inb) list[n1 + lanes_below(mb)] = (uint16_t)(((row + rstep) << 8) | col);
-            n1 += __popcll(mb);
-            row += 2 * rstep;
+        const int rlane = lane >> cw_shift;
+        const bool col_ok = col < dw;
+        const unsigned long long colmask = ballot64(col_ok);
+        int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
+        int nf = 0, nb = 0;   // front / back entries
+        for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {
+            const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
+            const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
+            const bool oka = col_ok & (rlane < dh - r0), okb = col_ok & (rlane < dh - r0 - rstep);
+            const bool fa = oka & (qa > f_hi), ba = oka & (qa > f_lo) & !(qa > f_hi);
+            const bool fb = okb & (qb > f_hi), bb = okb & (qb > f_lo) & !(qb > f_hi);
+            // masks from the compares themselves, combined in scalar code (a ballot of an and-chain
+            // would materialise the bool in a VGPR first)
+            const unsigned long long va = colmask & ballot64(rlane < dh - r0);
+            const unsigned long long vb = colmask & ballot64(rlane < dh - r0 - rstep);
+            const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
+            const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
+            const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
+            if (fa) list[nf + lanes_below(mfa)] = (uint16_t)t;
+            nf += __popcll(mfa);
+            if (fb) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
+            nf += __popcll(mfb);
+            if (ba) list[lcap - 1 - nb - lanes_below(mba)] = (uint16_t)t;
+            nb += __popcll(mba);
+            if (bb) list[lcap - 1 - nb - lanes_below(mbb)] = (uint16_t)(t + rstep * TP);
+            nb += __popcll(mbb);
+            t += 2 * rstep * TP;
         }
         wave_lds_sync();
         FP_STAMP(2);
-        int n2 = 0;
-        for (int j0 = 0; j0 < n1; j0 += 128) {   // two list entries per lane per trip
-            const int ja = j0 + lane, jb = ja + 64;
-            // branch-free: lanes past the list re-test its last entry, masked out below
-            const int ka = list[min(ja, n1 - 1)], kb = list[min(jb, n1 - 1)];
-            const int sa = fast_strength(tile + __mul24((ka >> 8) + 3, kTileP) + ((ka & 0xFF) + 3), kTileP);
-            const int sb = fast_strength(tile + __mul24((kb >> 8) + 3, kTileP) + ((kb & 0xFF) + 3), kTileP);
-            const bool ina = (ja < n1) & (sa > tq), inb = (jb < n1) & (sb > tq);
-            if (ina) map[__mul24((ka >> 8) + 1, W2) + (ka & 0xFF) + 1] = (uint8_t)sa;
-            if (inb) map[__mul24((kb >> 8) + 1, W2) + (kb & 0xFF) + 1] = (uint8_t)sb;
-            const unsigned long long ma = __ballot(ina), mb = __ballot(inb);
-            wave_lds_sync();   // both entries are read before the compaction overwrites the list
-            if (ina) list[n2 + lanes_below(ma)] = (uint16_t)ka;
-            n2 += __popcll(ma);
-            if (inb) list[n2 + lanes_below(mb)] = (uint16_t)kb;
-            n2 += __popcll(mb);
-        }
-        wave_lds_sync();
 
-        FP_STAMP(3);
-        // NMS at iniThFAST over the list; survivors remembered per round (rounds <= 57)
-        const int rounds = (n2 + 63) >> 6;
-        unsigned long long keepmask = 0;
-        int t = G->ini_th;
-        int kept = 0;
-        for (int r = 0; r < rounds; ++r) {
-            const int j = lane + (r << 6);
-            bool keep = false;
-            if (j < n2) {
-                const int k = list[j];
-                keep = nms_keep(map, __mul24((k >> 8) + 1, W2) + (k & 0xFF) + 1, W2, t);
+        // ---- pass 2: exact strengths of list entries [j0, j1) (front: ascending positions, back:
+        // descending from lcap - 1) into the map; the entries above the lower threshold are compacted in
+        // place (a trip writes at or before what it has read).  Returns the compacted count.
+        auto strengths = [&](int n, bool back) {
+            int n2 = 0;
+            for (int j0 = 0; j0 < n; j0 += 128) {   // two entries per lane per trip
+                const int ja = j0 + lane, jb = ja + 64;
+                // lanes past the list re-test its last entry, masked out below
+                const int pa = back ? lcap - 1 - min(ja, n - 1) : min(ja, n - 1);
+                const int pb = back ? lcap - 1 - min(jb, n - 1) : min(jb, n - 1);
+                const int ka = list[pa], kb = list[pb];
+                const int sa = fast_strength<TP>(tile + ka + (3 * TP + 3));
+                const int sb = fast_strength<TP>(tile + kb + (3 * TP + 3));
+                // masks before any branch (an i1 live across a divergent branch is materialised in a VGPR)
+                const unsigned long long ma = ballot64(ja < n) & ballot64(sa > t_lo);
+                const unsigned long long mb = ballot64(jb < n) & ballot64(sb > t_lo);
+                const bool ina = (ja < n) & (sa > t_lo), inb = (jb < n) & (sb > t_lo);
+                if (ina) map[ka + (TP + 1)] = (uint8_t)sa;
+                if (inb) map[kb + (TP + 1)] = (uint8_t)sb;
+                wave_lds_sync();   // both entries are read before the compaction overwrites the list
+                if (ina) list[back ? lcap - 1 - (n2 + lanes_below(ma)) : n2 + lanes_below(ma)] = (uint16_t)ka;
+                n2 += __popcll(ma);
+                if (inb) list[back ? lcap - 1 - (n2 + lanes_below(mb)) : n2 + lanes_below(mb)] = (uint16_t)kb;
+                n2 += __popcll(mb);
             }
-            keepmask |= (unsigned long long)keep << r;
-            kept += __popcll(__ballot(keep));
-        }
-        if (kept == 0) {   // src/ORBextractor.cc:982-987: retry the cell at minThFAST
-            t = G->min_th;
-            keepmask = 0;
+            wave_lds_sync();
+            return n2;
+        };
+        const int nf2 = strengths(nf, false);
+        FP_STAMP(3);
+
+        // ---- NMS: rounds of 64 entries over the front [0, nf2) then the back; survivors remembered
+        // per round (at most 2 * 57 rounds for the 66 x 66 cap: two masks)
+        auto nms = [&](int nfr, int nbk, int th, unsigned long long (&keepm)[2]) {
+            const int rounds = (nfr + nbk + 63) >> 6;
+            int kept_n = 0;
+            keepm[0] = keepm[1] = 0;
             for (int r = 0; r < rounds; ++r) {
                 const int j = lane + (r << 6);
                 bool keep = false;
-                if (j < n2) {
-                    const int k = list[j];
-                    keep = nms_keep(map, __mul24((k >> 8) + 1, W2) + (k & 0xFF) + 1, W2, t);
+                if (j < nfr + nbk) {
+                    const int k = list[j < nfr ? j : lcap - 1 - (j - nfr)];
+                    keep = nms_keep<TP>(map + k + (TP + 1), th);
                 }
-                keepmask |= (unsigned long long)keep << r;
+                keepm[r >> 6] |= (unsigned long long)keep << (r & 63);
+                kept_n += __popcll(ballot64(keep));
             }
+            return kept_n;
+        };
+        unsigned long long keepm[2];
+        int nbk = 0;
+        int kept_n = nms(nf2, 0, t_ini, keepm);
+        if (kept_n == 0) {   // src/ORBextractor.cc:982-987: retry the cell at minThFAST
+            if (t_min < t_ini) nbk = strengths(nb, true);
+            kept_n = nms(nf2, nbk, t_min, keepm);
         }
-
         FP_STAMP(4);
-        uint32_t* out = slots + (size_t)f * G->slots_per_frame + Cc.slot_base;
-        const int xr0 = Cc.roi_x0 + 3 - kMinBorder, yr0 = Cc.roi_y0 + 3 - kMinBorder;
-        int base = 0;
-        for (int r = 0; r < rounds; ++r) {
-            const bool keep = (keepmask >> r) & 1ull;
-            const unsigned long long m = __ballot(keep);
-            if (keep) {
-                const int k = list[lane + (r << 6)];
-                const int ii = k >> 8, jj = k & 0xFF;
-                const int idx = base + lanes_below(m);
-                out[idx] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + ii),
-                                   (uint32_t)(map[__mul24(ii + 1, W2) + jj + 1] - 1));
+
+        // ---- output: kept pixels into the per-row bitmask (the tile is dead now), then row-major into
+        // the wave's output buffer (or, for a cell with more than the buffer holds, straight to HBM)
+        if (kept_n > 0) {
+            for (int i = lane; i < dh; i += 64) kept[i] = 0ull;
+            wave_lds_sync();
+            const int rounds = (nf2 + nbk + 63) >> 6;
+            for (int r = 0; r < rounds; ++r) {
+                if (!((keepm[r >> 6] >> (r & 63)) & 1ull)) continue;
+                const int j = lane + (r << 6);
+                const int m = list[j < nf2 ? j : lcap - 1 - (j - nf2)];   // window (i, j) at m = i * TP + j
+                const int wi = m / TP;
+                atomicOr(&kept[wi], 1ull << (m - wi * TP));
             }
-            base += __popcll(m);
+            wave_lds_sync();
+            // lane i emits window row i (rows <= 60): prefix sum of the row counts gives its first slot
+            const unsigned long long rowbits = lane < dh ? kept[lane] : 0ull;
+            const int cnt = __popcll(rowbits);
+            int base = 0;
+            {
+                int v = cnt;
+                // inclusive wave scan of the counts
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int u = __shfl_up(v, o);
+                    if (lane >= o) v += u;
+                }
+                base = v - cnt;
+            }
+            const int xr0 = Cc.roi_x0 + 3 - kMinBorder, yr0 = Cc.roi_y0 + 3 - kMinBorder;
+            unsigned long long bits = rowbits;
+            int idx = base;
+            const int ci = c - c0;
+            if (kept_n <= kFastObCap) {
+                if (obn + kept_n > kFastObCap) flush(ci);   // rare: the buffered cells go out first
+                if (lane == ci) {
+                    c_off = obn;
+                    c_cnt = kept_n;
+                    c_slot = Cc.slot_base;
+                }
+                uint32_t* dst = obuf + obn;
+                while (bits) {
+                    const int jj = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const int sc = map[(lane + 1) * TP + jj + 1];
+                    dst[idx++] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + lane), (uint32_t)(sc - 1));
+                }
+                obn += kept_n;
+            } else {
+                uint32_t* dst = fslots + Cc.slot_base;
+                while (bits) {
+                    const int jj = __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const int sc = map[(lane + 1) * TP + jj + 1];
+                    dst[idx++] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + lane), (uint32_t)(sc - 1));
+                }
+            }
         }
-        if (lane == 0) *out_count = base;
+        if (lane == c - c0) cnt_all = kept_n;
         wave_lds_sync();   // tile, map and list are rewritten by the next cell
         FP_STAMP(5);
 #ifdef ORBX_FAST_PROF
         fp_acc[6] += 1;
 #endif
     }
+    flush(c1 - c0);
+    if (lane < c1 - c0) cell_counts[(size_t)f * G->ncells + c0 + lane] = cnt_all;
 #ifdef ORBX_FAST_PROF
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_fast_prof[k], (unsigned long long)fp_acc[k]);
@@ -578,7 +712,7 @@ namespace orbx {
 
 // LDS per CU on gfx950: the occupancy a FAST launch's per-wave tiles allow
 constexpr size_t kLdsPerCu = 160 * 1024;
-static int fast_blocks_per_cu(int w, int h) { return (int)(kLdsPerCu / (kFastWaves * fast_wave_bytes(w, h))); }
+static int fast_blocks_per_cu(int w, int h) { return (int)(kLdsPerCu / fast_wave_bytes(w, h)); }
 
 void fast_groups(Geometry& g)
 {
@@ -616,19 +750,28 @@ void fast_groups(Geometry& g)
     g.fast_rh[1] = h1;
 }
 
+template <int TP>
+static void fast_launch(const ExtractBufs& b, const FramePtrs& p, int cb, int ce, int rw, int rh, int cpw,
+                        int batch, hipStream_t s)
+{
+    dim3 grid((ce - cb + cpw - 1) / cpw, batch);
+    const size_t smem = fast_wave_bytes(rw, rh);
+    hipFuncSetAttribute((const void*)k_fast_cells<TP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL(k_fast_cells<TP>, grid, dim3(64), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts, cb, ce,
+                       rw, rh, cpw);
+}
+
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
     // small batches (the per-frame host path) are latency-bound: one cell per wave, 3x the waves
     const int cpw = batch <= kLatencyMaxBatch ? 1 : kCellsPerWave;
-    const int per_block = kFastWaves * cpw;
     for (int i = 0; i < g.fast_groups; ++i) {
         const int cb = g.fast_cb[i], ce = g.fast_cb[i + 1];
         if (ce <= cb) continue;
-        dim3 grid((ce - cb + per_block - 1) / per_block, batch);
-        const size_t smem = kFastWaves * fast_wave_bytes(g.fast_rw[i], g.fast_rh[i]);
-        hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        hipLaunchKernelGGL(k_fast_cells, grid, dim3(64 * kFastWaves), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
-                           cb, ce, g.fast_rw[i], g.fast_rh[i], cpw);
+        if (fast_tile_pitch(g.fast_rw[i]) == 40)
+            fast_launch<40>(b, p, cb, ce, g.fast_rw[i], g.fast_rh[i], cpw, batch, s);
+        else
+            fast_launch<68>(b, p, cb, ce, g.fast_rw[i], g.fast_rh[i], cpw, batch, s);
     }
 }
 
@@ -1537,6 +1680,9 @@ __device__ __forceinline__ uint32_t blur_acc(const uint32_t* rowT, uint32_t by, 
 #ifndef ORBX_DESC_WPE
 #define ORBX_DESC_WPE 1
 #endif
+#ifndef ORBX_DESC_DEFER
+#define ORBX_DESC_DEFER 0
+#endif
 __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
                                                const uint32_t* __restrict__ qt_out,
                                                const int* __restrict__ qt_cnt,
@@ -1545,6 +1691,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_raw[kDescWaves][kRawSlots];
     __shared__ __attribute__((aligned(16))) uint32_t s_rowT[kDescWaves][kTCols * kTP];
+    __shared__ uint32_t s_out[kDescWaves][15 * kDescPerWave];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x, bx = lb - f * gridDim.x;
@@ -1646,6 +1793,12 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     uint32_t npk = 0;
     bool nvalid = lookup(g0, nl, npk);
     if (nvalid) fill(nl, npk, sb, sp);
+    // The wave's outputs stay in LDS until its last keypoint (s_out: 8 descriptor dwords per keypoint, then
+    // 7 cv::KeyPoint dwords per keypoint).  A global store inside the loop would make the next keypoint's
+    // wait for its patch DMA (vmcnt counts loads and stores, completed in issue order) wait for the store's
+    // round trip as well.
+    uint32_t* sout = s_out[wave];
+    int nout = 0;
 #pragma unroll 1
     for (int jj = 0; jj < kpw && nvalid; ++jj) {
         const int oidx = g0 + jj, l = nl;
@@ -1722,25 +1875,51 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             }
             words[wd] = __ballot(t2[0] < (t2[1] < 255u ? t2[1] : 255u));
         }
-        const size_t o = (size_t)f * cap + oidx;
-        if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
-        if (lane == 0) {
+#if ORBX_DESC_DEFER == 0
+        {   // A/B knob: per-keypoint stores (round 2)
+            const size_t o = (size_t)f * cap + oidx;
+            if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
+            if (lane == 0) {
+                float x = (float)cx, y = (float)cy;
+                if (l != 0) {
+                    x *= LG.scale;
+                    y *= LG.scale;
+                }
+                orbx_keypoint k;
+                k.x = x;
+                k.y = y;
+                k.size = LG.patch_size;
+                k.angle = angle;
+                k.response = (float)score;
+                k.octave = l;
+                k.class_id = -1;
+                kps[o] = k;
+            }
+        }
+#else
+        if (lane < 8) {
+            const unsigned long long v = lane < 2 ? words[0] : lane < 4 ? words[1] : lane < 6 ? words[2] : words[3];
+            sout[8 * jj + lane] = (lane & 1) ? (uint32_t)(v >> 32) : (uint32_t)v;
+        } else if (lane < 15) {
             float x = (float)cx, y = (float)cy;
             if (l != 0) {
                 x *= LG.scale;
                 y *= LG.scale;
             }
-            orbx_keypoint k;
-            k.x = x;
-            k.y = y;
-            k.size = LG.patch_size;
-            k.angle = angle;
-            k.response = (float)score;
-            k.octave = l;
-            k.class_id = -1;
-            kps[o] = k;
+            const int k = lane - 8;   // cv::KeyPoint fields: x y size angle response octave class_id
+            sout[8 * kDescPerWave + 7 * jj + k] =
+                k == 0 ? __float_as_uint(x) : k == 1 ? __float_as_uint(y) : k == 2 ? __float_as_uint(LG.patch_size)
+                : k == 3 ? __float_as_uint(angle) : k == 4 ? __float_as_uint((float)score) : k == 5 ? (uint32_t)l
+                : 0xFFFFFFFFu;
         }
+#endif
+        nout = jj + 1;
         wave_lds_sync();   // rowT is rewritten by the next keypoint
+    }
+    if (ORBX_DESC_DEFER && nout > 0) {   // the wave's keypoints are consecutive outputs: one contiguous run of each array
+        const size_t o = (size_t)f * cap + g0;
+        if (lane < 8 * nout) reinterpret_cast<uint32_t*>(desc + o * 32)[lane] = sout[lane];
+        if (lane < 7 * nout) reinterpret_cast<uint32_t*>(kps + o)[lane] = sout[8 * kDescPerWave + lane];
     }
 }
 

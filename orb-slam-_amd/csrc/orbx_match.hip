@@ -425,15 +425,42 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
     const uint8_t* d1 = desc + (size_t)fa * cap * 32;
     const float2* pv = prev ? prev + (size_t)pair * cap : nullptr;
     const int nwaves = gridDim.y * (SI_BUILD_NT / 64);
+    // A wave handles about 18 queries.  The next query's descriptor and window centre are loaded before
+    // the current one's scan, and the results (top-4, count) collect in lane q of five registers and go to
+    // HBM after the wave's last query: a store per query would make every later load wait for its round
+    // trip (vmcnt counts loads and stores, completed in issue order).
     auto scan_queries = [&](auto staged_tag) {
         constexpr bool kStaged = decltype(staged_tag)::value;
         const uint32_t* K = kStaged ? (const uint32_t*)skeys : keys;
         const float2* XY = kStaged ? (const float2*)sxy : xy;
-        for (int i1 = blockIdx.y * (SI_BUILD_NT / 64) + wave; i1 < n10; i1 += nwaves) {
-            const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)i1 * 32);
-            const ulonglong2 a0 = a[0], a1 = a[1];
-            // window centre vbPrevMatched[i1] (src/ORBmatcher.cc:456-460); F1's own keypoint when not given
-            const float2 c = pv ? pv[i1] : make_float2(k1[i1].x, k1[i1].y);
+        const int q0 = blockIdx.y * (SI_BUILD_NT / 64) + wave;
+        ulonglong2 na0 = make_ulonglong2(0, 0), na1 = make_ulonglong2(0, 0);
+        float2 nc = make_float2(0.f, 0.f);
+        auto load_query = [&](int q) {
+            if (q < n10) {
+                const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)q * 32);
+                na0 = a[0];
+                na1 = a[1];
+                // window centre vbPrevMatched[q] (src/ORBmatcher.cc:456-460); F1's own keypoint when not given
+                nc = pv ? pv[q] : make_float2(k1[q].x, k1[q].y);
+            }
+        };
+        uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, rc = 0;   // lane j: the wave's query q0 + (qb + j) * nwaves
+        int nq = 0, qb = 0;
+        auto flush = [&]() {
+            if (lane < nq) {
+                const size_t at = (size_t)pair * cap + q0 + (size_t)(qb + lane) * nwaves;
+                qtop[at] = make_uint4(r0, r1, r2, r3);
+                qcnt[at] = (int)rc;
+            }
+            qb += nq;
+            nq = 0;
+        };
+        load_query(q0);
+        for (int i1 = q0; i1 < n10; i1 += nwaves) {
+            const ulonglong2 a0 = na0, a1 = na1;
+            const float2 c = nc;
+            load_query(i1 + nwaves);
             const SiWindow w = si_window(K, ng, c, (float)window, G, colstart);
             // lane-local 4 smallest (Hamming << 16 | visit position), with their i2
             uint32_t hk[SI_TOPK], hi2[SI_TOPK];
@@ -486,11 +513,16 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
                     hk[SI_TOPK - 1] = hi2[SI_TOPK - 1] = 0xFFFFFFFFu;
                 }
             }
-            if (lane == 0) {
-                qtop[(size_t)pair * cap + i1] = make_uint4(top[0], top[1], top[2], top[3]);
-                qcnt[(size_t)pair * cap + i1] = count;
+            if (lane == nq) {
+                r0 = top[0];
+                r1 = top[1];
+                r2 = top[2];
+                r3 = top[3];
+                rc = (uint32_t)count;
             }
+            if (++nq == 64) flush();
         }
+        flush();
     };
     if (staged)
         scan_queries(std::true_type{});
