@@ -1825,9 +1825,15 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         const int m10 = wave_sum((int)s1 - 16 * (int)s0);
         const int m01 = wave_sum(vrow * (int)s0);
 
-        // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns
-        const uint32_t K0 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
-        const uint32_t K1 = 49u | (34u << 8) | (18u << 16);
+        // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns.
+        // Output column j of the realigned bytes R0 | R1 | R2 is sum_t w[t] * byte[j + t]: a dot4 of each
+        // dword with the kernel shifted by j (zero outside the 7 taps), 10 dot4 per row instead of 8
+        // byte-realignments and 8 dot4.
+        constexpr uint32_t kW[4][3] = {
+            {18u | 34u << 8 | 49u << 16 | 55u << 24, 49u | 34u << 8 | 18u << 16, 0u},
+            {18u << 8 | 34u << 16 | 49u << 24, 55u | 49u << 8 | 34u << 16 | 18u << 24, 0u},
+            {18u << 16 | 34u << 24, 49u | 55u << 8 | 49u << 16 | 34u << 24, 18u},
+            {18u << 24, 34u | 49u << 8 | 55u << 16 | 49u << 24, 34u | 18u << 8}};
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
             if (bitem[it] == 0xFFFF) break;
@@ -1839,14 +1845,14 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                 const uint32_t sh = (uint32_t)((csb + r * csp) & 3);
                 const uint32_t* rr = raw32 + raw_slot(r) * (kRawP / 4) + cg;
                 const uint32_t W0 = rr[0], W1 = rr[1], W2 = rr[2], W3 = rr[3];
-                const uint32_t R0 = __builtin_amdgcn_alignbyte(W1, W0, sh);
-                const uint32_t R1 = __builtin_amdgcn_alignbyte(W2, W1, sh);
-                const uint32_t R2 = __builtin_amdgcn_alignbyte(W3, W2, sh);
+                const uint32_t R[3] = {__builtin_amdgcn_alignbyte(W1, W0, sh), __builtin_amdgcn_alignbyte(W2, W1, sh),
+                                       __builtin_amdgcn_alignbyte(W3, W2, sh)};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const uint32_t A = __builtin_amdgcn_alignbyte(R1, R0, (uint32_t)j);
-                    const uint32_t B = __builtin_amdgcn_alignbyte(R2, R1, (uint32_t)j);
-                    o[e][j] = __builtin_amdgcn_udot4(A, K0, __builtin_amdgcn_udot4(B, K1, 0u, false), false);
+                    uint32_t acc = __builtin_amdgcn_udot4(R[0], kW[j][0], 0u, false);
+                    acc = __builtin_amdgcn_udot4(R[1], kW[j][1], acc, false);
+                    if (j >= 2) acc = __builtin_amdgcn_udot4(R[2], kW[j][2], acc, false);
+                    o[e][j] = acc;
                 }
             }
 #pragma unroll
