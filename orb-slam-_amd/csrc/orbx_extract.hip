@@ -303,12 +303,14 @@ __device__ __forceinline__ int fast_strength(const _Float16* c)
 
 // Compass value q of the pixel at c[0]: a 9-arc holds two consecutive compass points (ring positions
 // 0, 4, 8, 12), so s > t needs some consecutive pair brighter than v + t or darker than v - t, i.e.
-// q = max(max pair-min - v, v - min pair-max) > t.  An integer-valued f16.
+// q = max(max pair-min - v, v - min pair-max) > t.  An integer-valued f16.  Over the 4-cycle
+// (N, E, S, W) the largest pair minimum is min(max(N, S), max(E, W)): each consecutive pair holds one of
+// {N, S} and one of {E, W}, and the larger of N, S forms a pair with each of E, W.  Three packed ops.
 template <int TP>
 __device__ __forceinline__ _Float16 fast_compass_q(const _Float16* c)
 {
     const fh2 a = dup_neg(c[3 * TP]), b = dup_neg(c[3]), d = dup_neg(c[-3 * TP]), e = dup_neg(c[-3]);
-    const fh2 m = pmax2(pmax3(pmin2(a, b), pmin2(b, d), pmin2(d, e)), pmin2(e, a));   // (br, -dk)
+    const fh2 m = pmin2(pmax2(a, d), pmax2(b, e));   // (br, -dk)
     const fh2 q = m - dup_neg(c[0]);                                                 // (br - v, v - dk)
     return __builtin_fmaxf16(q.x, q.y);   // one v_max_f16 (SDWA high-half operand)
 }
@@ -327,69 +329,71 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* m, int t)
     return keep;
 }
 
-// ROI bytes of one cell staged in registers: up to kFastLd aligned dword pairs per lane
-// (a 37x38 ROI is 6 passes of 64 lanes); bigger ROIs load their remainder synchronously.
-constexpr int kFastLd = 6;
+// ROI bytes of one cell staged in registers, in passes of rpp whole rows: lane = rl * (nd + 1) + kl loads
+// aligned dword kl of row u * rpp + rl (nd = dwords per ROI row; the row's extra dword kl = nd only feeds
+// its neighbour), and the realigning second dword of a lane is the next lane's, read by DPP at the
+// commit, so a pass costs one register.  LD passes are prefetched (the launch's largest ROI: 8 for
+// 38 x 39, 10 for 38 x 46 ROIs); bigger ROIs load their remainder synchronously.
 #ifndef ORBX_FAST_CPW
 #define ORBX_FAST_CPW 3
 #endif
 constexpr int kCellsPerWave = ORBX_FAST_CPW;   // cells per wave: the next cell's ROI loads fly under this one's passes
 
+template <int LD>
 struct FastPrefetch {
-    uint32_t lo[kFastLd], hi[kFastLd];   // placement (row, dword) is recomputed at the commit
+    uint32_t w[LD];
 };
 
 struct FastCellSrc {
     const uint8_t* src;   // ROI origin
-    int pitch, nd, ntot;
-    float inv_nd;
+    int pitch, nd, rh;    // dwords per row ceil(roi_w / 4), rows
+    int rpp, rl, kl;      // rows per pass floor(64 / (nd + 1)); this lane's row in a pass and dword
 };
 
-// ROI dword k of row r for flat index i (lane-major passes), at byte offset o from the aligned origin
-__device__ __forceinline__ bool fast_slot(const FastCellSrc& S, int i, int& r, int& k, uint32_t& o)
+__device__ __forceinline__ void fast_lane_map(FastCellSrc& S, int lane)
 {
-    if (i >= S.ntot) return false;
-    r = (int)(((float)i + 0.5f) * S.inv_nd);
-    k = i - __mul24(r, S.nd);
-    o = (uint32_t)((uintptr_t)S.src & 3) + (uint32_t)__mul24(r, S.pitch) + 4u * (uint32_t)k;
-    return true;
+    const int nd1 = S.nd + 1;
+    S.rpp = 64 / nd1;
+    S.rl = (int)(((float)lane + 0.5f) / (float)nd1);
+    S.kl = lane - S.rl * nd1;
 }
 
-__device__ __forceinline__ void fast_issue(const FastCellSrc& S, int i0, int lane, FastPrefetch& F)
+template <int LD>
+__device__ __forceinline__ void fast_issue(const FastCellSrc& S, int u0, FastPrefetch<LD>& F)
 {
     // 32-bit byte offsets from the wave-uniform aligned ROI origin: scalar base + vector offset
     // addressing, no 64-bit address arithmetic per load
     const __attribute__((address_space(1))) uint8_t* base =
         (const __attribute__((address_space(1))) uint8_t*)((uintptr_t)S.src & ~(uintptr_t)3);
+    const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
 #pragma unroll
-    for (int u = 0; u < kFastLd; ++u) {
-        int r, k;
-        uint32_t o;
-        if (fast_slot(S, i0 + u * 64 + lane, r, k, o)) {
-            const __attribute__((address_space(1))) uint32_t* ap =
-                (const __attribute__((address_space(1))) uint32_t*)(base + (o & ~3u));
-            F.lo[u] = ap[0];
-            F.hi[u] = ap[1];
+    for (int u = 0; u < LD; ++u) {
+        const int row = (u0 + u) * S.rpp + S.rl;
+        if (S.rl < S.rpp && row < S.rh) {
+            const uint32_t o = ((s0 + (uint32_t)__mul24(row, S.pitch)) & ~3u) + 4u * (uint32_t)S.kl;
+            F.w[u] = *(const __attribute__((address_space(1))) uint32_t*)(base + o);
         }
     }
 }
 
-// 4 pixels of ROI row r from column 4k as f16 (0x6400 | x): two v_perm (bytes 0, 1 and 2, 3 of the
-// realigned dword into the low bytes of two halves) and two ors, one 8-byte LDS store
-template <int TP>
-__device__ __forceinline__ void fast_commit(const FastPrefetch& F, const FastCellSrc& S, int i0, int lane,
-                                            _Float16* tile)
+// 4 pixels of ROI row r from column 4 kl as f16 (0x6400 | x): the lane's dword and its neighbour's
+// realigned by the row's byte shift, two v_perm (bytes 0, 1 and 2, 3 into the low bytes of two halves)
+// and two ors, one 8-byte LDS store
+template <int TP, int LD>
+__device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const FastCellSrc& S, int u0, _Float16* tile)
 {
+    const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
 #pragma unroll
-    for (int u = 0; u < kFastLd; ++u) {
-        int r, k;
-        uint32_t o;
-        if (!fast_slot(S, i0 + u * 64 + lane, r, k, o)) continue;
-        const uint32_t w = __builtin_amdgcn_alignbyte(F.hi[u], F.lo[u], o & 3u);
-        uint2 q;
-        q.x = __builtin_amdgcn_perm(0u, w, 0x0C010C00u) | 0x64006400u;
-        q.y = __builtin_amdgcn_perm(0u, w, 0x0C030C02u) | 0x64006400u;
-        *(uint2*)(tile + r * TP + 4 * k) = q;
+    for (int u = 0; u < LD; ++u) {
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)F.w[u], 0x130, 0xF, 0xF, false);   // wave_shl:1
+        const int row = (u0 + u) * S.rpp + S.rl;
+        if (S.rl < S.rpp && S.kl < S.nd && row < S.rh) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(hi, F.w[u], (s0 + (uint32_t)__mul24(row, S.pitch)) & 3u);
+            uint2 q;
+            q.x = __builtin_amdgcn_perm(0u, w, 0x0C010C00u) | 0x64006400u;
+            q.y = __builtin_amdgcn_perm(0u, w, 0x0C030C02u) | 0x64006400u;
+            *(uint2*)(tile + row * TP + 4 * S.kl) = q;
+        }
     }
 }
 
@@ -422,7 +426,10 @@ __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builti
 #ifndef ORBX_FAST_WPE
 #define ORBX_FAST_WPE 1
 #endif
-template <int TP>
+#ifndef ORBX_FAST_SPT
+#define ORBX_FAST_SPT 1   // strength entries per lane per trip
+#endif
+template <int TP, int LD>
 __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                    const Cell* __restrict__ cells, uint32_t* __restrict__ slots,
                                                    int* __restrict__ cell_counts, int cb, int ce, int rw, int rh,
@@ -477,8 +484,8 @@ __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry
         S.src = img + (size_t)C.roi_y0 * pitch + C.roi_x0;
         S.pitch = pitch;
         S.nd = (C.roi_w + 3) >> 2;
-        S.ntot = C.roi_h * S.nd;
-        S.inv_nd = 1.0f / (float)S.nd;   // exact row split for ntot < 4096
+        S.rh = C.roi_h;
+        fast_lane_map(S, lane);
         return S;
     };
     // the cell descriptor as whole dwords: scalar loads (a 16-bit field read is a vector load, whose
@@ -499,19 +506,19 @@ __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry
     };
     Cell C = load_cell(c0);
     FastCellSrc S = cell_src(C);
-    FastPrefetch F;
-    fast_issue(S, 0, lane, F);
+    FastPrefetch<LD> F;
+    fast_issue(S, 0, F);
 
 #pragma unroll 1
     for (int c = c0; c < c1; ++c) {
         const int dw = C.roi_w - 6, dh = C.roi_h - 6;
         const Cell Cc = C;
         FP_STAMP(7);
-        fast_commit<TP>(F, S, 0, lane, tile);
-        for (int i0 = 64 * kFastLd; i0 < S.ntot; i0 += 64 * kFastLd) {   // ROIs beyond 6 passes
-            FastPrefetch R;
-            fast_issue(S, i0, lane, R);
-            fast_commit<TP>(R, S, i0, lane, tile);
+        fast_commit<TP>(F, S, 0, tile);
+        for (int u0 = LD; u0 * S.rpp < S.rh; u0 += LD) {   // ROIs beyond LD passes
+            FastPrefetch<LD> R;
+            fast_issue(S, u0, R);
+            fast_commit<TP>(R, S, u0, tile);
         }
         const int mapn = (dh + 2) * TP;
         FP_STAMP(0);
@@ -521,7 +528,7 @@ __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry
         if (c + 1 < c1) {   // prefetch the next cell (registers only; lands under the passes below)
             C = load_cell(c + 1);
             S = cell_src(C);
-            fast_issue(S, 0, lane, F);
+            fast_issue(S, 0, F);
         }
         if (dw <= 0 || dh <= 0) {
             wave_lds_sync();
@@ -572,6 +579,7 @@ __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry
         // place (a trip writes at or before what it has read).  Returns the compacted count.
         auto strengths = [&](int n, bool back) {
             int n2 = 0;
+#if ORBX_FAST_SPT == 2
             for (int j0 = 0; j0 < n; j0 += 128) {   // two entries per lane per trip
                 const int ja = j0 + lane, jb = ja + 64;
                 // lanes past the list re-test its last entry, masked out below
@@ -592,6 +600,24 @@ __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry
                 if (inb) list[back ? lcap - 1 - (n2 + lanes_below(mb)) : n2 + lanes_below(mb)] = (uint16_t)kb;
                 n2 += __popcll(mb);
             }
+#else
+            // one entry per lane per trip: the strength's 16 ring values and their arc maxima are the
+            // kernel's register peak, and only ~15% of the window gets here
+            for (int j0 = 0; j0 < n; j0 += 64) {
+                const int ja = j0 + lane;
+                // lanes past the list re-test its last entry, masked out below
+                const int pa = back ? lcap - 1 - min(ja, n - 1) : min(ja, n - 1);
+                const int ka = list[pa];
+                const int sa = fast_strength<TP>(tile + ka + (3 * TP + 3));
+                // mask before any branch (an i1 live across a divergent branch is materialised in a VGPR)
+                const unsigned long long ma = ballot64(ja < n) & ballot64(sa > t_lo);
+                const bool ina = (ja < n) & (sa > t_lo);
+                if (ina) map[ka + (TP + 1)] = (uint8_t)sa;
+                wave_lds_sync();   // the entries are read before the compaction overwrites the list
+                if (ina) list[back ? lcap - 1 - (n2 + lanes_below(ma)) : n2 + lanes_below(ma)] = (uint16_t)ka;
+                n2 += __popcll(ma);
+            }
+#endif
             wave_lds_sync();
             return n2;
         };
@@ -750,15 +776,15 @@ void fast_groups(Geometry& g)
     g.fast_rh[1] = h1;
 }
 
-template <int TP>
+template <int TP, int LD>
 static void fast_launch(const ExtractBufs& b, const FramePtrs& p, int cb, int ce, int rw, int rh, int cpw,
                         int batch, hipStream_t s)
 {
     dim3 grid((ce - cb + cpw - 1) / cpw, batch);
     const size_t smem = fast_wave_bytes(rw, rh);
-    hipFuncSetAttribute((const void*)k_fast_cells<TP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(k_fast_cells<TP>, grid, dim3(64), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts, cb, ce,
-                       rw, rh, cpw);
+    hipFuncSetAttribute((const void*)k_fast_cells<TP, LD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL((k_fast_cells<TP, LD>), grid, dim3(64), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
+                       cb, ce, rw, rh, cpw);
 }
 
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
@@ -768,10 +794,15 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
     for (int i = 0; i < g.fast_groups; ++i) {
         const int cb = g.fast_cb[i], ce = g.fast_cb[i + 1];
         if (ce <= cb) continue;
-        if (fast_tile_pitch(g.fast_rw[i]) == 40)
-            fast_launch<40>(b, p, cb, ce, g.fast_rw[i], g.fast_rh[i], cpw, batch, s);
-        else
-            fast_launch<68>(b, p, cb, ce, g.fast_rw[i], g.fast_rh[i], cpw, batch, s);
+        const int rw = g.fast_rw[i], rh = g.fast_rh[i];
+        // register prefetch passes: the group's largest ROI in passes of whole rows (fast_lane_map)
+        const int rpp = 64 / (((rw + 3) >> 2) + 1), ld = (rh + rpp - 1) / rpp;
+        if (fast_tile_pitch(rw) == 40) {
+            if (ld <= 8) fast_launch<40, 8>(b, p, cb, ce, rw, rh, cpw, batch, s);
+            else fast_launch<40, 10>(b, p, cb, ce, rw, rh, cpw, batch, s);
+        } else {
+            fast_launch<68, 10>(b, p, cb, ce, rw, rh, cpw, batch, s);
+        }
     }
 }
 
