@@ -347,52 +347,61 @@ struct FastPrefetch {
 struct FastCellSrc {
     const uint8_t* src;   // ROI origin
     int pitch, nd, rh;    // dwords per row ceil(roi_w / 4), rows
-    int rpp, rl, kl;      // rows per pass floor(64 / (nd + 1)); this lane's row in a pass and dword
 };
 
-__device__ __forceinline__ void fast_lane_map(FastCellSrc& S, int lane)
-{
-    const int nd1 = S.nd + 1;
-    S.rpp = 64 / nd1;
-    S.rl = (int)(((float)lane + 0.5f) / (float)nd1);
-    S.kl = lane - S.rl * nd1;
-}
+// The lane map of the tile pitch's widest row (TP / 4 dwords + the extra one): rows per pass and the
+// lane's (row in pass, dword) are compile-time / per-kernel constants, so every pass's offsets are
+// immediates; a narrower cell leaves its lanes past its own dwords idle.
+template <int TP>
+struct FastLaneMap {
+    static constexpr int kND1 = TP / 4 + 1, kRPP = 64 / kND1;
+    int rl, kl;
+    __device__ explicit FastLaneMap(int lane) : rl(lane / kND1), kl(lane - (lane / kND1) * kND1) {}
+};
 
-template <int LD>
-__device__ __forceinline__ void fast_issue(const FastCellSrc& S, int u0, FastPrefetch<LD>& F)
+template <int TP, int LD>
+__device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneMap<TP>& M, int u0, FastPrefetch<LD>& F)
 {
     // 32-bit byte offsets from the wave-uniform aligned ROI origin: scalar base + vector offset
     // addressing, no 64-bit address arithmetic per load
     const __attribute__((address_space(1))) uint8_t* base =
         (const __attribute__((address_space(1))) uint8_t*)((uintptr_t)S.src & ~(uintptr_t)3);
     const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
+    const bool lane_ok = M.rl < FastLaneMap<TP>::kRPP && M.kl <= S.nd;
 #pragma unroll
     for (int u = 0; u < LD; ++u) {
-        const int row = (u0 + u) * S.rpp + S.rl;
-        if (S.rl < S.rpp && row < S.rh) {
-            const uint32_t o = ((s0 + (uint32_t)__mul24(row, S.pitch)) & ~3u) + 4u * (uint32_t)S.kl;
+        const int row = (u0 + u) * FastLaneMap<TP>::kRPP + M.rl;
+        if (lane_ok && row < S.rh) {
+            const uint32_t o = ((s0 + (uint32_t)__mul24(row, S.pitch)) & ~3u) + 4u * (uint32_t)M.kl;
             F.w[u] = *(const __attribute__((address_space(1))) uint32_t*)(base + o);
         }
     }
 }
 
 // 4 pixels of ROI row r from column 4 kl as f16 (0x6400 | x): the lane's dword and its neighbour's
-// realigned by the row's byte shift, two v_perm (bytes 0, 1 and 2, 3 into the low bytes of two halves)
-// and two ors, one 8-byte LDS store
+// realigned by the row's byte shift (v_alignbyte uses the shift's low two bits, so the shift of pass u
+// is the lane's first one plus a uniform step), two v_perm (bytes 0, 1 and 2, 3 into the low bytes of
+// two halves) and two ors, one 8-byte LDS store at an immediate offset per pass
 template <int TP, int LD>
-__device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const FastCellSrc& S, int u0, _Float16* tile)
+__device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const FastCellSrc& S,
+                                            const FastLaneMap<TP>& M, int u0, _Float16* tile)
 {
+    constexpr int kRPP = FastLaneMap<TP>::kRPP;
     const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
+    const bool lane_ok = M.rl < kRPP && M.kl < S.nd;
+    const int row0 = u0 * kRPP + M.rl;
+    const uint32_t sh0 = s0 + (uint32_t)__mul24(row0, S.pitch);
+    const uint32_t dsh = (uint32_t)__mul24(kRPP, S.pitch);
+    _Float16* dst = tile + row0 * TP + 4 * M.kl;
 #pragma unroll
     for (int u = 0; u < LD; ++u) {
         const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)F.w[u], 0x130, 0xF, 0xF, false);   // wave_shl:1
-        const int row = (u0 + u) * S.rpp + S.rl;
-        if (S.rl < S.rpp && S.kl < S.nd && row < S.rh) {
-            const uint32_t w = __builtin_amdgcn_alignbyte(hi, F.w[u], (s0 + (uint32_t)__mul24(row, S.pitch)) & 3u);
+        if (lane_ok && row0 + u * kRPP < S.rh) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(hi, F.w[u], sh0 + (uint32_t)u * dsh);
             uint2 q;
             q.x = __builtin_amdgcn_perm(0u, w, 0x0C010C00u) | 0x64006400u;
             q.y = __builtin_amdgcn_perm(0u, w, 0x0C030C02u) | 0x64006400u;
-            *(uint2*)(tile + row * TP + 4 * S.kl) = q;
+            *(uint2*)(dst + u * kRPP * TP) = q;
         }
     }
 }
@@ -426,11 +435,14 @@ __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builti
 #ifndef ORBX_FAST_WPE
 #define ORBX_FAST_WPE 1
 #endif
+#ifndef ORBX_FAST_WPE10
+#define ORBX_FAST_WPE10 1   // 6 (80 VGPRs, 6 dwords spilled) measured 200.9 against 183.3 us
+#endif
 #ifndef ORBX_FAST_SPT
 #define ORBX_FAST_SPT 1   // strength entries per lane per trip
 #endif
 template <int TP, int LD>
-__global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
+__global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                    const Cell* __restrict__ cells, uint32_t* __restrict__ slots,
                                                    int* __restrict__ cell_counts, int cb, int ce, int rw, int rh,
                                                    int cpw)
@@ -485,7 +497,6 @@ __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry
         S.pitch = pitch;
         S.nd = (C.roi_w + 3) >> 2;
         S.rh = C.roi_h;
-        fast_lane_map(S, lane);
         return S;
     };
     // the cell descriptor as whole dwords: scalar loads (a 16-bit field read is a vector load, whose
@@ -506,19 +517,20 @@ __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry
     };
     Cell C = load_cell(c0);
     FastCellSrc S = cell_src(C);
+    const FastLaneMap<TP> M(lane);
     FastPrefetch<LD> F;
-    fast_issue(S, 0, F);
+    fast_issue(S, M, 0, F);
 
 #pragma unroll 1
     for (int c = c0; c < c1; ++c) {
         const int dw = C.roi_w - 6, dh = C.roi_h - 6;
         const Cell Cc = C;
         FP_STAMP(7);
-        fast_commit<TP>(F, S, 0, tile);
-        for (int u0 = LD; u0 * S.rpp < S.rh; u0 += LD) {   // ROIs beyond LD passes
+        fast_commit(F, S, M, 0, tile);
+        for (int u0 = LD; u0 * FastLaneMap<TP>::kRPP < S.rh; u0 += LD) {   // ROIs beyond LD passes
             FastPrefetch<LD> R;
-            fast_issue(S, u0, R);
-            fast_commit<TP>(R, S, u0, tile);
+            fast_issue(S, M, u0, R);
+            fast_commit(R, S, M, u0, tile);
         }
         const int mapn = (dh + 2) * TP;
         FP_STAMP(0);
@@ -528,7 +540,7 @@ __global__ __launch_bounds__(64, ORBX_FAST_WPE) void k_fast_cells(const Geometry
         if (c + 1 < c1) {   // prefetch the next cell (registers only; lands under the passes below)
             C = load_cell(c + 1);
             S = cell_src(C);
-            fast_issue(S, 0, F);
+            fast_issue(S, M, 0, F);
         }
         if (dw <= 0 || dh <= 0) {
             wave_lds_sync();
@@ -795,8 +807,8 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
         const int cb = g.fast_cb[i], ce = g.fast_cb[i + 1];
         if (ce <= cb) continue;
         const int rw = g.fast_rw[i], rh = g.fast_rh[i];
-        // register prefetch passes: the group's largest ROI in passes of whole rows (fast_lane_map)
-        const int rpp = 64 / (((rw + 3) >> 2) + 1), ld = (rh + rpp - 1) / rpp;
+        // register prefetch passes: the group's largest ROI in passes of whole rows (FastLaneMap)
+        const int rpp = 64 / (fast_tile_pitch(rw) / 4 + 1), ld = (rh + rpp - 1) / rpp;
         if (fast_tile_pitch(rw) == 40) {
             if (ld <= 8) fast_launch<40, 8>(b, p, cb, ce, rw, rh, cpw, batch, s);
             else fast_launch<40, 10>(b, p, cb, ce, rw, rh, cpw, batch, s);
