@@ -835,13 +835,13 @@ constexpr int QT_NW = QT_NT / 64;
 // per-level phase cycle sums (thread 0 of each workgroup): gather, init, phase-1 rounds, phase-2
 // rounds, phase-2 sorts, retain, #phase-1 rounds, #phase-2 rounds, #workgroups
 __device__ unsigned long long g_qt_prof[16][16];
+// stamps accumulate in registers and are flushed once at the end: a global atomic per stamp would hold
+// every later barrier (__syncthreads waits for the wave's outstanding memory operations)
 #define QT_STAMP(slot, t0)                                                            \
     do {                                                                              \
-        if (threadIdx.x == 0) {                                                       \
-            const long long t1_ = clock64();                                          \
-            atomicAdd(&g_qt_prof[l][slot], (unsigned long long)(t1_ - (t0)));         \
-            t0 = t1_;                                                                 \
-        }                                                                             \
+        const long long t1_ = clock64();                                              \
+        qt_acc[slot] += (unsigned long long)(t1_ - (t0));                             \
+        t0 = t1_;                                                                     \
     } while (0)
 #else
 #define QT_STAMP(slot, t0) ((void)0)
@@ -893,6 +893,37 @@ __device__ uint32_t block_scan_excl(uint32_t* a, int n, uint32_t* wsum)
     return total;
 }
 
+// Exclusive scan of v(0..n) into a[]; returns the total.  v is evaluated (twice) by the thread whose run
+// holds the element, so a scan whose terms come from LDS already in place needs no barrier before it.
+template <int QT_NT, class F>
+__device__ uint32_t block_scan_fn(uint32_t* a, int n, uint32_t* wsum, F&& v)
+{
+    constexpr int QT_NW = QT_NT / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int per = (n + QT_NT - 1) / QT_NT;
+    const int b = tid * per, e = min(n, b + per);
+    uint32_t local = 0;
+    for (int i = b; i < e; ++i) local += v(i);
+    const uint32_t inc = wave_incl_scan(local);
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < QT_NW; ++w) {
+        const uint32_t t = wsum[w];
+        before += w < wid ? t : 0u;
+        total += t;
+    }
+    uint32_t run = before + inc - local;
+    for (int i = b; i < e; ++i) {
+        const uint32_t t = v(i);
+        a[i] = run;
+        run += t;
+    }
+    __syncthreads();
+    return total;
+}
+
 __device__ __forceinline__ int next_pow2(int v)
 {
     int p = 1;
@@ -901,11 +932,16 @@ __device__ __forceinline__ int next_pow2(int v)
 }
 
 struct QtLayout {
-    size_t scan, rect, cnt, srank, npos, snode, smx, smy, ccnt, cpos, vprev, vnew, skey, best, wsum, sh, total;
+    size_t scan, rect, cnt, srank, npos, snode, sinfo, ccnt, cpos, vprev, vnew, skey, best, wsum, sh, kpa, total;
 };
 
-// ixb: bytes per node index (2 with the node arrays in LDS, 4 in global memory)
-__host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap, int ixb = 2)
+// Keypoints held in LDS instead of registers (kpa, one dword per register slot) by the wide LDS-node
+// templates (16+ keypoints per thread): their 32 register arrays under the 128-VGPR budget spilled to
+// scratch.  Slot r of thread t is kpa[t + r * NT], so a wave's accesses are conflict-free.
+__host__ __device__ constexpr int qt_kpn(int nt, int kpt, int glob) { return (!glob && kpt >= 16) ? nt * kpt : 0; }
+
+// ixb: bytes per node index (2 with the node arrays in LDS, 4 in global memory); kpn: LDS keypoint slots
+__host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap, int ixb = 2, int kpn = 0)
 {
     QtLayout L;
     size_t o = 0;
@@ -923,8 +959,7 @@ __host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap, int ixb = 2
     L.srank = take((size_t)ixb * lcap);
     L.npos = take((size_t)ixb * lcap);
     L.snode = take((size_t)ixb * lcap);
-    L.smx = take(sizeof(int16_t) * lcap);
-    L.smy = take(sizeof(int16_t) * lcap);
+    L.sinfo = take(sizeof(uint32_t) * lcap);
     L.ccnt = take(sizeof(uint32_t) * 4 * lcap);
     L.cpos = take((size_t)ixb * 4 * lcap);
     L.vprev = take((size_t)ixb * lcap);
@@ -933,6 +968,7 @@ __host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap, int ixb = 2
     L.best = take(sizeof(unsigned long long) * lcap);
     L.wsum = take(sizeof(uint32_t) * (QT_NW + 1));
     L.sh = take(sizeof(int) * 16);
+    L.kpa = take(sizeof(uint32_t) * kpn);
     L.total = o;
     return L;
 }
@@ -1009,10 +1045,13 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
     const int tid = threadIdx.x;
 #ifdef ORBX_QT_PROF
     const long long qt_t0 = clock64();
+    unsigned long long qt_acc[16] = {};
 #endif
     const LevelGeom& LG = G->lv[l];
     // lcap / cellcap: node-list and cell capacity of this launch's levels (qt_launch)
-    const QtLayout Ly = qt_layout(lcap, cellcap, (int)sizeof(Ix));
+    constexpr bool kKpL = qt_kpn(QT_NT, QT_KPT, kG) > 0;
+    const QtLayout Ly = qt_layout(lcap, cellcap, (int)sizeof(Ix), qt_kpn(QT_NT, QT_KPT, kG));
+    uint32_t* kpa = (uint32_t*)(smem + Ly.kpa);
     uint8_t* nb = smem;
     if constexpr (kG) nb = gnodes + (size_t)f * G->qtg_per_frame + LG.qtg_off;
     uint32_t* scan = (uint32_t*)(nb + Ly.scan);
@@ -1021,8 +1060,7 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
     Ix* srank = (Ix*)(nb + Ly.srank);
     Ix* npos = (Ix*)(nb + Ly.npos);
     Ix* snode = (Ix*)(nb + Ly.snode);
-    int16_t* smx = (int16_t*)(nb + Ly.smx);
-    int16_t* smy = (int16_t*)(nb + Ly.smy);
+    uint32_t* sinfo = (uint32_t*)(nb + Ly.sinfo);   // per list position: split candidate flag | midlines
     uint32_t* ccnt = (uint32_t*)(nb + Ly.ccnt);
     Ix* cpos = (Ix*)(nb + Ly.cpos);
     Ix* vprev = (Ix*)(nb + Ly.vprev);
@@ -1036,10 +1074,36 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
 
     // ---- 1. gather this level's FAST candidates in reference order ----------
     const int ncl = LG.ncells, cb = LG.cell_begin;
-    for (int c = tid; c < ncl; c += QT_NT) scan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
+    const uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
+    // LDS node arrays (rect .. wsum) are free until the candidates are in registers: the cells' slot bases
+    // load there beside the counts (both in flight together), and after the scan a per-candidate owner
+    // map (u16 cell index) lets every candidate's slot load go out at once, with no per-candidate binary
+    // search and no dependent cell-table load.
+    uint32_t* gbase = (uint32_t*)(nb + Ly.rect);
+    uint16_t* owner = (uint16_t*)(gbase + ncl);
+    const size_t gregion = kG ? 0 : Ly.wsum - Ly.rect;
+    const bool gb_ok = !kG && ncl <= 65536 && (size_t)4 * ncl <= gregion;   // block-uniform
+    for (int c = tid; c < ncl; c += QT_NT) {
+        scan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
+        if (gb_ok) gbase[c] = (uint32_t)cells[cb + c].slot_base;
+    }
     __syncthreads();
     const int n = (int)block_scan_excl<QT_NT>(scan, ncl, wsum);
-    const uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
+#ifdef ORBX_QT_PROF
+    long long qt_g = qt_t0;
+    QT_STAMP(4, qt_g);
+#endif
+    const bool omap = gb_ok && (size_t)4 * ncl + 2 * (size_t)n <= gregion;
+    if (omap) {
+        for (int c = tid; c < ncl; c += QT_NT) {
+            const int base = (int)scan[c], cnt = (c + 1 < ncl ? (int)scan[c + 1] : n) - base;
+            for (int j = 0; j < cnt; ++j) owner[base + j] = (uint16_t)c;
+        }
+        __syncthreads();
+    }
+#ifdef ORBX_QT_PROF
+    QT_STAMP(14, qt_g);
+#endif
     uint32_t* fspill = spill + (size_t)f * G->spill_per_frame + (LG.slot_begin > 0 ? 0 : 0);
     uint32_t* fspill_node = spill_node + (size_t)f * G->spill_per_frame;
     // spill region of this level: levels share the frame's spill array in level order
@@ -1053,6 +1117,10 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
         fspill_node += off;
     }
     auto fetch = [&](int i) -> uint32_t {
+        if (omap) {
+            const int c = owner[i];
+            return fslots[gbase[c] + (uint32_t)(i - (int)scan[c])];
+        }
         int lo = 0, hi = ncl - 1;   // last cell with scan[c] <= i
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -1060,40 +1128,79 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
         }
         return fslots[cells[cb + lo].slot_base + (i - (int)scan[lo])];
     };
-    uint32_t kp[QT_KPT], nd[QT_KPT];
-    // The node arrays (rect .. wsum) are not in use yet: when the level's candidates
-    // fit there, every thread copies whole cells into it (a cell's candidates are contiguous in its
-    // slots) and then reads its own indices, instead of a binary search over the cells plus a
-    // dependent cell-table load per candidate.
+    uint32_t kp[kKpL ? 1 : QT_KPT], nd[QT_KPT];
+    // register slot r's keypoint (candidate tid + r * QT_NT)
+    auto kpr = [&](int r) -> uint32_t {
+        if constexpr (kKpL) return kpa[tid + r * QT_NT];
+        else return kp[r];
+    };
+    // kG: the level's global region is sized to stage every candidate slot (qt_prepare); every thread
+    // copies whole cells into it (a cell's candidates are contiguous in its slots) and then reads its own
+    // indices
     uint32_t* stage = (uint32_t*)(nb + Ly.rect);
-    // (small levels keep the search: their few hundred candidates spread over few cells, and a
-    // thread's serial copy of a whole cell costs more there than the lanes' parallel searches;
-    // a global region is sized to stage the level's every candidate slot, qt_prepare)
-    const bool staged = kG ? (long long)n * 4 <= LG.qtg_bytes - (long long)Ly.rect
-                           : n >= 1024 && (size_t)n * 4 <= Ly.wsum - Ly.rect;   // block-uniform; wsum / sh untouched
+    const bool staged = kG && (long long)n * 4 <= LG.qtg_bytes - (long long)Ly.rect;   // block-uniform
     if (staged) {
         for (int c = tid; c < ncl; c += QT_NT) {
             const int base = (int)scan[c], cnt = (c + 1 < ncl ? (int)scan[c + 1] : n) - base;
             const uint32_t* src = fslots + cells[cb + c].slot_base;
-            for (int j = 0; j < cnt; ++j) stage[base + j] = src[j];
+            // 8 loads in flight per batch instead of one dependent HBM round trip per candidate
+            for (int j0 = 0; j0 < cnt; j0 += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = j0 + u < cnt ? src[j0 + u] : 0u;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (j0 + u < cnt) stage[base + j0 + u] = v[u];
+            }
         }
         __syncthreads();
     }
+    // register slot r of thread t is candidate t + r * QT_NT (a wave's lanes hold consecutive candidates:
+    // coalesced loads, conflict-free LDS slots, runs of equal nodes for wave_run_add).  The owner-map and
+    // staged forms are branch-free (indices clamped, the loads of every slot in flight together); the
+    // search form branches.
+    if (n > 0 && (omap || staged)) {   // block-uniform
 #pragma unroll
-    for (int r = 0; r < QT_KPT; ++r) {
-        const int i = tid + r * QT_NT;
-        kp[r] = i < n ? (staged ? stage[i] : fetch(i)) : 0u;
-        nd[r] = 0;
+        for (int r = 0; r < QT_KPT; ++r) {
+            const int i = tid + r * QT_NT, ii = min(i, n - 1);
+            uint32_t v;
+            if (omap) {
+                const int c = owner[ii];
+                v = fslots[gbase[c] + (uint32_t)(ii - (int)scan[c])];
+            } else {
+                v = stage[ii];
+            }
+            if constexpr (kKpL) kpa[i] = i < n ? v : 0u;
+            else kp[r] = i < n ? v : 0u;
+            nd[r] = 0;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < QT_KPT; ++r) {
+            const int i = tid + r * QT_NT;
+            if constexpr (kKpL) kpa[i] = i < n ? fetch(i) : 0u;
+            else kp[r] = i < n ? fetch(i) : 0u;
+            nd[r] = 0;
+        }
     }
     for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) fspill[i - QT_NT * QT_KPT] = staged ? stage[i] : fetch(i);
+#ifdef ORBX_QT_PROF
+    QT_STAMP(15, qt_g);
+#endif
     __syncthreads();   // the staging area becomes the node arrays
+#ifdef ORBX_QT_PROF
+    QT_STAMP(13, qt_g);
+#endif
 
     // visit every keypoint (register part unrolled, spill part in a loop)
     auto visit = [&](auto&& fn) {
 #pragma unroll
         for (int r = 0; r < QT_KPT; ++r) {
             const int i = tid + r * QT_NT;
-            if (i < n) fn(kp[r], nd[r], i);
+            if (i < n) {
+                uint32_t k = kpr(r);
+                fn(k, nd[r], i);
+            }
         }
         for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) {
             uint32_t k = fspill[i - QT_NT * QT_KPT];
@@ -1105,8 +1212,7 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
 
 #ifdef ORBX_QT_PROF
     __syncthreads();
-    long long qt_t = 0;
-    if (threadIdx.x == 0) qt_t = qt_t0;
+    long long qt_t = qt_t0;
     QT_STAMP(0, qt_t);
 #endif
     // ---- 2. initial nodes, src/ORBextractor.cc:650-699 ------------------------
@@ -1126,7 +1232,7 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
         const int i = tid + r * QT_NT;
         int key = -1;
         if (i < n) {
-            key = root_of(kp[r]);
+            key = root_of(kpr(r));
             nd[r] = (uint32_t)key;
         }
         wave_run_add(ccnt, key);
@@ -1168,15 +1274,26 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
 #ifdef ORBX_QT_PROF
     __syncthreads();
     QT_STAMP(1, qt_t);
+    const long long qt_r0 = qt_t;
 #endif
+    // A round is five barrier-separated steps (phase 1: 8 barriers, was 15):
+    //   A  split set: phase 1 every node with more than one key, ranked in list order (a scan);
+    //      phase 2 vPrev ranked by (size, creation) descending.  The ranking thread also writes the
+    //      node's midlines (ExtractorNode::DivideNode, :572-573) and clears its four child counters.
+    //   B  count pass: every keypoint's child slot (4 * split rank + quadrant) and the child counts.
+    //   C  one scan of (children, expandable children) per split node, packed in 16-bit halves;
+    //      phase 2 then finds how many candidates are split (kk) and the non-split ranks.
+    //   D  the new list: children of split rank s at Ctot - prefix(s) - children(s) (later splits in
+    //      front, n4..n1), the rest after them in order; expandable children in creation order.
+    //   E  relabel every keypoint with its new list position.
+    // The scans evaluate their terms from LDS already in place (block_scan_fn), so no barrier precedes them.
+    uint32_t* scan2 = scan + lcap + 1;   // phase 2's non-split flags (scan[0..S] holds step C's prefixes)
     while (true) {
         __syncthreads();
         if (sh[SH_DONE]) break;
 #ifdef ORBX_QT_PROF
-        const int qt_phase = sh[SH_PHASE];
-        if (threadIdx.x == 0) atomicAdd(&g_qt_prof[l][qt_phase == 1 ? 6 : 7], 1ull);
-        long long qr = 0;
-        if (threadIdx.x == 0) qr = clock64();
+        if (sh[SH_PHASE] == 1) qt_acc[6] += 1;
+        else qt_acc[7] += 1;
 #endif
         const int L = sh[SH_L];
         const int phase = sh[SH_PHASE];
@@ -1184,46 +1301,52 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
         uint32_t* cntn = cntb + (size_t)(cur ^ 1) * lcap;
         int16_t *cx0 = R(cur, 0), *cx1 = R(cur, 1), *cy0 = R(cur, 2), *cy1 = R(cur, 3);
         int16_t *nx0 = R(cur ^ 1, 0), *nx1 = R(cur ^ 1, 1), *ny0 = R(cur ^ 1, 2), *ny1 = R(cur ^ 1, 3);
+        const Ix* vin = cur ? vnew : vprev;   // this round's vPrev (the previous round's expandable children)
+        Ix* vout = cur ? vprev : vnew;
+        auto set_split = [&](int s, int p) {
+            srank[p] = (Ix)s;
+            snode[s] = (Ix)p;
+            const int hx = (int)ceilf((float)(cx1[p] - cx0[p]) / 2);
+            const int hy = (int)ceilf((float)(cy1[p] - cy0[p]) / 2);
+            sinfo[p] = 0x80000000u | (uint32_t)(cx0[p] + hx) | ((uint32_t)(cy0[p] + hy) << 12);
+            ccnt[4 * p] = ccnt[4 * p + 1] = ccnt[4 * p + 2] = ccnt[4 * p + 3] = 0;
+        };
 
-        int S;           // number of candidate (split) nodes this round
-        int m = 0;       // phase 2: vPrev length
+        // ---- A ----
+        int S;   // number of candidate (split) nodes this round
         if (phase == 1) {
-            // split set = nodes with more than one key, ranked in list order
-            for (int p = tid; p < L; p += QT_NT) scan[p] = cntc[p] > 1 ? 1u : 0u;
-            __syncthreads();
-            S = (int)block_scan_excl<QT_NT>(scan, L, wsum);
+            S = (int)block_scan_fn<QT_NT>(scan, L, wsum, [&](int p) { return cntc[p] > 1 ? 1u : 0u; });
             for (int p = tid; p < L; p += QT_NT) {
+                const int sp = (int)scan[p];
                 if (cntc[p] > 1) {
-                    const int s = (int)scan[p];
-                    srank[p] = (Ix)s;
-                    snode[s] = (Ix)p;
+                    set_split(sp, p);
                 } else {
                     srank[p] = kNoneI;
+                    sinfo[p] = 0u;
                 }
-                npos[p] = (Ix)(p - (int)scan[p]);   // rank among non-split nodes
+                npos[p] = (Ix)(p - sp);   // rank among non-split nodes
             }
         } else {
             // phase 2: sort vPrev by (size, creation) descending and split from the front.  The keys
             // are unique (creation index in the low bits), so an element's place is the number of
             // larger keys: every thread ranks its elements against the whole key array by broadcast
             // 16-byte reads, with one barrier in place of a bitonic network's log2(m)^2 / 2 stages.
-            m = sh[SH_M];
+            const int m = sh[SH_M];
             const int m4 = (m + 3) >> 2;
             for (int k = tid; k < 4 * m4; k += QT_NT) {
                 uint32_t key = 0u;   // 0: below every key
                 if (k < m) {
-                    const uint32_t c = cntc[vprev[k]];
+                    const uint32_t c = cntc[vin[k]];
                     key = (c << 16) | (uint32_t)k;
                     if (c > 0xFFFFu) sh[SH_BIG] = 1;   // the packed key would wrap (reset at the round's end)
                 }
                 skey[k] = key;
             }
-            for (int p = tid; p < L; p += QT_NT) srank[p] = kNoneI;
+            for (int p = tid; p < L; p += QT_NT) {
+                srank[p] = kNoneI;
+                sinfo[p] = 0u;
+            }
             __syncthreads();
-#ifdef ORBX_QT_PROF
-            long long qs = 0;
-            if (threadIdx.x == 0) qs = clock64();
-#endif
             if (sh[SH_BIG] == 0 && m <= 0x10000) {   // block-uniform
                 const uint4* k4 = (const uint4*)skey;
                 for (int k = tid; k < m; k += QT_NT) {
@@ -1233,113 +1356,99 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
                         const uint4 v = k4[i4];
                         j += (int)(v.x > key) + (int)(v.y > key) + (int)(v.z > key) + (int)(v.w > key);
                     }
-                    const int p = vprev[k];
-                    srank[p] = (Ix)j;
-                    snode[j] = (Ix)p;
+                    set_split(j, (int)vin[k]);
                 }
             } else {
                 // a node of more than 0xFFFF keys (huge levels with small budgets) or more than 2^16
                 // candidates: the same order, compared as (size, creation) pairs
                 for (int k = tid; k < m; k += QT_NT) {
-                    const uint32_t c = cntc[vprev[k]];
+                    const uint32_t c = cntc[vin[k]];
                     int j = 0;
                     for (int k2 = 0; k2 < m; ++k2) {
-                        const uint32_t c2 = cntc[vprev[k2]];
+                        const uint32_t c2 = cntc[vin[k2]];
                         j += (int)(c2 > c || (c2 == c && k2 > k));
                     }
-                    const int p = vprev[k];
-                    srank[p] = (Ix)j;
-                    snode[j] = (Ix)p;
+                    set_split(j, (int)vin[k]);
                 }
             }
-#ifdef ORBX_QT_PROF
-            if (threadIdx.x == 0) atomicAdd(&g_qt_prof[l][4], (unsigned long long)(clock64() - qs));
-#endif
             S = m;
         }
         __syncthreads();
-#ifdef ORBX_QT_PROF
-        QT_STAMP(3, qr);
-#endif
-        // midlines of candidate nodes (ExtractorNode::DivideNode, :572-573)
-        for (int s = tid; s < S; s += QT_NT) {
-            const int p = snode[s];
-            const int hx = (int)ceilf((float)(cx1[p] - cx0[p]) / 2);
-            const int hy = (int)ceilf((float)(cy1[p] - cy0[p]) / 2);
-            smx[s] = (int16_t)(cx0[p] + hx);
-            smy[s] = (int16_t)(cy0[p] + hy);
-            ccnt[4 * s] = ccnt[4 * s + 1] = ccnt[4 * s + 2] = ccnt[4 * s + 3] = 0;
-        }
-        __syncthreads();
-        // a keypoint's child slot 4 * split rank + quadrant is kept in the upper half of its node word
-        // for the relabel below (the lower half is the node's list position)
-        // (kG: node words hold the full position, and the relabel below recomputes the child slot;
-        // srank, smx and smy stay unchanged until then)
+        QT_STAMP(3, qt_t);
+
+        // ---- B: a keypoint's child slot is 4 * (its node's list position) + quadrant; the candidate flag
+        // and quadrant are kept in its node word beside the position for the relabel (bit 18, bits 16-17).
+        // kG: node words hold the full position, and the relabel recomputes the child slot (sinfo is
+        // unchanged until then).
         auto child_key = [&](uint32_t k, uint32_t d) {
-            const Ix sx = srank[d & kPosMask];
-            if (sx == kNoneI) return -1;
-            const int s = (int)sx;
-            const int x = (int)(k & 0xFFF), y = (int)((k >> 12) & 0xFFF);
-            return 4 * s + (x >= smx[s] ? 1 : 0) + (y >= smy[s] ? 2 : 0);
+            const uint32_t p = d & kPosMask;
+            const uint32_t w = sinfo[p];
+            if (!(w & 0x80000000u)) return -1;
+            const uint32_t x = k & 0xFFFu, y = (k >> 12) & 0xFFFu;
+            return (int)(4 * p + (x >= (w & 0xFFFu) ? 1u : 0u) + (y >= ((w >> 12) & 0xFFFu) ? 2u : 0u));
         };
+        if constexpr (!kG) {
+            // keys first (independent LDS loads of every register slot in flight together), then the
+            // counts: interleaved, each slot's loads would wait behind the previous slot's atomics
 #pragma unroll
-        for (int r = 0; r < QT_KPT; ++r) {
-            if (wave_i0 + r * QT_NT >= n) break;   // wave-uniform
-            const int i = tid + r * QT_NT;
-            const int key = i < n ? child_key(kp[r], nd[r]) : -1;
-            if constexpr (!kG) nd[r] = (nd[r] & 0xFFFFu) | ((uint32_t)(key + 1) << 16);
-            wave_run_add(ccnt, key);
+            for (int r = 0; r < QT_KPT; ++r) {
+                const int i = tid + r * QT_NT;
+                const int key = i < n ? child_key(kpr(r), nd[r]) : -1;
+                nd[r] = (nd[r] & 0xFFFFu) | (key >= 0 ? 0x40000u | ((uint32_t)(key & 3) << 16) : 0u);
+            }
+#pragma unroll
+            for (int r = 0; r < QT_KPT; ++r) {
+                if (wave_i0 + r * QT_NT >= n) break;   // wave-uniform
+                wave_run_add(ccnt, (nd[r] & 0x40000u) ? (int)(4 * (nd[r] & 0xFFFFu) + ((nd[r] >> 16) & 3u)) : -1);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < QT_KPT; ++r) {
+                if (wave_i0 + r * QT_NT >= n) break;   // wave-uniform
+                const int i = tid + r * QT_NT;
+                wave_run_add(ccnt, i < n ? child_key(kpr(r), nd[r]) : -1);
+            }
         }
         for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) {
             uint32_t& d = fspill_node[i - QT_NT * QT_KPT];
             const int key = child_key(fspill[i - QT_NT * QT_KPT], d);
-            if constexpr (!kG) d = (d & 0xFFFFu) | ((uint32_t)(key + 1) << 16);
+            if constexpr (!kG) d = (d & 0xFFFFu) | (key >= 0 ? 0x40000u | ((uint32_t)(key & 3) << 16) : 0u);
             if (key >= 0) atomicAdd(&ccnt[key], 1u);
         }
+        if (tid == 0) sh[SH_KK] = S;   // phase 2: lowered in step C by the split that reaches N
         __syncthreads();
-#ifdef ORBX_QT_PROF
-        QT_STAMP(9, qr);
-#endif
+        QT_STAMP(9, qt_t);
 
-        // how many candidates are actually split (phase 2 stops once size >= N)
-        int kk = S;
-        if (phase == 2) {
-            for (int j = tid; j < S; j += QT_NT) {
-                int cs = 0;
-                for (int q = 0; q < 4; ++q) cs += ccnt[4 * j + q] > 0;
-                scan[j] = (uint32_t)cs;   // delta + 1
+        // ---- C: children (low half) and expandable children (high half) per split rank ----
+        auto kids = [&](int s) -> uint32_t {
+            const int p = snode[s];
+            uint32_t v = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = ccnt[4 * p + q];
+                v += (c > 0 ? 1u : 0u) + (c > 1 ? 0x10000u : 0u);
             }
-            if (tid == 0) sh[SH_KK] = S;
-            __syncthreads();
-            block_scan_excl<QT_NT>(scan, S, wsum);
+            return v;
+        };
+        const uint32_t T = block_scan_fn<QT_NT>(scan, S, wsum, kids);
+        int kk = S;
+        uint32_t pre = T;   // prefix at kk
+        if (phase == 2) {
+            // how many candidates are actually split: the size after splitting j grows with j (a split
+            // node leaves >= 1 child), so the one j that crosses N writes
             for (int j = tid; j < S; j += QT_NT) {
-                int cs = 0;
-                for (int q = 0; q < 4; ++q) cs += ccnt[4 * j + q] > 0;
-                const int run = L + (int)scan[j] + cs - (j + 1);   // size after splitting j
-                // run grows with j (a split node leaves >= 1 child): the one j that crosses N writes
-                if (run >= N && L + (int)scan[j] - j < N) sh[SH_KK] = j + 1;
+                const int cs = (int)(kids(j) & 0xFFFFu), sj = (int)(scan[j] & 0xFFFFu);
+                if (L + sj + cs - (j + 1) >= N && L + sj - j < N) sh[SH_KK] = j + 1;
             }
             __syncthreads();
             kk = sh[SH_KK];
-            // non-split rank of every current node
-            for (int p = tid; p < L; p += QT_NT) scan[p] = (srank[p] != kNoneI && (int)srank[p] < kk) ? 1u : 0u;
-            __syncthreads();
-            block_scan_excl<QT_NT>(scan, L, wsum);
-            for (int p = tid; p < L; p += QT_NT) npos[p] = (Ix)(p - (int)scan[p]);
-            __syncthreads();
+            if (kk < S) pre = scan[kk];
+            block_scan_fn<QT_NT>(scan2, L, wsum, [&](int p) {
+                return (srank[p] != kNoneI && (int)srank[p] < kk) ? 1u : 0u;
+            });
         }
-#ifdef ORBX_QT_PROF
-        QT_STAMP(10, qr);
-#endif
-
-        // children: count and exclusive offsets over split ranks 0..kk-1
-        for (int s = tid; s < kk; s += QT_NT) {
-            int cs = 0;
-            for (int q = 0; q < 4; ++q) cs += ccnt[4 * s + q] > 0;
-            scan[s] = (uint32_t)cs;
-        }
-        __syncthreads();
-        const int Ctot = (int)block_scan_excl<QT_NT>(scan, kk, wsum);
+        QT_STAMP(10, qt_t);
+        const int Ctot = (int)(pre & 0xFFFFu), nexp = (int)(pre >> 16);
         const int newL = Ctot + (L - kk);
         if (newL > lcap) {
             if (tid == 0) {
@@ -1348,86 +1457,81 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
             }
             continue;
         }
+
+        // ---- D ----
         for (int s = tid; s < kk; s += QT_NT) {
             const int p = snode[s];
+            const uint32_t ps = scan[s];
+            uint32_t c4[4];
             int cs = 0;
-            for (int q = 0; q < 4; ++q) cs += ccnt[4 * s + q] > 0;
-            const int pos0 = Ctot - (int)scan[s] - cs;   // later splits are pushed in front
-            const int mx = smx[s], my = smy[s];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c4[q] = ccnt[4 * p + q];
+                cs += c4[q] > 0;
+            }
+            const int pos0 = Ctot - (int)(ps & 0xFFFFu) - cs;   // later splits are pushed in front
+            int e = (int)(ps >> 16);
+            const uint32_t w = sinfo[p];
+            const int mx = (int)(w & 0xFFFu), my = (int)((w >> 12) & 0xFFFu);
             const int x0 = cx0[p], x1 = cx1[p], y0 = cy0[p], y1 = cy1[p];
-            int j = 0;
-            for (int q = 3; q >= 0; --q) {
-                const uint32_t c = ccnt[4 * s + q];
-                if (c == 0) {
-                    cpos[4 * s + q] = kNoneI;
-                    continue;
-                }
-                const int np = pos0 + j++;
-                cpos[4 * s + q] = (Ix)np;
+            int np = pos0 + cs;   // n1 lands last (it was pushed first)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = c4[q];
+                if (c == 0) continue;   // (no keypoint looks its slot up)
+                --np;
+                cpos[4 * p + q] = (Ix)np;
                 nx0[np] = (int16_t)((q & 1) ? mx : x0);
                 nx1[np] = (int16_t)((q & 1) ? x1 : mx);
                 ny0[np] = (int16_t)((q & 2) ? my : y0);
                 ny1[np] = (int16_t)((q & 2) ? y1 : my);
                 cntn[np] = c;
+                if (c > 1) vout[e++] = (Ix)np;   // creation order: split rank, then n1..n4
             }
         }
         for (int p = tid; p < L; p += QT_NT) {
             const bool split = srank[p] != kNoneI && (int)srank[p] < kk;
             if (!split) {
-                const int np = Ctot + (int)npos[p];
+                const int np = Ctot + (phase == 1 ? (int)npos[p] : p - (int)scan2[p]);
                 npos[p] = (Ix)np;
                 nx0[np] = cx0[p];
                 nx1[np] = cx1[p];
                 ny0[np] = cy0[p];
                 ny1[np] = cy1[p];
                 cntn[np] = cntc[p];
+                // a phase-2 candidate past kk keeps its keypoints: its child slots all lead to its new place
+                if (srank[p] != kNoneI) cpos[4 * p] = cpos[4 * p + 1] = cpos[4 * p + 2] = cpos[4 * p + 3] = (Ix)np;
             }
         }
-        __syncthreads();
-#ifdef ORBX_QT_PROF
-        QT_STAMP(11, qr);
-#endif
-        // new expandable children in creation order (split rank, then n1..n4)
-        for (int e = tid; e < 4 * kk; e += QT_NT) scan[e] = ccnt[e] > 1 ? 1u : 0u;
-        __syncthreads();
-        const int nexp = (int)block_scan_excl<QT_NT>(scan, 4 * kk, wsum);
-        for (int e = tid; e < 4 * kk; e += QT_NT)
-            if (ccnt[e] > 1) vnew[scan[e]] = cpos[e];   // (Ix)
-        // relabel keypoints with their new list position
-        visit([&](uint32_t& k, uint32_t& d, int) {
-            // child slot from the count pass, -1 if the node was not a candidate
-            const int ck = kG ? child_key(k, d) : (int)(d >> 16) - 1;
-            d = (ck >= 0 && (ck >> 2) < kk) ? (uint32_t)cpos[ck] : (uint32_t)npos[d & kPosMask];
-        });
-        __syncthreads();
-#ifdef ORBX_QT_PROF
-        QT_STAMP(12, qr);
-#endif
         if (tid == 0) {
-            // src/ORBextractor.cc:793-803 and :871-872
+            // src/ORBextractor.cc:793-803 and :871-872 (read at the next round's start)
             sh[SH_L] = newL;
             if (newL >= N || newL == L) {
                 sh[SH_DONE] = 1;
             } else if (phase == 1) {
-                if (newL + 3 * nexp > N) {
-                    sh[SH_PHASE] = 2;
-                }
+                if (newL + 3 * nexp > N) sh[SH_PHASE] = 2;
             }
             sh[SH_M] = nexp;
             sh[SH_BIG] = 0;
         }
-        // vnew -> vprev for the next round
-        for (int e = tid; e < nexp; e += QT_NT) vprev[e] = vnew[e];
-#ifdef ORBX_QT_PROF
-        QT_STAMP(13, qr);
-#endif
+        __syncthreads();
+        QT_STAMP(11, qt_t);
+
+        // ---- E: relabel keypoints with their new list position ----
+        visit([&](uint32_t& k, uint32_t& d, int) {
+            // child slot from the count pass, -1 if the node was not a candidate
+            const int ck = kG ? child_key(k, d) : (d & 0x40000u) ? (int)(4 * (d & 0xFFFFu) + ((d >> 16) & 3u)) : -1;
+            d = ck >= 0 ? (uint32_t)cpos[ck] : (uint32_t)npos[d & kPosMask];
+        });
+        QT_STAMP(12, qt_t);
         cur ^= 1;
     }
 
 #ifdef ORBX_QT_PROF
     // (the round loop's time: stamped at each round's end below would need the phase; charge the
     // whole loop to slot 2 and let the caller split it with the sort and round counts)
-    QT_STAMP(2, qt_t);
+    qt_acc[2] += (unsigned long long)(clock64() - qt_r0);
+    qt_t = clock64();
 #endif
     // ---- 4. retain the best keypoint per node (first max wins), :882-906 -----
     const int L = sh[SH_L];
@@ -1455,7 +1559,8 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
         qt_cnt[(size_t)f * G->nlevels + l] = outn;
 #ifdef ORBX_QT_PROF
         QT_STAMP(5, qt_t);
-        atomicAdd(&g_qt_prof[l][8], 1ull);
+        qt_acc[8] = 1;
+        for (int k = 0; k < 16; ++k) atomicAdd(&g_qt_prof[l][k], qt_acc[k]);
 #endif
         atomicAdd(&frame_counts[f], outn);
         int err = sh[SH_ERR];
@@ -1468,7 +1573,7 @@ template <int NT, int KPT, bool kG>
 static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
                       hipStream_t s)
 {
-    const size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap).total;
+    const size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap, 2, qt_kpn(NT, KPT, 0)).total;
     hipFuncSetAttribute((const void*)k_quadtree<NT, KPT, kG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_quadtree<NT, KPT, kG>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
                        b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt, frame_counts,
@@ -1497,7 +1602,7 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
     if (batch <= kQtMergedMaxBatch && !anyg) {
         QtGroup q{0, g.nlevels, 512, g.qt_kpt0, 0, 0, 0};
         caps(q);
-        if (qt_layout(q.lcap, q.cellcap).total <= kQtLdsMax) {
+        if (qt_layout(q.lcap, q.cellcap, 2, qt_kpn(q.nt, q.kpt, 0)).total <= kQtLdsMax) {
             out[0] = q;
             return 1;
         }
@@ -1522,7 +1627,8 @@ bool qt_prepare(Geometry& g)
     // a level's own node list decides; a group whose shared capacity outgrows LDS moves to global too
     for (int l = 0; l < g.nlevels; ++l) {
         const int lc = g.lv[l].cap + 4;
-        g.lv[l].qt_glob = lc > kQtLdsMaxList || qt_layout(lc, g.lv[l].ncells).total > kQtLdsMax;
+        const int kpn = qt_kpn(l == 0 ? 512 : 256, l == 0 ? g.qt_kpt0 : 4, 0);
+        g.lv[l].qt_glob = lc > kQtLdsMaxList || qt_layout(lc, g.lv[l].ncells, 2, kpn).total > kQtLdsMax;
         g.lv[l].qtg_off = g.lv[l].qtg_bytes = 0;
     }
     QtGroup grp[kQtMaxGroups];
@@ -1530,7 +1636,8 @@ bool qt_prepare(Geometry& g)
         const int ng = qt_plan(g, 1 << 30, grp);
         bool moved = false;
         for (int i = 0; i < ng; ++i) {
-            if (grp[i].glob || qt_layout(grp[i].lcap, grp[i].cellcap).total <= kQtLdsMax) continue;
+            if (grp[i].glob || qt_layout(grp[i].lcap, grp[i].cellcap, 2, qt_kpn(grp[i].nt, grp[i].kpt, 0)).total <= kQtLdsMax)
+                continue;
             for (int l = grp[i].l0; l < grp[i].l0 + grp[i].nl; ++l) g.lv[l].qt_glob = 1;
             moved = true;
         }
@@ -1766,20 +1873,35 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
 #pragma unroll
     for (int it = 0; it < 3; ++it) bitem[it] = c_blur_items[lane + 64 * it];
 
-    // output index g (level-major, as the reference concatenates levels) -> level, keypoint.
-    // The wave's indices are consecutive, so past the frame's total the rest are too.
-    auto lookup = [&](int g, int& l, uint32_t& pk) -> bool {
-        int base = 0;
-        for (l = 0; l < L; ++l) {
+    // output index g (level-major, as the reference concatenates levels) -> level, keypoint: lane j < kpw
+    // looks up the wave's keypoint j once, up front, so no keypoint waits for its packed entry's global load
+    // before its patch DMA can go out.  The wave's indices are consecutive, so past the frame's total (or
+    // the output capacity) the rest are too, and the valid lanes are a prefix.
+    int my_l = 0;
+    uint32_t my_pk = 0;
+    bool my_ok = false;
+    if (lane < kpw) {
+        const int g = g0 + lane;
+        int base = 0, l = 0;
+        for (; l < L; ++l) {
             if (g < base + cnts[l]) break;
             base += cnts[l];
         }
-        if (l == L) return false;
-        if (g >= cap) {
-            if (lane == 0) atomicOr(status, (int)kStatusCapOverflow);
-            return false;
+        if (l < L) {
+            if (g >= cap) {
+                atomicOr(status, (int)kStatusCapOverflow);
+            } else {
+                my_ok = true;
+                my_l = l;
+                my_pk = qt_out[(size_t)f * G->out_per_frame + G->lv[l].out_off + (g - base)];
+            }
         }
-        pk = qt_out[(size_t)f * G->out_per_frame + G->lv[l].out_off + (g - base)];
+    }
+    const int nkp = __builtin_popcountll(__ballot(my_ok));
+    auto lookup = [&](int jj, int& l, uint32_t& pk) -> bool {
+        if (jj >= nkp) return false;
+        l = __builtin_amdgcn_readlane(my_l, jj);
+        pk = (uint32_t)__builtin_amdgcn_readlane((int)my_pk, jj);
         return true;
     };
     // raw patch rows cy-21..cy+21 from column cx-21 (48 bytes used per row); sets the
@@ -1834,7 +1956,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
 
     int nl = 0, sb = 0, sp = 0;
     uint32_t npk = 0;
-    bool nvalid = lookup(g0, nl, npk);
+    bool nvalid = lookup(0, nl, npk);
     if (nvalid) fill(nl, npk, sb, sp);
     // The wave's outputs stay in LDS until its last keypoint (s_out: 8 descriptor dwords per keypoint, then
     // 7 cv::KeyPoint dwords per keypoint).  A global store inside the loop would make the next keypoint's
@@ -1902,7 +2024,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
         }
         wave_lds_sync();   // raw is free: start the next keypoint's patch, it lands under BRIEF
-        nvalid = jj + 1 < kpw && lookup(oidx + 1, nl, npk);
+        nvalid = lookup(jj + 1, nl, npk);
         if (nvalid) fill(nl, npk, sb, sp);
 
         // rBRIEF with the reference's contracted FMAs; blur evaluated at each sample point

@@ -22,9 +22,10 @@ for it in range(4):
     if it == 0:
         fn(buf.ctypes.data, 1)
 fn(buf.ctypes.data, 0)
-names = ["gather", "init", "rounds", "splitset", "p2sort", "retain", "#p1", "#p2", "#wg", "mid+cnt", "p2kk",
-         "children", "exp+relab", "tail"]
+# round steps (csrc/orbx_extract.hip k_quadtree): A split set + midlines, B count pass, C scans (+ phase-2
+# kk), D new list, E relabel; gather = g.scan (cell counts loaded and scanned) + g.copy (candidates to registers)
+names = ["gather", "init", "rounds", "A", "g.scan", "retain", "#p1", "#p2", "#wg", "B", "C", "D", "E", "g.copy", "g.owner", "g.load"]
 print("level  " + " ".join("%9s" % n for n in names))
 for l in range(8):
     wg = max(int(buf[l, 8]), 1)
-    print("%5d  " % l + " ".join("%9.0f" % (buf[l, k] / wg) for k in range(14)))
+    print("%5d  " % l + " ".join("%9.0f" % (buf[l, k] / wg) for k in range(16)))
