@@ -222,11 +222,15 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
 // (src/ORBextractor.cc:982-987).  Survivors are emitted row-major, i.e. in
 // OpenCV's emission order.
 // ---------------------------------------------------------------------------
-// The ROI tile holds every pixel x as the f16 h = 1024 + x (bit pattern 0x6400 | x: integers in
-// [1024, 2048) are exact f16 values with unit spacing), 2 bytes per pixel.  Each ring value enters the
-// arithmetic as the packed pair (h, -h): the compiler folds that into the first packed instruction's
-// source modifiers (op_sel_hi = 0, neg_hi), so it costs nothing, and packed f16 max/min/sub are then exact
-// integer ops on both polarities at once.  gfx950's v_pk_maximum3_f16 / v_pk_minimum3_f16 take three
+// The ROI tile holds the pixel bytes x, one byte per pixel.  A byte read into the low half of a VGPR
+// (ds_read_u8_d16) is the f16 bit pattern of the denormal x * 2^-24: denormals are exact fixed-point
+// values (the kernels run with f16 denormals preserved, .amdhsa_float_denorm_mode_16_64 3), so f16
+// max/min/sub/compare on them are exact integer operations, and a non-negative result's bit pattern is
+// its integer value.  Each ring value enters the arithmetic as the packed pair (h, -h): the compiler
+// folds that into the first packed instruction's source modifiers (op_sel_hi = 0, neg_hi), so it costs
+// nothing, and packed f16 max/min/sub work on both polarities at once.  (Round 2 stored 0x6400 | x, the
+// normal f16 1024 + x, 2 bytes per pixel: the byte tile halves the tile's LDS and its commit is one
+// alignbyte and one 4-byte store per pass.)  gfx950's v_pk_maximum3_f16 / v_pk_minimum3_f16 take three
 // operands: a 9-arc max of the pairs is the "brighter" arc value and, in the other half, minus the 9-arc
 // min ("darker").
 typedef _Float16 fh2 __attribute__((ext_vector_type(2)));
@@ -236,6 +240,9 @@ __device__ __forceinline__ fh2 pmax2(fh2 a, fh2 b) { return __builtin_elementwis
 __device__ __forceinline__ fh2 pmin2(fh2 a, fh2 b) { return __builtin_elementwise_minimum(a, b); }
 __device__ __forceinline__ fh2 pmax3(fh2 a, fh2 b, fh2 c) { return pmax2(pmax2(a, b), c); }
 __device__ __forceinline__ fh2 pmin3(fh2 a, fh2 b, fh2 c) { return pmin2(pmin2(a, b), c); }
+// pixel byte as the f16 denormal x * 2^-24; an integer threshold likewise
+__device__ __forceinline__ _Float16 px16(const uint8_t* p) { return __builtin_bit_cast(_Float16, (uint16_t)*p); }
+__device__ __forceinline__ _Float16 int16_as_f16(int t) { return __builtin_bit_cast(_Float16, (uint16_t)t); }
 __device__ __forceinline__ fh2 dup_neg(_Float16 h)
 {
     fh2 r;
@@ -248,7 +255,7 @@ __device__ __forceinline__ fh2 dup_neg(_Float16 h)
 // and neighbour access is one base register plus an immediate LDS offset (no per-access address
 // arithmetic).  40 covers the ROIs of every BASELINE configuration (37-38 px); 68 the 66-px cap.
 __host__ __device__ constexpr int fast_tile_pitch(int max_roi_w) { return max_roi_w <= 40 ? 40 : 68; }
-// per-wave LDS: ROI tile [rh][TP] f16 values, zero-bordered strength map [rh - 4][TP] bytes (the
+// per-wave LDS: ROI tile [rh][TP] bytes, zero-bordered strength map [rh - 4][TP] bytes (the
 // detection window plus a one-pixel frame, at the tile's pitch so a map index is a tile index minus a
 // constant), and the candidate list (u16 tile indices) of the largest window, filled from both ends
 __host__ __device__ inline size_t fast_map_bytes(int rw, int rh)
@@ -263,32 +270,32 @@ constexpr int kFastObCap = 128;
 __host__ __device__ inline size_t fast_list_bytes(int rw, int rh) { return (2 * (size_t)fast_list_cap(rw, rh) + 3) & ~(size_t)3; }
 __host__ __device__ inline size_t fast_wave_bytes(int rw, int rh)
 {
-    const size_t tile = (size_t)2 * rh * fast_tile_pitch(rw);
+    const size_t tile = (size_t)rh * fast_tile_pitch(rw);
     return (tile + fast_map_bytes(rw, rh) + fast_list_bytes(rw, rh) + 4 * kFastObCap + 15) & ~(size_t)15;
 }
 
 // max(v - minMax, maxMin - v) over the 16 cyclic 9-arcs of the Bresenham ring of the
-// pixel at tile value c[0]
+// pixel at tile byte c[0]
 template <int TP>
-__device__ __forceinline__ int fast_strength(const _Float16* c)
+__device__ __forceinline__ int fast_strength(const uint8_t* c)
 {
     fh2 x[16];
-    x[0] = dup_neg(c[3 * TP]);
-    x[1] = dup_neg(c[3 * TP + 1]);
-    x[2] = dup_neg(c[2 * TP + 2]);
-    x[3] = dup_neg(c[TP + 3]);
-    x[4] = dup_neg(c[3]);
-    x[5] = dup_neg(c[-TP + 3]);
-    x[6] = dup_neg(c[-2 * TP + 2]);
-    x[7] = dup_neg(c[-3 * TP + 1]);
-    x[8] = dup_neg(c[-3 * TP]);
-    x[9] = dup_neg(c[-3 * TP - 1]);
-    x[10] = dup_neg(c[-2 * TP - 2]);
-    x[11] = dup_neg(c[-TP - 3]);
-    x[12] = dup_neg(c[-3]);
-    x[13] = dup_neg(c[TP - 3]);
-    x[14] = dup_neg(c[2 * TP - 2]);
-    x[15] = dup_neg(c[3 * TP - 1]);
+    x[0] = dup_neg(px16(c + 3 * TP));
+    x[1] = dup_neg(px16(c + 3 * TP + 1));
+    x[2] = dup_neg(px16(c + 2 * TP + 2));
+    x[3] = dup_neg(px16(c + TP + 3));
+    x[4] = dup_neg(px16(c + 3));
+    x[5] = dup_neg(px16(c - TP + 3));
+    x[6] = dup_neg(px16(c - 2 * TP + 2));
+    x[7] = dup_neg(px16(c - 3 * TP + 1));
+    x[8] = dup_neg(px16(c - 3 * TP));
+    x[9] = dup_neg(px16(c - 3 * TP - 1));
+    x[10] = dup_neg(px16(c - 2 * TP - 2));
+    x[11] = dup_neg(px16(c - TP - 3));
+    x[12] = dup_neg(px16(c - 3));
+    x[13] = dup_neg(px16(c + TP - 3));
+    x[14] = dup_neg(px16(c + 2 * TP - 2));
+    x[15] = dup_neg(px16(c + 3 * TP - 1));
     fh2 m3[16], a[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) m3[k] = pmax3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
@@ -297,8 +304,9 @@ __device__ __forceinline__ int fast_strength(const _Float16* c)
     const fh2 b0 = pmin3(a[0], a[1], a[2]), b1 = pmin3(a[3], a[4], a[5]), b2 = pmin3(a[6], a[7], a[8]);
     const fh2 b3 = pmin3(a[9], a[10], a[11]), b4 = pmin3(a[12], a[13], a[14]);
     const fh2 mm = pmin3(pmin3(b0, b1, b2), pmin2(b3, b4), a[15]);   // (minMax, -maxMin)
-    const fh2 d = dup_neg(c[0]) - mm;                                 // (v - minMax, maxMin - v)
-    return (int)__builtin_fmaxf16(d.x, d.y);
+    const fh2 d = dup_neg(px16(c)) - mm;   // (v - minMax, maxMin - v)
+    // the integer value of a non-negative result; a negative one reads as a negative int16 (not a corner)
+    return (int)__builtin_bit_cast(int16_t, __builtin_fmaxf16(d.x, d.y));
 }
 
 // Compass value q of the pixel at c[0]: a 9-arc holds two consecutive compass points (ring positions
@@ -307,11 +315,12 @@ __device__ __forceinline__ int fast_strength(const _Float16* c)
 // (N, E, S, W) the largest pair minimum is min(max(N, S), max(E, W)): each consecutive pair holds one of
 // {N, S} and one of {E, W}, and the larger of N, S forms a pair with each of E, W.  Three packed ops.
 template <int TP>
-__device__ __forceinline__ _Float16 fast_compass_q(const _Float16* c)
+__device__ __forceinline__ _Float16 fast_compass_q(const uint8_t* c)
 {
-    const fh2 a = dup_neg(c[3 * TP]), b = dup_neg(c[3]), d = dup_neg(c[-3 * TP]), e = dup_neg(c[-3]);
+    const fh2 a = dup_neg(px16(c + 3 * TP)), b = dup_neg(px16(c + 3)), d = dup_neg(px16(c - 3 * TP)),
+              e = dup_neg(px16(c - 3));
     const fh2 m = pmin2(pmax2(a, d), pmax2(b, e));   // (br, -dk)
-    const fh2 q = m - dup_neg(c[0]);                                                 // (br - v, v - dk)
+    const fh2 q = m - dup_neg(px16(c));              // (br - v, v - dk)
     return __builtin_fmaxf16(q.x, q.y);   // one v_max_f16 (SDWA high-half operand)
 }
 
@@ -378,13 +387,12 @@ __device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneM
     }
 }
 
-// 4 pixels of ROI row r from column 4 kl as f16 (0x6400 | x): the lane's dword and its neighbour's
-// realigned by the row's byte shift (v_alignbyte uses the shift's low two bits, so the shift of pass u
-// is the lane's first one plus a uniform step), two v_perm (bytes 0, 1 and 2, 3 into the low bytes of
-// two halves) and two ors, one 8-byte LDS store at an immediate offset per pass
+// 4 pixels of ROI row r from column 4 kl: the lane's dword and its neighbour's realigned by the row's
+// byte shift (v_alignbyte uses the shift's low two bits, so the shift of pass u is the lane's first one
+// plus a uniform step), one 4-byte LDS store at an immediate offset per pass
 template <int TP, int LD>
 __device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const FastCellSrc& S,
-                                            const FastLaneMap<TP>& M, int u0, _Float16* tile)
+                                            const FastLaneMap<TP>& M, int u0, uint8_t* tile)
 {
     constexpr int kRPP = FastLaneMap<TP>::kRPP;
     const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
@@ -392,17 +400,12 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const Fas
     const int row0 = u0 * kRPP + M.rl;
     const uint32_t sh0 = s0 + (uint32_t)__mul24(row0, S.pitch);
     const uint32_t dsh = (uint32_t)__mul24(kRPP, S.pitch);
-    _Float16* dst = tile + row0 * TP + 4 * M.kl;
+    uint8_t* dst = tile + row0 * TP + 4 * M.kl;
 #pragma unroll
     for (int u = 0; u < LD; ++u) {
         const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)F.w[u], 0x130, 0xF, 0xF, false);   // wave_shl:1
-        if (lane_ok && row0 + u * kRPP < S.rh) {
-            const uint32_t w = __builtin_amdgcn_alignbyte(hi, F.w[u], sh0 + (uint32_t)u * dsh);
-            uint2 q;
-            q.x = __builtin_amdgcn_perm(0u, w, 0x0C010C00u) | 0x64006400u;
-            q.y = __builtin_amdgcn_perm(0u, w, 0x0C030C02u) | 0x64006400u;
-            *(uint2*)(dst + u * kRPP * TP) = q;
-        }
+        if (lane_ok && row0 + u * kRPP < S.rh)
+            *(uint32_t*)(dst + u * kRPP * TP) = __builtin_amdgcn_alignbyte(hi, F.w[u], sh0 + (uint32_t)u * dsh);
     }
 }
 
@@ -455,8 +458,8 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     const int c0 = cb + (lb - f * gridDim.x) * cpw;
     const int c1 = min(c0 + cpw, ce);
     if (c0 >= c1) return;   // wave-uniform; no block barriers below
-    _Float16* tile = (_Float16*)s_fast;
-    uint8_t* map = (uint8_t*)(tile + (size_t)rh * TP);
+    uint8_t* tile = s_fast;
+    uint8_t* map = tile + (size_t)rh * TP;
     uint16_t* list = (uint16_t*)(map + fast_map_bytes(rw, rh));
     uint32_t* obuf = (uint32_t*)((uint8_t*)list + fast_list_bytes(rw, rh));
     const int lcap = fast_list_cap(rw, rh);
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     unsigned long long* kept = (unsigned long long*)tile;
     const int t_ini = G->ini_th, t_min = G->min_th;
     const int t_lo = min(t_ini, t_min);
-    const _Float16 f_hi = (_Float16)t_ini, f_lo = (_Float16)t_lo;
+    const _Float16 f_hi = int16_as_f16(t_ini), f_lo = int16_as_f16(t_lo);   // thresholds as denormals
 #ifdef ORBX_FAST_PROF
     long long fp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long fp_t = clock64();
@@ -748,15 +751,21 @@ extern "C" int orbx_debug_fast_prof(unsigned long long* out, int reset)
 namespace orbx {
 #endif
 
-// LDS per CU on gfx950: the occupancy a FAST launch's per-wave tiles allow
+// LDS per CU on gfx950: the occupancy a FAST launch's per-wave tiles allow, up to what the kernel's
+// registers allow (80 VGPRs: 6 waves per SIMD, 24 one-wave workgroups per CU)
 constexpr size_t kLdsPerCu = 160 * 1024;
-static int fast_blocks_per_cu(int w, int h) { return (int)(kLdsPerCu / fast_wave_bytes(w, h)); }
+constexpr int kFastVgprWavesPerCu = 24;
+static int fast_blocks_per_cu(int w, int h)
+{
+    return std::min((int)(kLdsPerCu / fast_wave_bytes(w, h)), kFastVgprWavesPerCu);
+}
 
 void fast_groups(Geometry& g)
 {
-    // The longest prefix of levels whose largest ROI keeps level 0's occupancy is launch 0;
-    // the remaining levels (KITTI 1241x376: levels 4-7, ROIs up to 38x46 against 38x39) are
-    // launch 1.  Cells are stored level by level, so each launch is a contiguous range.
+    // The longest prefix of levels whose largest ROI keeps level 0's occupancy is launch 0; the
+    // remaining levels are launch 1.  Cells are stored level by level, so each launch is a contiguous
+    // range.  With the byte tile every KITTI level's ROI (up to 38x46) fits the register-limited 6 waves
+    // per SIMD, so KITTI runs one launch.
     int w = g.lv[0].roi_mw, h = g.lv[0].roi_mh, split = g.nlevels;
     const int occ0 = fast_blocks_per_cu(std::max(w, 8), std::max(h, 8));
     for (int l = 1; l < g.nlevels; ++l) {
