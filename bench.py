@@ -399,12 +399,13 @@ def main():
         "describe": B * (sum(A) + kept * (4 + 60)),
         "match": (B - 1) * 2 * kept * 60,
     }
+    n_launch = ex.debug_launches(H, W, B)
     def roofline(st):
         dom = max(st, key=lambda k: st[k])
         # several launches of one kernel per stage: per-launch figures are stage / launches,
-        # like rocprofv3's per-kernel average (FAST: two LDS classes of cells on config 2,
-        # levels 0-3 and 4-7, orbx_extract.hip fast_groups)
-        launches = {"pyramid": NLEVELS - 1, "fast": 2}.get(dom, 1)
+        # like rocprofv3's per-kernel average (the library reports its launch plan for this batch:
+        # pyramid one per level, FAST one per LDS class of cells, orbx_extract.hip fast_groups)
+        launches = {"pyramid": n_launch["pyramid"], "fast": n_launch["fast"]}.get(dom, 1)
         t_launch = st[dom] / launches * 1e-3
         achieved = alg[dom] / launches / t_launch / 1e9
         kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree<512,16|512,8|256,4>",

@@ -532,6 +532,21 @@ int orbx_capacity(const orbx_handle* h, int rows, int cols)
     return m->geom.out_per_frame;
 }
 
+orbx_status orbx_debug_launches(orbx_handle* h, int rows, int cols, int batch, int* counts, int n)
+{
+    if (!h || !counts || n < 1 || batch < 1) return ORBX_EINVAL;
+    DeviceGuard guard(h->device);
+    const orbx_status st = ensure_geometry(h, rows, cols);
+    if (st != ORBX_OK) return st;
+    const Geometry& g = h->geom;
+    int fast = 0;
+    for (int i = 0; i < g.fast_groups; ++i) fast += g.fast_cb[i + 1] > g.fast_cb[i];
+    QtGroup grp[kQtMaxGroups];
+    const int c[4] = {g.nlevels - 1, fast, qt_plan(g, batch, grp), 1};
+    for (int i = 0; i < n; ++i) counts[i] = i < 4 ? c[i] : 0;
+    return ORBX_OK;
+}
+
 orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols, size_t step, orbx_keypoint* kps,
                          int cap, uint8_t* desc, int* n_out)
 {

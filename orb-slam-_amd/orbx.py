@@ -34,7 +34,7 @@ TOP2, FULL_U16 = 0, 1
 EXPORTED = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_capacity", "orbx_extract", "orbx_get_level",
     "orbx_extract_batch_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
-    "orbx_debug_pyramid", "orbx_debug_candidates", "orbm_descriptor_distance", "orbm_allpairs_device", "orbm_allpairs",
+    "orbx_debug_pyramid", "orbx_debug_candidates", "orbx_debug_launches", "orbm_descriptor_distance", "orbm_allpairs_device", "orbm_allpairs",
     "orbm_search_init_batch_device", "orbm_search_for_initialization_device", "orbm_search_for_initialization",
     "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
     "orbm_bow_search_device", "orbm_bow_search",
@@ -169,6 +169,7 @@ def _load():
     L.orbx_get_stage_times.argtypes = [vp, f32p, C.c_int]
     L.orbx_debug_pyramid.argtypes = [vp, C.c_int, u8p, C.c_size_t]
     L.orbx_debug_candidates.argtypes = [vp, C.c_int, C.c_int, i32p, C.c_int, i32p]
+    L.orbx_debug_launches.argtypes = [vp, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
     L.orbm_descriptor_distance.argtypes = [u8p, u8p]
     L.orbm_allpairs_device.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]
     L.orbm_allpairs.argtypes = [C.c_int, u8p, C.c_int, u8p, C.c_int, C.c_int, vp, vp, vp, vp]
@@ -382,6 +383,13 @@ class ORBextractor:
                                                                   out.ctypes.data_as(C.POINTER(C.c_int)), cap,
                                                                   C.byref(n)))
         return out[:n.value].copy()
+
+    def debug_launches(self, rows, cols, batch):
+        """Kernel launches per stage of one batched extract: {pyramid, fast, quadtree, describe}."""
+        c = np.zeros(4, np.int32)
+        _check("orbx_debug_launches", lib.orbx_debug_launches(self._h, rows, cols, batch,
+                                                              c.ctypes.data_as(C.POINTER(C.c_int)), 4))
+        return dict(zip(("pyramid", "fast", "quadtree", "describe"), (int(v) for v in c)))
 
 
 def compute_stereo_matches(left, right, kps_l, desc_l, kps_r, desc_r, bf, fx):
