@@ -412,7 +412,18 @@ def main():
                  "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
         # stages made of several kernels: their per-launch counters add up
         PARTS = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"],
-                 "quadtree": ["k_quadtree<512, 16>", "k_quadtree<512, 8>", "k_quadtree<256, 4>"]}
+                 "quadtree": ["k_quadtree<512, 16", "k_quadtree<512, 8", "k_quadtree<256, 4"]}
+
+        def per_launch(K, dom, kname, field):
+            """A counter per launch from a per-kernel table keyed by full names (template arguments
+            included): a multi-kernel stage adds one launch of each part; otherwise the average per
+            dispatch over every template of the kernel."""
+            if dom in PARTS:
+                return sum(sum(K[k][field] for k in K if k == p or k.startswith(p + "<") or
+                               (p.endswith(tuple("0123456789")) and k.startswith(p + ","))) for p in PARTS[dom])
+            ks = [k for k in K if k == kname or k.startswith(kname + "<")]
+            nd = sum(K[k]["dispatches"] for k in ks)
+            return sum(K[k][field] * K[k]["dispatches"] for k in ks) / nd
         # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
         # same command (tools/collect_pmc.sh -> tools/pmc_summary.py); null when absent
         traffic = None
@@ -421,8 +432,7 @@ def main():
             try:
                 d = json.load(open(pmc))
                 if d.get("batch") == B:
-                    parts = PARTS.get(dom, [kname])
-                    traffic = int(sum(d["kernels"][k]["bytes_per_launch"] for k in parts))
+                    traffic = int(per_launch(d["kernels"], dom, kname, "bytes_per_launch"))
             except Exception:
                 traffic = None
         r = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -436,9 +446,7 @@ def main():
             try:
                 d = json.load(open(sq))
                 if d.get("batch") == B:
-                    parts = PARTS.get(dom, [kname])
-                    per = d["per_dispatch_averages"]
-                    ins = sum(per[k]["SQ_INSTS_VALU"] for k in parts)
+                    ins = per_launch(d["per_dispatch_averages"], dom, kname, "SQ_INSTS_VALU")
                     rate = ins / t_launch / 1e9
                     pk, pins, p2 = valu_peak(kname)
                     r["valu_issue"] = {
