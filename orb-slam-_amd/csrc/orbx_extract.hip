@@ -1739,6 +1739,9 @@ constexpr int kDescPerWave = ORBX_DESC_KPW;           // keypoints per wave (lan
 // and no wave waits on slower siblings (4 waves: 863 us per 384 frames, 2: 815, 1: 768; pipelined 169.1k ->
 // 176.4k frames/s)
 constexpr int kDescWaves = ORBX_DESC_WAVES;
+#ifndef ORBX_DESC_ICG
+#define ORBX_DESC_ICG 1   // IC_Angle and the angle's trigonometry once per wave (0: per keypoint, round 2)
+#endif
 
 // Horizontal-pass items (row pair rp << 8 | column group cg) that BRIEF can read: a sample
 // (18 + xx, 18 + yy) has |(x, y)| <= 18.39 before rounding (the pattern's largest radius), so a
@@ -1967,6 +1970,50 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     uint32_t npk = 0;
     bool nvalid = lookup(0, nl, npk);
     if (nvalid) fill(nl, npk, sb, sp);
+#if ORBX_DESC_ICG
+    // IC_Angle (src/ORBextractor.cc:84-128) of the wave's keypoints up front, from the level images in
+    // global memory: a keypoint lies >= 19 px inside its level (FAST's cell windows), so its radius-15 disc
+    // never leaves it (lanes 62-63 read row 16 with zero weights).  cv::fastAtan2 and sincosf then run
+    // once per wave with lane j on keypoint j, instead of once per keypoint on every lane (the angle was
+    // 17% of the launch).  Loads of every keypoint first, then the sums.
+    float kp_ang = 0.f, kp_cos = 1.f, kp_sin = 0.f;
+    if (nkp > 0) {
+        uint32_t q[kDescPerWave][5], qs[kDescPerWave];
+#pragma unroll
+        for (int jj = 0; jj < kDescPerWave; ++jj) {
+            const int jc = jj < nkp ? jj : nkp - 1;   // wave-uniform
+            const int l = __builtin_amdgcn_readlane(my_l, jc);
+            const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)my_pk, jc);
+            const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF);
+            int pitch;
+            const uint8_t* img = level_base(P, G, f, l, pitch);
+            const uintptr_t a = (uintptr_t)(img + (size_t)(cy + vrow) * pitch + (cx - 15 + 16 * ich));
+            const uint32_t* src = (const uint32_t*)(a & ~(uintptr_t)3);
+            qs[jj] = (uint32_t)(a & 3);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) q[jj][k] = src[k];
+        }
+        int m10 = 0, m01 = 0;
+#pragma unroll
+        for (int jj = 0; jj < kDescPerWave; ++jj) {
+            uint32_t s1 = 0u, s0 = 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(q[jj][k + 1], q[jj][k], qs[jj]);
+                s1 = __builtin_amdgcn_udot4(w, W1[k], s1, false);
+                s0 = __builtin_amdgcn_udot4(w, W0[k], s0, false);
+            }
+            const int x10 = wave_sum((int)s1 - 16 * (int)s0);
+            const int x01 = wave_sum(vrow * (int)s0);
+            if (lane == jj) {
+                m10 = x10;
+                m01 = x01;
+            }
+        }
+        kp_ang = fast_atan2_deg((float)m01, (float)m10);
+        glibc_sincosf_pair(kp_ang * kFactorPI, &kp_sin, &kp_cos);   // (src/ORBextractor.cc:148)
+    }
+#endif
     // The wave's outputs stay in LDS until its last keypoint (s_out: 8 descriptor dwords per keypoint, then
     // 7 cv::KeyPoint dwords per keypoint).  A global store inside the loop would make the next keypoint's
     // wait for its patch DMA (vmcnt counts loads and stores, completed in issue order) wait for the store's
@@ -1983,6 +2030,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this keypoint's DMA has landed
         wave_lds_sync();
 
+#if !ORBX_DESC_ICG
         // IC_Angle (src/ORBextractor.cc:84-128): integer moments over the disc, any order
         const int icb0 = raw_slot(ic_row) * kRawP + ((csb + ic_row * csp) & 3) + ic_col;
         const uint32_t* icq = raw32 + (icb0 >> 2);
@@ -1998,6 +2046,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         }
         const int m10 = wave_sum((int)s1 - 16 * (int)s0);
         const int m01 = wave_sum(vrow * (int)s0);
+#endif
 
         // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns.
         // Output column j of the realigned bytes R0 | R1 | R2 is sum_t w[t] * byte[j + t]: a dot4 of each
@@ -2008,6 +2057,9 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             {18u << 8 | 34u << 16 | 49u << 24, 55u | 49u << 8 | 34u << 16 | 18u << 24, 0u},
             {18u << 16 | 34u << 24, 49u | 55u << 8 | 49u << 16 | 34u << 24, 18u},
             {18u << 24, 34u | 49u << 8 | 55u << 16 | 49u << 24, 34u | 18u << 8}};
+#ifdef ORBX_DIAG_NOHPASS   // diagnostic build (wrong results): the horizontal pass's cost
+        if (lane < 32) rowT[lane * 23] = raw32[lane];
+#else
 #pragma unroll
         for (int it = 0; it < 3; ++it) {
             if (bitem[it] == 0xFFFF) break;
@@ -2032,15 +2084,25 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
 #pragma unroll
             for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
         }
+#endif
         wave_lds_sync();   // raw is free: start the next keypoint's patch, it lands under BRIEF
         nvalid = lookup(jj + 1, nl, npk);
         if (nvalid) fill(nl, npk, sb, sp);
 
         // rBRIEF with the reference's contracted FMAs; blur evaluated at each sample point
+#if ORBX_DESC_ICG
+        const float angle = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_ang), jj));
+        const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_cos), jj));
+        const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_sin), jj));
+#elif defined(ORBX_DIAG_NOTRIG)   // diagnostic build (wrong results): the angle's cost
+        const float angle = (float)m01 * 1e-3f;
+        const float a = (float)m10 * 1e-3f, b = angle;
+#else
         const float angle = fast_atan2_deg((float)m01, (float)m10);
         const float ang = angle * kFactorPI;
         float a, b;
         glibc_sincosf_pair(ang, &b, &a);   // a = cosf, b = sinf (src/ORBextractor.cc:148)
+#endif
         // GaussianBlur's u8 saturation: min(t0, 255) < min(t1, 255) iff t0 < min(t1, 255)
         unsigned long long words[4];
 #pragma unroll
