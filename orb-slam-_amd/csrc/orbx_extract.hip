@@ -1700,11 +1700,11 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 
 // ---------------------------------------------------------------------------
 // K4: a wave describes kDescPerWave consecutive retained keypoints.
-//   raw   the 43-row neighbourhood of the keypoint in LDS, 64 B per row.
-//         Interior keypoints arrive by LDS-DMA (global_load_lds_dword of 13
-//         aligned dwords per row, so row r starts at byte sh_r = (src +
-//         r*pitch) & 3 of its LDS row); border keypoints are filled with reflect-101 bytes
-//         at shift 0.  The next keypoint's DMA is issued as soon as the
+//   raw   the 43-row neighbourhood of the keypoint in LDS, 48 B per row.
+//         Interior keypoints arrive by LDS-DMA (global_load_lds_dwordx4: three
+//         instructions of 16-byte pieces, three per row, so row r starts at
+//         byte sh_r = (src + r*pitch) & 3 of its LDS row);
+//         border keypoints are filled with reflect-101 bytes at shift 0.  The next keypoint's DMA is issued as soon as the
 //         current one's raw reads are done, so it lands under the BRIEF work.
 //   angle IC_Angle: u*I and v*I over the 749-pixel disc as per-lane column
 //         sums (lane = disc column, half-wave = upper/lower rows), wave
@@ -1717,16 +1717,9 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 //   BRIEF fmaf sample coordinates, 256 tests -> four __ballot
 //         words = the descriptor's little-endian u64 words (:141-192).
 // ---------------------------------------------------------------------------
-constexpr int kRawD = 13;                             // dwords loaded per raw row: 48 B + shift slack
-constexpr int kRawP = 64;                             // LDS row pitch (bytes): 4 rows per 64-lane DMA
-constexpr int kRawRows = 44;                          // 43 rows used
+constexpr int kRawP = 48;                             // LDS row pitch (bytes): the 43 columns + shift slack
+constexpr int kRawRows = 44;                          // 43 rows used (row 43 repeats row 42)
 constexpr int kRawSlots = kRawRows * kRawP / 4;
-// LDS row slot of raw row r (an involution).  With a 16-dword pitch, rows 2 apart share their
-// banks; swapping rows 4k + 2 and 4k + 3 puts the even (odd) rows of consecutive row pairs on
-// alternate bank halves, which halves the horizontal pass's bank conflicts (208 -> 112 LDS cycles
-// per keypoint, tools/diag model).  The DMA applies it per lane for free: slot 4t + q holds row
-// 4t + (q ^ (q >> 1)).
-__host__ __device__ constexpr int raw_slot(int r) { return r ^ ((r >> 1) & 1); }
 constexpr int kTCols = 40, kTP = 22;                  // row-blurred, transposed: [col][row pairs], 22 dwords/col
 #ifndef ORBX_DESC_KPW
 #define ORBX_DESC_KPW 4
@@ -1928,40 +1921,41 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         // and only feed blurred columns BRIEF never samples (|x| <= 18 + the 3-tap reach).  About 2/3 of the
         // 6.5% of KITTI keypoints the reflect-101 byte path took before (13% of the describe launch).
         if (cx >= 21 && cy >= 21 && cy + 21 < h && (cx + 31 <= w || (cx + 21 < w && cy + 22 < h))) {
-            // DMA instruction t moves rows 4t..4t+3 (lane = 16 * row + dword; dwords 13..15
-            // repeat dword 12, row 43 repeats row 42).  Each row's aligned dwords start at or after the
-            // 4-byte aligned allocation.
+            // 16-byte piece c = 64 t + lane of DMA instruction t (global_load_lds_dwordx4: lane L's 16 bytes
+            // land at byte 16 L of the instruction's 1 KiB) is piece c % 3 of row c / 3, so three instructions
+            // fill rows 0..43 (the third with lanes 0..3 only; row 43 repeats row 42).  Each row's aligned
+            // bytes start at or after the 4-byte aligned allocation; a row reads 48 bytes from its aligned
+            // start, at most cx + 26 (inside the level row, or in the next row of the same level for the
+            // right-border case).  (Round 2: eleven 4-row global_load_lds_dword instructions into 64-byte
+            // rows, 2816 B; the 48-byte rows take the wave to 5.6 KB of LDS, 7 waves per SIMD.)
             const uintptr_t s0 = (uintptr_t)(img + (size_t)(cy - 21) * pitch + (cx - 21));
             const uint8_t* ub = (const uint8_t*)(s0 & ~(uintptr_t)3);   // wave-uniform, aligned
             sb = (int)(s0 & 3);
             sp = pitch & 3;
-            // slot row 4t + (lane >> 4) receives source row 4t + rr (raw_slot); row 43 (slot 42)
-            // repeats row 42
-            const int rr = raw_slot(lane >> 4), kk = min(lane & 15, kRawD - 1);
-            const uint32_t off = (uint32_t)((sb + rr * pitch) & ~3) + 4u * kk;
 #pragma unroll
-            for (int t = 0; t < kRawRows / 4; ++t) {
-                const uint32_t o = (t == kRawRows / 4 - 1 && rr == 3) ? off - (uint32_t)pitch : off;
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(ub + (size_t)(4 * t) * pitch + o),
-                    (__attribute__((address_space(3))) void*)(raw32 + 64 * t), 4, 0, 0);
+            for (int t = 0; t < 3; ++t) {
+                const int c = 64 * t + lane, row = c / 3, k = c - 3 * row;
+                if (t < 2 || lane < 4) {
+                    const uint32_t o = (uint32_t)((sb + min(row, 42) * pitch) & ~3) + 16u * (uint32_t)k;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ub + o),
+                                                     (__attribute__((address_space(3))) void*)(raw32 + 256 * t), 16, 0, 0);
+                }
             }
         } else {
             sb = 0;
             sp = 0;
-            // reflect-101 bytes, lane = column of a 64-byte slot row: the column reflection once per lane, the
-            // row's per slot (wave-uniform), and 11 slots' loads in flight before their LDS stores
-            static_assert(kRawP == 64 && kRawRows % 11 == 0, "one lane per slot column, 11-slot batches");
-            const uint8_t* col = img + reflect101(cx - 21 + lane, w);
-            for (int s0 = 0; s0 < kRawRows; s0 += 11) {
+            // reflect-101 bytes, lane = column (43 of the 48 per row), the column reflection once per lane,
+            // the row's per row (wave-uniform), and 11 rows' loads in flight before their LDS stores
+            static_assert(kRawRows >= 44, "rows 0..43 filled");
+            const uint8_t* col = img + reflect101(cx - 21 + min(lane, 42), w);
+            for (int s0 = 0; s0 < 44; s0 += 11) {
                 uint8_t v[11];
 #pragma unroll
-                for (int u = 0; u < 11; ++u) {
-                    const int r = raw_slot(min(s0 + u, 43));   // slot -> row; row 43 repeats row 42
-                    v[u] = col[(size_t)reflect101(cy - 21 + min(r, 42), h) * pitch];
-                }
+                for (int u = 0; u < 11; ++u) v[u] = col[(size_t)reflect101(cy - 21 + min(s0 + u, 42), h) * pitch];   // row 43 repeats row 42
+                if (lane < kRawP) {
 #pragma unroll
-                for (int u = 0; u < 11; ++u) raw[(s0 + u) * kRawP + lane] = v[u];
+                    for (int u = 0; u < 11; ++u) raw[(s0 + u) * kRawP + lane] = v[u];
+                }
             }
         }
     };
@@ -2032,7 +2026,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
 
 #if !ORBX_DESC_ICG
         // IC_Angle (src/ORBextractor.cc:84-128): integer moments over the disc, any order
-        const int icb0 = raw_slot(ic_row) * kRawP + ((csb + ic_row * csp) & 3) + ic_col;
+        const int icb0 = ic_row * kRawP + ((csb + ic_row * csp) & 3) + ic_col;
         const uint32_t* icq = raw32 + (icb0 >> 2);
         const uint32_t icsh = (uint32_t)(icb0 & 3);
         const uint32_t q0 = icq[0], q1 = icq[1], q2 = icq[2], q3 = icq[3], q4 = icq[4];
@@ -2069,7 +2063,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * rp + e;
                 const uint32_t sh = (uint32_t)((csb + r * csp) & 3);
-                const uint32_t* rr = raw32 + raw_slot(r) * (kRawP / 4) + cg;
+                const uint32_t* rr = raw32 + r * (kRawP / 4) + cg;
                 const uint32_t W0 = rr[0], W1 = rr[1], W2 = rr[2], W3 = rr[3];
                 const uint32_t R[3] = {__builtin_amdgcn_alignbyte(W1, W0, sh), __builtin_amdgcn_alignbyte(W2, W1, sh),
                                        __builtin_amdgcn_alignbyte(W3, W2, sh)};
