@@ -248,6 +248,14 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
                     if ((x & 0xFFFF) < first || (x >> 16) - first > 7) L.pyr_win = 0;
                 }
             }
+            // the window path's x4 vertical sums: 4 * 255 * sum(a) * sum(b) + 2^23 < 2^32 (then every
+            // result is <= 255 as well); OpenCV's coefficient pairs sum to 2048, give or take a rounding
+            long long sa = 0, sb = 0;
+            for (int i = L.xtab_off; i < (int)xt.size(); ++i)
+                sa = std::max(sa, (long long)(xt[i].y & 0xFFFF) + ((unsigned)xt[i].y >> 16));
+            for (int i = L.ytab_off; i < (int)yt.size(); ++i)
+                sb = std::max(sb, (long long)(yt[i].y & 0xFFFF) + ((unsigned)yt[i].y >> 16));
+            if (4LL * 255 * sa * sb + (1LL << 23) >= (1LL << 32)) L.pyr_win = 0;
         }
         prev_w = L.w;
         prev_h = L.h;

@@ -61,19 +61,23 @@ __device__ __forceinline__ ushort2_t as_us2(uint32_t v)
 #endif
 constexpr int kPyrRows = ORBX_PYR_ROWS;
 constexpr int kPyrNT = ORBX_PYR_NT;   // threads per pyramid workgroup
-constexpr int kPyrLd = 8;   // staged dwords in flight per thread
 
 template <bool kWin>
 __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
                                                        const int2* __restrict__ xtab,
-                                                       const int2* __restrict__ ytab)
+                                                       const int2* __restrict__ ytab, int lp)
 {
-    // A block makes kPyrRows output rows of one frame: the source rows they need are
-    // staged in LDS with coalesced dword loads (realigned with v_alignbyte, so any
-    // source pitch works), then each thread makes 4 output pixels per dword store.
+    // A block makes kPyrRows output rows of one frame.  The source rows they need arrive in LDS by
+    // LDS-DMA (global_load_lds_dwordx4): row r is the 16-byte aligned run of lp bytes that holds it,
+    // at LDS byte r * lp, so its pixel x sits at r * lp + sh_r + x with sh_r = its start address & 15
+    // (0 on every row of levels >= 1, whose pitch is a multiple of 64).  A chunk is fetched only if it
+    // holds a byte of its row: it then lies in the row's own 16-byte aligned span, which cannot cross a
+    // page boundary, so no read leaves the caller's allocation.  (Round 2: aligned dword loads realigned
+    // by alignbyte and stored to LDS, about 14 VALU per staged dword.)
     extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
     const int lb = xcd_block(blockIdx.y + blockIdx.z * gridDim.y, gridDim.y * gridDim.z);
     const int f = lb / gridDim.y, dy0 = (lb - f * gridDim.y) * kPyrRows;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const LevelGeom& D = G->lv[l];
     const int sw = G->lv[l - 1].w;
     const int dyn = min(kPyrRows, D.h - dy0);
@@ -82,46 +86,28 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
     const int sy0 = ytab[D.ytab_off + dy0].x & 0xFFFF;
     const int sy1 = (int)((uint32_t)ytab[D.ytab_off + dy0 + dyn - 1].x >> 16);
     const int nrows = sy1 - sy0 + 1;
-    const int nd = (sw + 3) >> 2;                 // dwords per staged row
-    // 32-bit byte offsets from the block-uniform aligned base (scalar base + vector offset loads);
-    // the row split uses a float reciprocal: (i + 0.5) / nd sits 0.5 / nd from any integer and the
-    // float product errs by < (i + 1) / nd * 2^-23, so r is exact for i < 2^22 (here i < 13k)
-    const __attribute__((address_space(1))) uint8_t* base =
-        (const __attribute__((address_space(1))) uint8_t*)((uintptr_t)src & ~(uintptr_t)3);
-    const uint32_t o0 = (uint32_t)((uintptr_t)src & 3) + (uint32_t)sy0 * (uint32_t)spitch;
-    const float inv_nd = 1.0f / (float)nd;
-    // kPyrLd dwords per thread in flight: every load of a batch is issued before the first is used
-    // (one dependent load per dword left each thread waiting ~14 HBM latencies per block at level 1)
-    const int total = nrows * nd;
-    for (int i0 = threadIdx.x; i0 < total; i0 += kPyrNT * kPyrLd) {
-        uint32_t lo[kPyrLd], hi[kPyrLd], sh[kPyrLd];
-        int dst[kPyrLd];
-#pragma unroll
-        for (int u = 0; u < kPyrLd; ++u) {
-            const int i = i0 + kPyrNT * u;
-            dst[u] = -1;
-            if (i < total) {
-                const int r = (int)(((float)i + 0.5f) * inv_nd), k = i - __mul24(r, nd);
-                const uint32_t o = o0 + __umul24((uint32_t)r, (uint32_t)spitch) + 4u * (uint32_t)k;
-                const __attribute__((address_space(1))) uint32_t* ap =
-                    (const __attribute__((address_space(1))) uint32_t*)(base + (o & ~3u));
-                // the second dword is needed only if some of its bytes belong to the row; an aligned
-                // dword that starts inside the row cannot run past the (4-byte aligned) buffer end, so a
-                // tail re-reads the first (alignbyte by 0 ignores it, and bytes past the row are never read)
-                sh[u] = o & 3u;
-                const bool tail = sh[u] == 0 || 4 * k + 4 - (int)sh[u] >= sw;
-                lo[u] = ap[0];
-                hi[u] = ap[tail ? 0 : 1];
-                dst[u] = r * nd + k;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kPyrLd; ++u)
-            if (dst[u] >= 0) s_src[dst[u]] = __builtin_amdgcn_alignbyte(hi[u], lo[u], sh[u]);
+    const int nc = lp >> 4;   // 16-byte chunks per staged row
+    const uintptr_t ra = (uintptr_t)src + (size_t)sy0 * spitch;
+    const uint8_t* gb = (const uint8_t*)(ra & ~(uintptr_t)15);
+    const uint32_t sh0 = (uint32_t)(ra & 15);
+    // row r's offset from gb: sh0 + r * spitch; the chunk split uses the float reciprocal of nc
+    // ((i + 0.5) / nc sits 0.5 / nc from any integer: exact for i < 2^22)
+    const int total = nrows * nc;
+    const float inv_nc = 1.0f / (float)nc;
+    for (int i0 = wave * 64; i0 < total; i0 += kPyrNT) {
+        const int i = i0 + lane;
+        const int r = (int)(((float)i + 0.5f) * inv_nc), c = i - __mul24(r, nc);
+        const uint32_t ro = sh0 + __umul24((uint32_t)r, (uint32_t)spitch);
+        const uint32_t co = (ro & ~15u) + 16u * (uint32_t)c;
+        if (i < total && co < ro + (uint32_t)sw)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(gb + co),
+                                             (__attribute__((address_space(3))) void*)(s_src + 4 * i0), 16, 0, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint8_t* S = (const uint8_t*)s_src;
-    const int srow = nd * 4;
+    // LDS byte of staged row r's pixel 0 (block-uniform)
+    auto rowb = [&](int r) -> uint32_t { return (uint32_t)(r * lp) + ((sh0 + (uint32_t)r * (uint32_t)spitch) & 15u); };
     // a thread owns a group of 4 output columns: their coefficients are loaded once and
     // reused for the block's rows
     const int q = (D.w + 3) >> 2;
@@ -146,42 +132,65 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
             // The group's 8 taps lie in the 8 bytes from x0[0] (LevelGeom::pyr_win, checked on the host):
             // per source row three dword reads, realigned to x0[0] by two alignbytes; each column's tap
             // pair is one v_perm into a u16 pair and one v_dot2_u32_u16 with (a0, a1)
-            const uint32_t wb = (uint32_t)(x0[0] & ~3), wo = (uint32_t)(x0[0] & 3);
             uint32_t sel[4], ak[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 sel[k] = (uint32_t)(x0[k] - x0[0]) | 0x0C00u | ((uint32_t)(x1[k] - x0[0]) << 16) | 0x0C000000u;
                 ak[k] = a0[k] | (a1[k] << 16);
             }
-            auto hrow = [&](const uint8_t* row, uint32_t h[4]) {
-                const uint32_t* q = (const uint32_t*)(row + wb);
-                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+            auto hrow = [&](int r, uint32_t h[4]) {
+                const uint32_t A = rowb(r) + (uint32_t)x0[0];
+                const uint32_t* qd = (const uint32_t*)(S + (A & ~3u));
+                const uint32_t d0 = qd[0], d1 = qd[1], d2 = qd[2], wo = A & 3u;
                 const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, wo), e1 = __builtin_amdgcn_alignbyte(d2, d1, wo);
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     h[k] = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(e1, e0, sel[k])), as_us2(ak[k]), 0u,
                                                   false);
             };
-            for (int rr = 0; rr < dyn; ++rr) {
-                const int2 yt = ytab[D.ytab_off + dy0 + rr];
-                const uint32_t b0 = (uint32_t)yt.y & 0xFFFFu, b1 = (uint32_t)yt.y >> 16;
-                uint32_t h0[4], h1[4];
-                hrow(S + ((yt.x & 0xFFFF) - sy0) * srow, h0);
-                hrow(S + ((int)((uint32_t)yt.x >> 16) - sy0) * srow, h1);
-                uint32_t packed = 0;
+            // Output rows in order; consecutive rows share a source row (lo(y + 1) == hi(y)) at scale
+            // factors up to 2, and that row's horizontal sums are kept instead of recomputed.  The
+            // vertical sum is taken x4, (4 (h0 b0 + h1 b1) + 2^23) >> 24 = (h0 b0 + h1 b1 + 2^21) >> 22,
+            // so each result is byte 3 of its sum and two v_perm pack four of them; the host checks that
+            // the coefficient sums keep 4 * 255 * sum(a) * sum(b) + 2^23 below 2^32, which also makes
+            // every result <= 255 (no saturation).
+            int cr = -1;
+            uint32_t hc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t v = (__umul24(h0[k], b0) + __umul24(h1[k], b1) + (1u << 21)) >> 22;
-                    packed |= min(v, 255u) << (8 * k);
+            for (int rr = 0; rr < kPyrRows; ++rr) {
+                if (rr >= dyn) break;
+                const int2 yt = ytab[D.ytab_off + dy0 + rr];
+                const int lo = (yt.x & 0xFFFF) - sy0, hi = (int)((uint32_t)yt.x >> 16) - sy0;
+                const uint32_t b0 = ((uint32_t)yt.y & 0xFFFFu) << 2, b1 = ((uint32_t)yt.y >> 16) << 2;
+                uint32_t h0[4], h1[4];
+                if (lo == cr) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) h0[k] = hc[k];
+                } else {
+                    hrow(lo, h0);
                 }
+                if (hi == lo) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) h1[k] = h0[k];
+                } else {
+                    hrow(hi, h1);
+                }
+                uint32_t acc[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] = __umul24(h1[k], b1) + (__umul24(h0[k], b0) + (1u << 23));
+                const uint32_t packed = __builtin_amdgcn_perm(acc[1], acc[0], 0x0C0C0703u) |
+                                        __builtin_amdgcn_perm(acc[3], acc[2], 0x07030C0Cu);
                 *reinterpret_cast<uint32_t*>(drow0 + (size_t)rr * D.pitch + dx0) = packed;
+                cr = hi;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) hc[k] = h1[k];
             }
             continue;
         }
         for (int rr = 0; rr < dyn; ++rr) {
             const int2 yt = ytab[D.ytab_off + dy0 + rr];
-            const uint8_t* r0 = S + ((yt.x & 0xFFFF) - sy0) * srow;
-            const uint8_t* r1 = S + ((int)((uint32_t)yt.x >> 16) - sy0) * srow;
+            const uint8_t* r0 = S + rowb((yt.x & 0xFFFF) - sy0);
+            const uint8_t* r1 = S + rowb((int)((uint32_t)yt.x >> 16) - sy0);
             const uint32_t b0 = (uint32_t)yt.y & 0xFFFFu, b1 = (uint32_t)yt.y >> 16;
             uint32_t packed = 0;
 #pragma unroll
@@ -203,13 +212,15 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         const int h = g.lv[l].h;
         // source rows per block: kPyrRows * (src/dst scale) + 2, bounded by the level ratio
         const int srows = (kPyrRows * g.lv[l - 1].h + g.lv[l].h - 1) / g.lv[l].h + 2;
-        // + 8 bytes: the window path's third dword of a group at the end of the last row
-        const size_t smem = (size_t)srows * (((g.lv[l - 1].w + 3) >> 2) * 4) + 8;
+        // LDS row: the 16-byte chunks spanning a row at any start alignment; + 16 bytes: the window
+        // path's third dword of a group at the end of the last row
+        const int lp = ((g.lv[l - 1].w + 15 + 15) >> 4) << 4;
+        const size_t smem = (size_t)srows * lp + 16;
         dim3 grid(1, (h + kPyrRows - 1) / kPyrRows, batch);
         if (g.lv[l].pyr_win)
-            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(kPyrNT), smem, s, b.geom, p, l, b.xtab, b.ytab);
+            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(kPyrNT), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
         else
-            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(kPyrNT), smem, s, b.geom, p, l, b.xtab, b.ytab);
+            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(kPyrNT), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
     }
 }
 
