@@ -390,8 +390,10 @@ def main():
         pass
     kept = float(counts.mean())
     cand = float(n_cand if n_cand is not None else 10 * NFEAT)
+    n_launch = ex.debug_launches(H, W, B)
     alg = {
-        "pyramid": B * sum(A[l - 1] + A[l] for l in range(1, NLEVELS)),
+        # each launch reads its source level once and writes its levels (orbx_debug_launches)
+        "pyramid": B * (sum(A[l] for l in range(NLEVELS) if n_launch["pyramid_sources"] >> l & 1) + sum(A[1:])),
         "fast": B * (sum(A) + 4 * cand),
         "quadtree": B * (4 * cand + 4 * kept),
         # compulsory bytes: every level pixel once (patches overlap), the packed keypoint in,
@@ -399,12 +401,11 @@ def main():
         "describe": B * (sum(A) + kept * (4 + 60)),
         "match": (B - 1) * 2 * kept * 60,
     }
-    n_launch = ex.debug_launches(H, W, B)
     def roofline(st):
         dom = max(st, key=lambda k: st[k])
         # several launches of one kernel per stage: per-launch figures are stage / launches,
         # like rocprofv3's per-kernel average (the library reports its launch plan for this batch:
-        # pyramid one per level, FAST one per LDS class of cells, orbx_extract.hip fast_groups)
+        # pyramid one per level, FAST one per LDS class of cells, orbx_extract.hip)
         launches = {"pyramid": n_launch["pyramid"], "fast": n_launch["fast"]}.get(dom, 1)
         t_launch = st[dom] / launches * 1e-3
         achieved = alg[dom] / launches / t_launch / 1e9

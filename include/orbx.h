@@ -121,7 +121,8 @@ orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n);
 orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t out_size);
 orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys, int cap, int* n);
 /* Kernel launches per stage of one batched extract of `batch` frames of rows x cols (measurement
- * hook: per-launch roofline figures): counts[0] pyramid, [1] FAST, [2] quadtree, [3] describe. */
+ * hook: per-launch roofline figures): counts[0] pyramid, [1] FAST, [2] quadtree, [3] describe;
+ * counts[4]: bit l set if a pyramid launch reads level l. */
 orbx_status orbx_debug_launches(orbx_handle* h, int rows, int cols, int batch, int* counts, int n);
 
 /* ---- Stereo (Frame::ComputeStereoMatches, src/Frame.cc:630-872) ----

@@ -550,8 +550,10 @@ orbx_status orbx_debug_launches(orbx_handle* h, int rows, int cols, int batch, i
     int fast = 0;
     for (int i = 0; i < g.fast_groups; ++i) fast += g.fast_cb[i + 1] > g.fast_cb[i];
     QtGroup grp[kQtMaxGroups];
-    const int c[4] = {g.nlevels - 1, fast, qt_plan(g, batch, grp), 1};
-    for (int i = 0; i < n; ++i) counts[i] = i < 4 ? c[i] : 0;
+    // the pyramid's launches each read one level (counts[4]: bit mask): one launch per level from the one
+    // before it
+    const int c[5] = {g.nlevels - 1, fast, qt_plan(g, batch, grp), 1, (1 << (g.nlevels - 1)) - 1};
+    for (int i = 0; i < n; ++i) counts[i] = i < 5 ? c[i] : 0;
     return ORBX_OK;
 }
 

@@ -8,6 +8,9 @@
 //                       :84-128, :1300-1332, :141-192
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "orbx_kernels.hpp"
 #include "orbx_math.hpp"
 
@@ -94,7 +97,8 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
     // ((i + 0.5) / nc sits 0.5 / nc from any integer: exact for i < 2^22)
     const int total = nrows * nc;
     const float inv_nc = 1.0f / (float)nc;
-    for (int i0 = wave * 64; i0 < total; i0 += kPyrNT) {
+    const int nt = blockDim.x;
+    for (int i0 = wave * 64; i0 < total; i0 += nt) {
         const int i = i0 + lane;
         const int r = (int)(((float)i + 0.5f) * inv_nc), c = i - __mul24(r, nc);
         const uint32_t ro = sh0 + __umul24((uint32_t)r, (uint32_t)spitch);
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
     // reused for the block's rows
     const int q = (D.w + 3) >> 2;
     uint8_t* drow0 = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off + (size_t)dy0 * D.pitch;
-    for (int g = threadIdx.x; g < q; g += kPyrNT) {
+    for (int g = threadIdx.x; g < q; g += nt) {
         const int dx0 = g * 4;
         // every product fits a 24 x 24 -> 32-bit multiply (v_mul_u32_u24, full rate; the compiler
         // otherwise emits the quarter-rate v_mul_lo_u32 for h * b).  The two taps keep separate
@@ -217,10 +221,15 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         const int lp = ((g.lv[l - 1].w + 15 + 15) >> 4) << 4;
         const size_t smem = (size_t)srows * lp + 16;
         dim3 grid(1, (h + kPyrRows - 1) / kPyrRows, batch);
+        // a thread per 4-column group: narrow levels take fewer waves per block (ORBX_PYR_NARROW=0: always
+        // kPyrNT, A/B knob)
+        static const int narrow = getenv("ORBX_PYR_NARROW") ? atoi(getenv("ORBX_PYR_NARROW")) : 1;
+        const int q = (g.lv[l].w + 3) >> 2;
+        const int nt = narrow ? std::min(kPyrNT, (q + 63) & ~63) : kPyrNT;
         if (g.lv[l].pyr_win)
-            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(kPyrNT), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
+            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
         else
-            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(kPyrNT), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
+            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
     }
 }
 

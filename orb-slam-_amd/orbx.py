@@ -385,11 +385,12 @@ class ORBextractor:
         return out[:n.value].copy()
 
     def debug_launches(self, rows, cols, batch):
-        """Kernel launches per stage of one batched extract: {pyramid, fast, quadtree, describe}."""
-        c = np.zeros(4, np.int32)
+        """Kernel launches per stage of one batched extract: {pyramid, fast, quadtree, describe}, and
+        pyramid_sources, the bit mask of the levels the pyramid launches resize from."""
+        c = np.zeros(5, np.int32)
         _check("orbx_debug_launches", lib.orbx_debug_launches(self._h, rows, cols, batch,
-                                                              c.ctypes.data_as(C.POINTER(C.c_int)), 4))
-        return dict(zip(("pyramid", "fast", "quadtree", "describe"), (int(v) for v in c)))
+                                                              c.ctypes.data_as(C.POINTER(C.c_int)), 5))
+        return dict(zip(("pyramid", "fast", "quadtree", "describe", "pyramid_sources"), (int(v) for v in c)))
 
 
 def compute_stereo_matches(left, right, kps_l, desc_l, kps_r, desc_r, bf, fx):
