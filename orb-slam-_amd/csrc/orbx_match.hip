@@ -11,6 +11,8 @@
 #include <algorithm>
 
 #include <type_traits>
+#include <cstdlib>
+
 #include "orbx_kernels.hpp"
 
 namespace orbx {
@@ -203,10 +205,10 @@ void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, ui
 //               Frame::GetFeaturesInArea visits them — grid cell (ix outer,
 //               iy inner, Frame::PosInGrid rounding), then index
 //               (AssignFeaturesToGrid insertion order), src/Frame.cc:292-518.
-//   k_si_build  (pair, query-slice) workgroups, one wave per query: the
-//               window's columns are one contiguous key range (binary search
-//               in LDS), filtered by row and |dx|,|dy| < r.  The wave keeps the
-//               4 smallest (Hamming, visit position) candidates and the count.
+//   k_si_build  (pair, query-slice) workgroups, four lanes per query: the
+//               window's columns are one contiguous key range (a column-start
+//               table in LDS), filtered by row and |dx|,|dy| < r.  The quad keeps
+//               the 4 smallest (Hamming, visit position) candidates and the count.
 //   k_si_greedy one workgroup per pair: one wave replays the order-dependent
 //               greedy pass (vMatchedDistance skip, best/second, ratio test,
 //               eviction) and the rotation-histogram filter
@@ -425,53 +427,47 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
     const uint8_t* d1 = desc + (size_t)fa * cap * 32;
     const float2* pv = prev ? prev + (size_t)pair * cap : nullptr;
     const int nwaves = gridDim.y * (SI_BUILD_NT / 64);
-    // A wave handles about 18 queries.  The next query's descriptor and window centre are loaded before
-    // the current one's scan, and the results (top-4, count) collect in lane q of five registers and go to
-    // HBM after the wave's last query: a store per query would make every later load wait for its round
-    // trip (vmcnt counts loads and stores, completed in issue order).
+    // Four lanes per query (a quad), 16 queries per wave: the quad's lanes take the window's key range
+    // round-robin, each keeping its 4 smallest (Hamming << 16 | visit position), and two quad-DPP steps per
+    // output merge them.  A candidate's visit position is the quad's in-window count before it in key
+    // order (the quad's ballot bits).  (Round 2: a wave per query, whose 64-lane merge of the top-4 was
+    // most of the kernel's instructions for ~74 keys per window.)
+    auto quad_min = [](uint32_t v) {
+        v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
+        return min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));  // quad_perm [2,3,0,1]
+    };
+    auto quad_or = [](uint32_t v) {
+        v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);
+        return v | (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);
+    };
+    const int sub = lane & 3, qbase = lane & ~3;
     auto scan_queries = [&](auto staged_tag) {
         constexpr bool kStaged = decltype(staged_tag)::value;
         const uint32_t* K = kStaged ? (const uint32_t*)skeys : keys;
         const float2* XY = kStaged ? (const float2*)sxy : xy;
-        const int q0 = blockIdx.y * (SI_BUILD_NT / 64) + wave;
-        ulonglong2 na0 = make_ulonglong2(0, 0), na1 = make_ulonglong2(0, 0);
-        float2 nc = make_float2(0.f, 0.f);
-        auto load_query = [&](int q) {
+        const int wg = blockIdx.y * (SI_BUILD_NT / 64) + wave;
+        for (int r0 = wg * 16; r0 < n10; r0 += nwaves * 16) {   // wave-uniform
+            const int q = r0 + (lane >> 2);
+            SiWindow w;
+            ulonglong2 a0 = make_ulonglong2(0, 0), a1 = make_ulonglong2(0, 0);
+            w.lo = w.hi = 0;
             if (q < n10) {
                 const ulonglong2* a = (const ulonglong2*)(d1 + (size_t)q * 32);
-                na0 = a[0];
-                na1 = a[1];
+                a0 = a[0];
+                a1 = a[1];
                 // window centre vbPrevMatched[q] (src/ORBmatcher.cc:456-460); F1's own keypoint when not given
-                nc = pv ? pv[q] : make_float2(k1[q].x, k1[q].y);
+                const float2 c = pv ? pv[q] : make_float2(k1[q].x, k1[q].y);
+                w = si_window(K, ng, c, (float)window, G, colstart);
             }
-        };
-        uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, rc = 0;   // lane j: the wave's query q0 + (qb + j) * nwaves
-        int nq = 0, qb = 0;
-        auto flush = [&]() {
-            if (lane < nq) {
-                const size_t at = (size_t)pair * cap + q0 + (size_t)(qb + lane) * nwaves;
-                qtop[at] = make_uint4(r0, r1, r2, r3);
-                qcnt[at] = (int)rc;
-            }
-            qb += nq;
-            nq = 0;
-        };
-        load_query(q0);
-        for (int i1 = q0; i1 < n10; i1 += nwaves) {
-            const ulonglong2 a0 = na0, a1 = na1;
-            const float2 c = nc;
-            load_query(i1 + nwaves);
-            const SiWindow w = si_window(K, ng, c, (float)window, G, colstart);
-            // lane-local 4 smallest (Hamming << 16 | visit position), with their i2
             uint32_t hk[SI_TOPK], hi2[SI_TOPK];
 #pragma unroll
-            for (int q = 0; q < SI_TOPK; ++q) hk[q] = hi2[q] = 0xFFFFFFFFu;
+            for (int t = 0; t < SI_TOPK; ++t) hk[t] = hi2[t] = 0xFFFFFFFFu;
             int count = 0;
-            for (int g0 = w.lo; g0 < w.hi; g0 += 64) {
+            for (int g0 = w.lo; g0 < w.hi; g0 += 4) {   // quad-uniform trip count
                 int i2 = 0;
-                const int g = g0 + lane;
+                const int g = g0 + sub;
                 const bool in = si_in_window(K, XY, w, g, i2);
-                const unsigned long long m = __ballot(in);
+                const uint32_t qb = (uint32_t)(__ballot(in) >> qbase) & 0xFu;
                 if (in) {
                     int d;
                     if constexpr (kStaged) {
@@ -480,49 +476,44 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
                         const ulonglong2* b = (const ulonglong2*)(d2 + (size_t)i2 * 32);
                         d = ham256(a0, a1, b[0], b[1]);
                     }
-                    const int pos = count + lanes_below_u64(m);
+                    const int pos = count + __builtin_popcount(qb & ((1u << sub) - 1u));
                     uint32_t k = ((uint32_t)d << 16) | (uint32_t)pos, v = (uint32_t)i2;
 #pragma unroll
-                    for (int q = 0; q < SI_TOPK; ++q) {   // sorted insert
-                        if (k < hk[q]) {
-                            const uint32_t tk = hk[q], tv = hi2[q];
-                            hk[q] = k;
-                            hi2[q] = v;
+                    for (int t = 0; t < SI_TOPK; ++t) {   // sorted insert
+                        if (k < hk[t]) {
+                            const uint32_t tk = hk[t], tv = hi2[t];
+                            hk[t] = k;
+                            hi2[t] = v;
                             k = tk;
                             v = tv;
                         }
                     }
                 }
-                count += __popcll(m);
+                count += __builtin_popcount(qb);
             }
-            // wave merge: keys are unique (visit positions), so one lane pops per round
+            // quad merge: keys are unique (visit positions), so one lane pops per round
             uint32_t top[SI_TOPK];
 #pragma unroll
-            for (int q = 0; q < SI_TOPK; ++q) {
-                const uint32_t kmin = wave_min_u32(hk[0]);
-                const unsigned long long wm = __ballot(hk[0] == kmin);
-                const int wl = wm ? (int)__builtin_ctzll(wm) : 0;
-                const uint32_t i2 = (uint32_t)__builtin_amdgcn_readlane((int)hi2[0], wl);
-                top[q] = kmin == 0xFFFFFFFFu ? 0xFFFFFFFFu : ((kmin & 0xFFFF0000u) | i2);
-                if (kmin != 0xFFFFFFFFu && hk[0] == kmin) {
+            for (int t = 0; t < SI_TOPK; ++t) {
+                const uint32_t kmin = quad_min(hk[0]);
+                const bool own = kmin != 0xFFFFFFFFu && hk[0] == kmin;
+                const uint32_t i2 = quad_or(own ? hi2[0] : 0u);
+                top[t] = kmin == 0xFFFFFFFFu ? 0xFFFFFFFFu : ((kmin & 0xFFFF0000u) | i2);
+                if (own) {
 #pragma unroll
-                    for (int r = 0; r + 1 < SI_TOPK; ++r) {
-                        hk[r] = hk[r + 1];
-                        hi2[r] = hi2[r + 1];
+                    for (int u = 0; u + 1 < SI_TOPK; ++u) {
+                        hk[u] = hk[u + 1];
+                        hi2[u] = hi2[u + 1];
                     }
                     hk[SI_TOPK - 1] = hi2[SI_TOPK - 1] = 0xFFFFFFFFu;
                 }
             }
-            if (lane == nq) {
-                r0 = top[0];
-                r1 = top[1];
-                r2 = top[2];
-                r3 = top[3];
-                rc = (uint32_t)count;
+            if (sub == 0 && q < n10) {
+                const size_t at = (size_t)pair * cap + q;
+                qtop[at] = make_uint4(top[0], top[1], top[2], top[3]);
+                qcnt[at] = count;
             }
-            if (++nq == 64) flush();
         }
-        flush();
     };
     if (staged)
         scan_queries(std::true_type{});
@@ -925,7 +916,9 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)p2 * 4, s, kps, counts, cap, G, gkeys, gxy, gn);
     const size_t bsmem = si_build_smem_bytes();
     // query slices per pair: about 8 waves per SIMD over the chip, at least 4 queries per wave
-    const int qsplit = std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
+    // (ORBX_SI_QSPLIT: A/B knob)
+    static const int qs_env = getenv("ORBX_SI_QSPLIT") ? atoi(getenv("ORBX_SI_QSPLIT")) : 0;
+    const int qsplit = qs_env > 0 ? qs_env : std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
     hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, G,
                        window, (const float2*)prev, gkeys, gxy, gn, qcnt, qtop);
     const int ldscap = std::min(cap, si_lds_max_cap());
