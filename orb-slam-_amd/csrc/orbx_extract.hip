@@ -1189,18 +1189,25 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
     // staged forms are branch-free (indices clamped, the loads of every slot in flight together); the
     // search form branches.
     if (n > 0 && (omap || staged)) {   // block-uniform
+        // every slot's load in flight before the first LDS store: an LDS store waiting for its global load
+        // holds the LDS reads queued behind it (the next slot's owner lookups), which serialised the slots'
+        // HBM round trips (level 0: 17.9k of the workgroup's 130k cycles)
+        uint32_t v[QT_KPT];
 #pragma unroll
         for (int r = 0; r < QT_KPT; ++r) {
-            const int i = tid + r * QT_NT, ii = min(i, n - 1);
-            uint32_t v;
+            const int ii = min(tid + r * QT_NT, n - 1);
             if (omap) {
                 const int c = owner[ii];
-                v = fslots[gbase[c] + (uint32_t)(ii - (int)scan[c])];
+                v[r] = fslots[gbase[c] + (uint32_t)(ii - (int)scan[c])];
             } else {
-                v = stage[ii];
+                v[r] = stage[ii];
             }
-            if constexpr (kKpL) kpa[i] = i < n ? v : 0u;
-            else kp[r] = i < n ? v : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < QT_KPT; ++r) {
+            const int i = tid + r * QT_NT;
+            if constexpr (kKpL) kpa[i] = i < n ? v[r] : 0u;
+            else kp[r] = i < n ? v[r] : 0u;
             nd[r] = 0;
         }
     } else {

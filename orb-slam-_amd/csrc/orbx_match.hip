@@ -201,7 +201,7 @@ void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, ui
 // ---------------------------------------------------------------------------
 // M1: SearchForInitialization (src/ORBmatcher.cc:417-588) for a batch of
 // frame pairs, in three launches:
-//   k_si_grid   one workgroup per frame: its level-0 keypoints sorted the way
+//   k_si_grid   one workgroup per frame: its level-0 keypoints ranked the way
 //               Frame::GetFeaturesInArea visits them — grid cell (ix outer,
 //               iy inner, Frame::PosInGrid rounding), then index
 //               (AssignFeaturesToGrid insertion order), src/Frame.cc:292-518.
@@ -275,18 +275,20 @@ __global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict
                                                  int cap, orbm_grid G, uint32_t* __restrict__ gkeys,
                                                  float2* __restrict__ gxy, int* __restrict__ gn)
 {
+    // Keys (cell << 16 | index) are unique, so a key's place in the sorted order is the number of smaller
+    // keys: every thread ranks its keys against the whole array by broadcast 16-byte LDS reads, one
+    // barrier, and scatters (round 2: a bitonic network, log2(n)^2 / 2 barrier-separated stages).
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
     __shared__ int s_ng;
     const int f = blockIdx.x, tid = threadIdx.x;
     const orbx_keypoint* k = kps + (size_t)f * cap;
     const int n = min(counts[f], cap);
     const int n0 = level0_count(k, n);
-    int p2 = 1;
-    while (p2 < n0) p2 <<= 1;
+    const int n4 = (n0 + 3) >> 2;
     if (tid == 0) s_ng = 0;
     __syncthreads();
-    for (int i = tid; i < p2; i += 256) {
-        uint32_t key = 0xFFFFFFFFu;
+    for (int i = tid; i < 4 * n4; i += 256) {
+        uint32_t key = 0xFFFFFFFFu;   // outside the grid (or padding): above every key, never ranked
         if (i < n0) {
             const int px = (int)roundf((k[i].x - G.min_x) * G.grid_w_inv);
             const int py = (int)roundf((k[i].y - G.min_y) * G.grid_h_inv);
@@ -298,31 +300,21 @@ __global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict
         keys[i] = key;
     }
     __syncthreads();
-    for (int size = 2; size <= p2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = tid; i < (p2 >> 1); i += 256) {
-                const int lo = 2 * i - (i & (stride - 1));
-                const int hi = lo + stride;
-                const bool asc = (lo & size) == 0;
-                const uint32_t a = keys[lo], b = keys[hi];
-                if ((a > b) == asc) {
-                    keys[lo] = b;
-                    keys[hi] = a;
-                }
-            }
-            __syncthreads();
+    const uint4* k4 = (const uint4*)keys;
+    for (int i = tid; i < n0; i += 256) {
+        const uint32_t key = keys[i];
+        if (key == 0xFFFFFFFFu) continue;
+        int r = 0;
+        for (int j4 = 0; j4 < n4; ++j4) {
+            const uint4 v = k4[j4];
+            r += (int)(v.x < key) + (int)(v.y < key) + (int)(v.z < key) + (int)(v.w < key);
         }
-    }
-    const int ng = s_ng;
-    for (int g = tid; g < ng; g += 256) {
-        const uint32_t key = keys[g];
-        const int i2 = (int)(key & 0xFFFF);
-        gkeys[(size_t)f * cap + g] = key;
-        gxy[(size_t)f * cap + g] = make_float2(k[i2].x, k[i2].y);
+        gkeys[(size_t)f * cap + r] = key;
+        gxy[(size_t)f * cap + r] = make_float2(k[i].x, k[i].y);
     }
     if (tid == 0) {
         gn[2 * f] = n0;
-        gn[2 * f + 1] = ng;
+        gn[2 * f + 1] = s_ng;
     }
 }
 
@@ -621,7 +613,12 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
     }
     if (tid < 32) s_hist[tid] = 0;
     __syncthreads();
-    if (tid >= 64) return;
+    if (tid >= 64) {
+        // vnMatches12 past the level-0 queries is -1: written by the idle waves while wave 0 runs the
+        // greedy pass (one wave writing all cap entries at the end was a third of the kernel's time)
+        for (int i = n10 + tid - 64; i < cap; i += 192) out[i] = -1;
+        return;
+    }
 #ifdef ORBX_SI_PROF
     const long long pt1 = clock64();
 #endif
@@ -856,8 +853,8 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     int nmatches = 0;
-    for (int i = lane; i < cap; i += 64) {
-        const int v = i < n10 ? (int)m12[i] : -1;
+    for (int i = lane; i < n10; i += 64) {
+        const int v = (int)m12[i];
         out[i] = v;
         nmatches += v >= 0;
         if (pv && v >= 0) pv[i] = make_float2(k2[v].x, k2[v].y);   // update vbPrevMatched (:580-584)
@@ -911,9 +908,8 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     int* gn = (int*)carve((size_t)nframes * 2 * 4);
     int* qcnt = (int*)carve((size_t)npairs * cap * 4);
     uint4* qtop = (uint4*)carve((size_t)npairs * cap * 16);
-    int p2 = 1;
-    while (p2 < cap) p2 <<= 1;
-    hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)p2 * 4, s, kps, counts, cap, G, gkeys, gxy, gn);
+    hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)((cap + 3) & ~3) * 4, s, kps, counts, cap, G, gkeys,
+                       gxy, gn);
     const size_t bsmem = si_build_smem_bytes();
     // query slices per pair: about 8 waves per SIMD over the chip, at least 4 queries per wave
     // (ORBX_SI_QSPLIT: A/B knob)
