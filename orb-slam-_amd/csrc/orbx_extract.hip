@@ -1424,13 +1424,22 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
             return (int)(4 * p + (x >= (w & 0xFFFu) ? 1u : 0u) + (y >= ((w >> 12) & 0xFFFu) ? 2u : 0u));
         };
         if constexpr (!kG) {
-            // keys first (independent LDS loads of every register slot in flight together), then the
-            // counts: interleaved, each slot's loads would wait behind the previous slot's atomics
+            // keys first, branch-free (every slot's node and keypoint LDS reads in flight together; a slot
+            // past n has node 0, a valid index, and is masked), then the counts: interleaved, each slot's
+            // loads would wait behind the previous slot's atomics
+            uint32_t wv[QT_KPT], kv[QT_KPT];
+#pragma unroll
+            for (int r = 0; r < QT_KPT; ++r) wv[r] = sinfo[nd[r] & 0xFFFFu];
+#pragma unroll
+            for (int r = 0; r < QT_KPT; ++r) kv[r] = kpr(r);
 #pragma unroll
             for (int r = 0; r < QT_KPT; ++r) {
                 const int i = tid + r * QT_NT;
-                const int key = i < n ? child_key(kpr(r), nd[r]) : -1;
-                nd[r] = (nd[r] & 0xFFFFu) | (key >= 0 ? 0x40000u | ((uint32_t)(key & 3) << 16) : 0u);
+                const uint32_t w = wv[r], k = kv[r];
+                const bool cand = i < n && (w & 0x80000000u);
+                const uint32_t qd = ((k & 0xFFFu) >= (w & 0xFFFu) ? 1u : 0u) +
+                                    (((k >> 12) & 0xFFFu) >= ((w >> 12) & 0xFFFu) ? 2u : 0u);
+                nd[r] = (nd[r] & 0xFFFFu) | (cand ? 0x40000u | (qd << 16) : 0u);
             }
 #pragma unroll
             for (int r = 0; r < QT_KPT; ++r) {
@@ -1554,11 +1563,30 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
         QT_STAMP(11, qt_t);
 
         // ---- E: relabel keypoints with their new list position ----
-        visit([&](uint32_t& k, uint32_t& d, int) {
-            // child slot from the count pass, -1 if the node was not a candidate
-            const int ck = kG ? child_key(k, d) : (d & 0x40000u) ? (int)(4 * (d & 0xFFFFu) + ((d >> 16) & 3u)) : -1;
-            d = ck >= 0 ? (uint32_t)cpos[ck] : (uint32_t)npos[d & kPosMask];
-        });
+        if constexpr (!kG) {
+            // register slots branch-free: one LDS read per slot from the child or the node table, every
+            // slot's read in flight together; slots past n keep node 0
+            uint32_t v[QT_KPT];
+#pragma unroll
+            for (int r = 0; r < QT_KPT; ++r) {
+                const uint32_t d = nd[r];
+                const Ix* src = (d & 0x40000u) ? cpos + (4 * (d & 0xFFFFu) + ((d >> 16) & 3u)) : npos + (d & 0xFFFFu);
+                v[r] = (uint32_t)*src;
+            }
+#pragma unroll
+            for (int r = 0; r < QT_KPT; ++r) nd[r] = tid + r * QT_NT < n ? v[r] : 0u;
+            for (int i = QT_NT * QT_KPT + tid; i < n; i += QT_NT) {   // spilled keypoints
+                uint32_t& d = fspill_node[i - QT_NT * QT_KPT];
+                const int ck = (d & 0x40000u) ? (int)(4 * (d & 0xFFFFu) + ((d >> 16) & 3u)) : -1;
+                d = ck >= 0 ? (uint32_t)cpos[ck] : (uint32_t)npos[d & kPosMask];
+            }
+        } else {
+            visit([&](uint32_t& k, uint32_t& d, int) {
+                // child slot from the count pass, -1 if the node was not a candidate
+                const int ck = child_key(k, d);
+                d = ck >= 0 ? (uint32_t)cpos[ck] : (uint32_t)npos[d & kPosMask];
+            });
+        }
         QT_STAMP(12, qt_t);
         cur ^= 1;
     }
@@ -2089,7 +2117,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int r = 2 * rp + e;
-                const uint32_t sh = (uint32_t)((csb + r * csp) & 3);
+                const uint32_t sh = ((uint32_t)csb + __umul24((uint32_t)r, (uint32_t)csp)) & 3u;
                 const uint32_t* rr = raw32 + r * (kRawP / 4) + cg;
                 const uint32_t W0 = rr[0], W1 = rr[1], W2 = rr[2], W3 = rr[3];
                 const uint32_t R[3] = {__builtin_amdgcn_alignbyte(W1, W0, sh), __builtin_amdgcn_alignbyte(W2, W1, sh),
