@@ -260,17 +260,6 @@ __device__ __forceinline__ int lower_bound_u32(const uint32_t* a, int n, uint32_
     return lo;
 }
 
-__device__ __forceinline__ int level0_count(const orbx_keypoint* k, int n)
-{
-    // keypoints are concatenated level by level (src/ORBextractor.cc:1290-1333): binary search
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (k[mid].octave == 0) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
 __global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict__ kps, const int* __restrict__ counts,
                                                  int cap, orbm_grid G, uint32_t* __restrict__ gkeys,
                                                  float2* __restrict__ gxy, int* __restrict__ gn)
@@ -279,27 +268,36 @@ __global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict
     // keys: every thread ranks its keys against the whole array by broadcast 16-byte LDS reads, one
     // barrier, and scatters (round 2: a bitonic network, log2(n)^2 / 2 barrier-separated stages).
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
-    __shared__ int s_ng;
-    const int f = blockIdx.x, tid = threadIdx.x;
+    __shared__ int s_ng, s_n0;
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const orbx_keypoint* k = kps + (size_t)f * cap;
     const int n = min(counts[f], cap);
-    const int n0 = level0_count(k, n);
-    const int n4 = (n0 + 3) >> 2;
-    if (tid == 0) s_ng = 0;
+    if (tid == 0) s_ng = s_n0 = 0;
     __syncthreads();
-    for (int i = tid; i < 4 * n4; i += 256) {
-        uint32_t key = 0xFFFFFFFFu;   // outside the grid (or padding): above every key, never ranked
-        if (i < n0) {
+    // one pass over the keypoints: the level-0 count is the number of octave-0 keypoints (they come first,
+    // src/ORBextractor.cc:1290-1333), the grid count the number of valid keys; both by wave ballots, one
+    // LDS atomic per wave (per-key atomics on one word, or a binary search of dependent global loads,
+    // serialised)
+    for (int i = tid; i < ((n + 3) & ~3); i += 256) {
+        uint32_t key = 0xFFFFFFFFu;   // another octave, outside the grid, or padding: above every key
+        bool l0 = false;
+        if (i < n && k[i].octave == 0) {
+            l0 = true;
             const int px = (int)roundf((k[i].x - G.min_x) * G.grid_w_inv);
             const int py = (int)roundf((k[i].y - G.min_y) * G.grid_h_inv);
-            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows) {   // PosInGrid
+            if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows)   // PosInGrid
                 key = ((uint32_t)(px * kGridRows + py) << 16) | (uint32_t)i;
-                atomicAdd(&s_ng, 1);
-            }
         }
         keys[i] = key;
+        const unsigned long long b0 = __ballot(l0), bg = __ballot(key != 0xFFFFFFFFu);
+        if (lane == 0) {
+            atomicAdd(&s_n0, __popcll(b0));
+            atomicAdd(&s_ng, __popcll(bg));
+        }
     }
     __syncthreads();
+    const int n0 = s_n0;
+    const int n4 = (n0 + 3) >> 2;
     const uint4* k4 = (const uint4*)keys;
     for (int i = tid; i < n0; i += 256) {
         const uint32_t key = keys[i];
