@@ -1867,13 +1867,19 @@ constexpr uint32_t kRoundBits = 0x4B400000u;
 
 // blurred value at patch row 18 + yy, column 18 + xx (|xx|, |yy| <= 19, given as kRoundMagic
 // bits by, bx): sum_t k[t] * rowblur[y+t][x], + 2^15 (the >> 16 rounding) folded into the sum.
-// The dword index (18 + xx) * kTP + ((18 + yy) >> 1) is kBlurIdx0 + (by >> 1) + bx * kTP in
-// wrapping u32 arithmetic (bx as its low 24 bits, 0x400000 + xx).
-constexpr uint32_t kBlurIdx0 = 9u - (kRoundBits >> 1) + (18u - (kRoundBits & 0xFFFFFFu)) * (uint32_t)kTP;
-__device__ __forceinline__ uint32_t blur_acc(const uint32_t* rowT, uint32_t by, uint32_t bx)
+// The dword index is (18 + xx) * kTP + ((18 + yy) >> 1), in wrapping u32 arithmetic on the bits of
+// bx (its low 24 bits are 0x400000 + xx) and by (bits 1..23: 0x200000 + ((18 + yy) >> 1) - 9).
+// The LDS byte address in three VALU: bfe of by's bits 1..23 (0x200000 + (yy >> 1)), shifted and added to
+// mad24(bx, 4 kTP, C) with C = rowT + 4 (9 - 0x200000 + (18 - 0x400000) kTP) (mod 2^32); the compiler's
+// form of (by >> 1) + bx * kTP + rowT took five.
+constexpr uint32_t kBlurByte0 = 4u * (9u - 0x200000u + (18u - 0x400000u) * (uint32_t)kTP);
+__device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t bx)
 {
-    const uint32_t idx = kBlurIdx0 + (by >> 1) + __umul24(bx, (uint32_t)kTP);   // < 40 * kTP
-    const uint32_t* col = rowT + idx;
+    const uint32_t t = __umul24(bx, 4u * (uint32_t)kTP) + C, f = __builtin_amdgcn_ubfe(by, 1, 23);
+    uint32_t a;
+    // one v_lshl_add_u32 (the compiler rewrites (f << 2) + t as (by << 1) & mask plus an add)
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"(f), "v"(t));
+    const __attribute__((address_space(3))) uint32_t* col = (const __attribute__((address_space(3))) uint32_t*)(uintptr_t)a;
     const uint32_t d0 = col[0], d1 = col[1], d2 = col[2], d3 = col[3];
     // even y: rows y..y+6 = (d0.lo d0.hi d1.lo d1.hi d2.lo d2.hi d3.lo); odd y: (d0.hi .. d3.hi)
     const bool odd = by & 1u;
@@ -2153,6 +2159,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         glibc_sincosf_pair(ang, &b, &a);   // a = cosf, b = sinf (src/ORBextractor.cc:148)
 #endif
         // GaussianBlur's u8 saturation: min(t0, 255) < min(t1, 255) iff t0 < min(t1, 255)
+        const uint32_t cblur = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)rowT + kBlurByte0;
         unsigned long long words[4];
 #pragma unroll
         for (int wd = 0; wd < 4; ++wd) {
@@ -2162,7 +2169,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                 const float px = ppx[2 * wd + e], py = ppy[2 * wd + e];
                 const uint32_t by = __float_as_uint(__builtin_fmaf(px, b, py * a) + kRoundMagic);
                 const uint32_t bx = __float_as_uint(__builtin_fmaf(px, a, -(py * b)) + kRoundMagic);
-                t2[e] = blur_acc(rowT, by, bx) >> 16;
+                t2[e] = blur_acc(cblur, by, bx) >> 16;
             }
             words[wd] = __ballot(t2[0] < (t2[1] < 255u ? t2[1] : 255u));
         }
