@@ -65,7 +65,9 @@ __device__ __forceinline__ ushort2_t as_us2(uint32_t v)
 constexpr int kPyrRows = ORBX_PYR_ROWS;
 constexpr int kPyrNT = ORBX_PYR_NT;   // threads per pyramid workgroup
 
-template <bool kWin>
+// kA: every staged source row starts 4-byte aligned in LDS (source pitch and base multiples of 4, always
+// so for levels >= 1), so a lane's realignment shift is the same on every row
+template <bool kWin, bool kA>
 __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
                                                        const int2* __restrict__ xtab,
                                                        const int2* __restrict__ ytab, int lp)
@@ -142,10 +144,19 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
                 sel[k] = (uint32_t)(x0[k] - x0[0]) | 0x0C00u | ((uint32_t)(x1[k] - x0[0]) << 16) | 0x0C000000u;
                 ak[k] = a0[k] | (a1[k] << 16);
             }
+            const uint32_t xo = (uint32_t)x0[0] & ~3u, xw = (uint32_t)x0[0] & 3u;
             auto hrow = [&](int r, uint32_t h[4]) {
-                const uint32_t A = rowb(r) + (uint32_t)x0[0];
-                const uint32_t* qd = (const uint32_t*)(S + (A & ~3u));
-                const uint32_t d0 = qd[0], d1 = qd[1], d2 = qd[2], wo = A & 3u;
+                uint32_t A, wo;
+                if constexpr (kA) {   // one add per row: the row offset is block-uniform, the shift per lane
+                    A = rowb(r) + xo;
+                    wo = xw;
+                } else {
+                    A = rowb(r) + (uint32_t)x0[0];
+                    wo = A & 3u;
+                    A &= ~3u;
+                }
+                const uint32_t* qd = (const uint32_t*)(S + A);
+                const uint32_t d0 = qd[0], d1 = qd[1], d2 = qd[2];
                 const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, wo), e1 = __builtin_amdgcn_alignbyte(d2, d1, wo);
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
@@ -181,7 +192,12 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
                 }
                 uint32_t acc[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) acc[k] = __umul24(h1[k], b1) + (__umul24(h0[k], b0) + (1u << 23));
+                for (int k = 0; k < 4; ++k) {
+                    // two v_mad_u32_u24 (the compiler's form is two multiplies and an add3)
+                    uint32_t t;
+                    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(t) : "v"(h0[k]), "s"(b0), "v"(1u << 23));
+                    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(acc[k]) : "v"(h1[k]), "s"(b1), "v"(t));
+                }
                 const uint32_t packed = __builtin_amdgcn_perm(acc[1], acc[0], 0x0C0C0703u) |
                                         __builtin_amdgcn_perm(acc[3], acc[2], 0x07030C0Cu);
                 *reinterpret_cast<uint32_t*>(drow0 + (size_t)rr * D.pitch + dx0) = packed;
@@ -226,10 +242,13 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         static const int narrow = getenv("ORBX_PYR_NARROW") ? atoi(getenv("ORBX_PYR_NARROW")) : 1;
         const int q = (g.lv[l].w + 3) >> 2;
         const int nt = narrow ? std::min(kPyrNT, (q + 63) & ~63) : kPyrNT;
-        if (g.lv[l].pyr_win)
-            hipLaunchKernelGGL(k_pyramid_level<true>, grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
+        const bool al = l >= 2 || (((uintptr_t)p.in | (uintptr_t)p.in_pitch | (uintptr_t)p.in_fstride) & 3) == 0;
+        if (g.lv[l].pyr_win && al)
+            hipLaunchKernelGGL((k_pyramid_level<true, true>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
+        else if (g.lv[l].pyr_win)
+            hipLaunchKernelGGL((k_pyramid_level<true, false>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
         else
-            hipLaunchKernelGGL(k_pyramid_level<false>, grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
+            hipLaunchKernelGGL((k_pyramid_level<false, false>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
     }
 }
 
