@@ -103,6 +103,18 @@ orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int
                                       orbx_keypoint* d_kps, uint8_t* d_desc, int* d_counts, int cap,
                                       void* stream);
 
+/* The same extraction as orbx_extract_batch_device, issued one stage at a time so that a caller can
+ * software-pipeline batches across streams (the VALU-bound FAST / describe stages of one batch beside
+ * the latency-bound pyramid / quadtree stages of others).  stage 0: pyramid (and the counts reset),
+ * 1: FAST, 2: quadtree (DistributeOctTree; writes d_counts), 3: describe (writes d_kps / d_desc).
+ * Every stage takes the batch's full arguments and runs on its own `stream`; the caller orders the
+ * four stages of a batch (events) and starts stage 0 of the handle's next batch only after stage 3 of
+ * this one has completed (the stages share the handle's workspace).  Stage 0 sizes the workspace for
+ * rows x cols x batch; later stages with other sizes return ORBX_EINVAL. */
+orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* d_imgs, int batch, int rows,
+                                      int cols, size_t step, size_t frame_stride, orbx_keypoint* d_kps,
+                                      uint8_t* d_desc, int* d_counts, int cap, void* stream);
+
 /* Wait for the work queued on `stream` (NULL = HIP null stream) and
  * return the device-side status (ORBX_ENOSPC when a frame exceeded `cap`). */
 orbx_status orbx_sync(orbx_handle* h, void* stream);

@@ -701,6 +701,47 @@ orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int
     return run_pipeline(h, P, batch, d_kps, d_desc, d_counts, cap, s);
 }
 
+orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* d_imgs, int batch, int rows, int cols,
+                                      size_t step, size_t frame_stride, orbx_keypoint* d_kps, uint8_t* d_desc,
+                                      int* d_counts, int cap, void* stream)
+{
+    if (!h || stage < 0 || stage > 3 || !d_imgs || batch <= 0 || !d_kps || !d_desc || !d_counts || cap <= 0)
+        return ORBX_EINVAL;
+    if (step < (size_t)cols || frame_stride < step * (size_t)rows) return ORBX_EINVAL;
+    DeviceGuard guard(h->device);
+    orbx_status st;
+    if (stage == 0) {   // sizes the geometry and workspace; later stages must match them
+        if ((st = ensure_geometry(h, rows, cols)) != ORBX_OK) return st;
+        if ((st = ensure_batch(h, batch)) != ORBX_OK) return st;
+    } else if (!h->geom_ok || h->grows != rows || h->gcols != cols || batch > h->batch_cap) {
+        return ORBX_EINVAL;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const Geometry& g = h->geom;
+    ExtractBufs b = bufs(h);
+    FramePtrs P{d_imgs, frame_stride, (int)step, h->d_pyr, (size_t)g.pyr_bytes};
+    switch (stage) {
+    case 0:
+        hipMemsetAsync(d_counts, 0, sizeof(int) * batch, s);
+        hipMemsetAsync(h->d_status, 0, sizeof(int), s);
+        launch_pyramid(g, b, P, batch, s);
+        break;
+    case 1:
+        launch_fast(g, b, P, batch, s);
+        break;
+    case 2:
+        launch_quadtree(g, b, d_counts, batch, s);
+        break;
+    default:
+        launch_describe(g, b, P, d_kps, d_desc, cap, batch, s);
+        h->last = P;
+        h->last_batch = batch;
+        std::fill(h->level_cached.begin(), h->level_cached.end(), false);
+        break;
+    }
+    return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
 orbx_status orbx_sync(orbx_handle* h, void* stream)
 {
     if (!h) return ORBX_EINVAL;

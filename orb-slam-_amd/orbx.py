@@ -33,7 +33,7 @@ TOP2, FULL_U16 = 0, 1
 
 EXPORTED = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_capacity", "orbx_extract", "orbx_get_level",
-    "orbx_extract_batch_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
+    "orbx_extract_batch_device", "orbx_extract_stage_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
     "orbx_debug_pyramid", "orbx_debug_candidates", "orbx_debug_launches", "orbm_descriptor_distance", "orbm_allpairs_device", "orbm_allpairs",
     "orbm_search_init_batch_device", "orbm_search_for_initialization_device", "orbm_search_for_initialization",
     "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
@@ -164,6 +164,8 @@ def _load():
     L.orbx_get_level.argtypes = [vp, C.c_int, P(u8p), i32p, i32p, P(C.c_size_t)]
     L.orbx_extract_batch_device.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_size_t, vp, vp,
                                             vp, C.c_int, vp]
+    L.orbx_extract_stage_device.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_size_t, vp,
+                                            vp, vp, C.c_int, vp]
     L.orbx_sync.argtypes = [vp, vp]
     L.orbx_set_timing.argtypes = [vp, C.c_int]
     L.orbx_get_stage_times.argtypes = [vp, f32p, C.c_int]
@@ -337,6 +339,15 @@ class ORBextractor:
         rc = lib.orbx_extract_batch_device(self._h, _ptr(imgs), B, H, W, imgs.stride(1), imgs.stride(0), _ptr(kps),
                                            _ptr(desc), _ptr(counts), cap, _stream(stream))
         _check("orbx_extract_batch_device", rc)
+
+    def extract_stage_device(self, stage, imgs, kps, desc, counts, stream=None):
+        """One stage (0 pyramid, 1 FAST, 2 quadtree, 3 describe) of extract_batch_device, on `stream`; the caller
+        orders a batch's stages across streams (orbx_extract_stage_device)."""
+        B, H, W = imgs.shape
+        cap = kps.shape[1]
+        rc = lib.orbx_extract_stage_device(self._h, int(stage), _ptr(imgs), B, H, W, imgs.stride(1), imgs.stride(0),
+                                           _ptr(kps), _ptr(desc), _ptr(counts), cap, _stream(stream))
+        _check("orbx_extract_stage_device", rc)
 
     def stereo_batch_device(self, kps, desc, counts, left, right, bf, fx, u_right=None, depth=None, n_good=None,
                             stream=None):
