@@ -1817,6 +1817,17 @@ constexpr int kDescWaves = ORBX_DESC_WAVES;
 // load read neighbouring raw dwords (distinct LDS banks).
 __constant__ uint16_t c_blur_items[192] = {2,3,4,5,6,257,258,259,260,261,262,263,513,514,515,516,517,518,519,768,769,770,771,772,773,774,775,776,1024,1025,1026,1027,1028,1029,1030,1031,1032,1280,1281,1282,1283,1284,1285,1286,1287,1288,1536,1537,1538,1539,1540,1541,1542,1543,1544,1545,1792,1793,1794,1795,1796,1797,1798,1799,1800,1801,2048,2049,2050,2051,2052,2053,2054,2055,2056,2057,2304,2305,2306,2307,2308,2309,2310,2311,2312,2313,2560,2561,2562,2563,2564,2565,2566,2567,2568,2569,2816,2817,2818,2819,2820,2821,2822,2823,2824,2825,3072,3073,3074,3075,3076,3077,3078,3079,3080,3081,3328,3329,3330,3331,3332,3333,3334,3335,3336,3337,3584,3585,3586,3587,3588,3589,3590,3591,3592,3593,3840,3841,3842,3843,3844,3845,3846,3847,3848,3849,4096,4097,4098,4099,4100,4101,4102,4103,4104,4352,4353,4354,4355,4356,4357,4358,4359,4360,4609,4610,4611,4612,4613,4614,4615,4616,4865,4866,4867,4868,4869,4870,4871,5122,5123,5124,5125,5126,5127,5379,5380,5381,5382,65535,65535,65535};
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+// GaussianBlur's 7 taps starting at byte `off` of four consecutive raw dwords: the weight bytes of dword d
+__host__ __device__ constexpr uint32_t blur_wshift(int off, int d)
+{
+    constexpr uint32_t k[7] = {18, 34, 49, 55, 49, 34, 18};
+    uint32_t w = 0;
+    for (int b = 0; b < 4; ++b) {
+        const int t = 4 * d + b - off;
+        if (t >= 0 && t < 7) w |= k[t] << (8 * b);
+    }
+    return w;
+}
 constexpr int kPattern[1024] = {
 #include "orb_pattern.inc"
 };
@@ -2134,30 +2145,55 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
 #ifdef ORBX_DIAG_NOHPASS   // diagnostic build (wrong results): the horizontal pass's cost
         if (lane < 32) rowT[lane * 23] = raw32[lane];
 #else
+        // Rows that all start at the same byte shift S (csp == 0: the level pitch is a multiple of 4, or the
+        // reflect-101 byte path) skip the realignment: output column j is a dot4 of each raw dword with the
+        // kernel shifted by S + j bytes, still 10 dot4 per row (2 or 3 per column) and no alignbyte.
+        auto hpass = [&](auto s_tag) {
+            constexpr int S = decltype(s_tag)::value;   // -1: per-row shifts
 #pragma unroll
-        for (int it = 0; it < 3; ++it) {
-            if (bitem[it] == 0xFFFF) break;
-            const int rp = bitem[it] >> 8, cg = bitem[it] & 0xFF;
-            uint32_t o[2][4];
+            for (int it = 0; it < 3; ++it) {
+                if (bitem[it] == 0xFFFF) break;
+                const int rp = bitem[it] >> 8, cg = bitem[it] & 0xFF;
+                uint32_t o[2][4];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int r = 2 * rp + e;
-                const uint32_t sh = ((uint32_t)csb + __umul24((uint32_t)r, (uint32_t)csp)) & 3u;
-                const uint32_t* rr = raw32 + r * (kRawP / 4) + cg;
-                const uint32_t W0 = rr[0], W1 = rr[1], W2 = rr[2], W3 = rr[3];
-                const uint32_t R[3] = {__builtin_amdgcn_alignbyte(W1, W0, sh), __builtin_amdgcn_alignbyte(W2, W1, sh),
-                                       __builtin_amdgcn_alignbyte(W3, W2, sh)};
+                for (int e = 0; e < 2; ++e) {
+                    const int r = 2 * rp + e;
+                    const uint32_t* rr = raw32 + r * (kRawP / 4) + cg;
+                    const uint32_t W[4] = {rr[0], rr[1], rr[2], rr[3]};
+                    if constexpr (S < 0) {
+                        const uint32_t sh = ((uint32_t)csb + __umul24((uint32_t)r, (uint32_t)csp)) & 3u;
+                        const uint32_t R[3] = {__builtin_amdgcn_alignbyte(W[1], W[0], sh),
+                                               __builtin_amdgcn_alignbyte(W[2], W[1], sh),
+                                               __builtin_amdgcn_alignbyte(W[3], W[2], sh)};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    uint32_t acc = __builtin_amdgcn_udot4(R[0], kW[j][0], 0u, false);
-                    acc = __builtin_amdgcn_udot4(R[1], kW[j][1], acc, false);
-                    if (j >= 2) acc = __builtin_amdgcn_udot4(R[2], kW[j][2], acc, false);
-                    o[e][j] = acc;
+                        for (int j = 0; j < 4; ++j) {
+                            uint32_t acc = __builtin_amdgcn_udot4(R[0], kW[j][0], 0u, false);
+                            acc = __builtin_amdgcn_udot4(R[1], kW[j][1], acc, false);
+                            if (j >= 2) acc = __builtin_amdgcn_udot4(R[2], kW[j][2], acc, false);
+                            o[e][j] = acc;
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            uint32_t acc = 0u;
+#pragma unroll
+                            for (int d = 0; d < 4; ++d) {
+                                const uint32_t w = blur_wshift(S + j, d);   // folds to a constant
+                                if (w) acc = __builtin_amdgcn_udot4(W[d], w, acc, false);
+                            }
+                            o[e][j] = acc;
+                        }
+                    }
                 }
-            }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
-        }
+                for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
+            }
+        };
+        if (csp != 0) hpass(std::integral_constant<int, -1>{});
+        else if (csb == 0) hpass(std::integral_constant<int, 0>{});
+        else if (csb == 1) hpass(std::integral_constant<int, 1>{});
+        else if (csb == 2) hpass(std::integral_constant<int, 2>{});
+        else hpass(std::integral_constant<int, 3>{});
 #endif
         wave_lds_sync();   // raw is free: start the next keypoint's patch, it lands under BRIEF
         nvalid = lookup(jj + 1, nl, npk);
