@@ -2218,14 +2218,16 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         unsigned long long words[4];
 #pragma unroll
         for (int wd = 0; wd < 4; ++wd) {
+            // the test's two samples as packed f32 pairs (v_pk_mul / v_pk_fma / v_pk_add: the same roundings
+            // as the scalar statements, two samples per instruction)
+            typedef float f2v __attribute__((ext_vector_type(2)));
+            const f2v PX = {ppx[2 * wd], ppx[2 * wd + 1]}, PY = {ppy[2 * wd], ppy[2 * wd + 1]};
+            const f2v va = {a, a}, vb = {b, b}, mg = {kRoundMagic, kRoundMagic};
+            const f2v BY = __builtin_elementwise_fma(PX, vb, PY * va) + mg;
+            const f2v BX = __builtin_elementwise_fma(PX, va, -(PY * vb)) + mg;
             uint32_t t2[2];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const float px = ppx[2 * wd + e], py = ppy[2 * wd + e];
-                const uint32_t by = __float_as_uint(__builtin_fmaf(px, b, py * a) + kRoundMagic);
-                const uint32_t bx = __float_as_uint(__builtin_fmaf(px, a, -(py * b)) + kRoundMagic);
-                t2[e] = blur_acc(cblur, by, bx) >> 16;
-            }
+            for (int e = 0; e < 2; ++e) t2[e] = blur_acc(cblur, __float_as_uint(BY[e]), __float_as_uint(BX[e])) >> 16;
             words[wd] = __ballot(t2[0] < (t2[1] < 255u ? t2[1] : 255u));
         }
 #if ORBX_DESC_DEFER == 0
