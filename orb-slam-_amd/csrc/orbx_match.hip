@@ -832,13 +832,28 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (check_ori) {   // ComputeThreeMaxima + removal, src/ORBmatcher.cc:562-580
-        int ind1 = -1, ind2 = -1, ind3 = -1, max1 = 0, max2 = 0, max3 = 0;
-        for (int i = 0; i < 30; ++i) {
-            const int s = s_hist[i];
-            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-            else if (s > max3) { max3 = s; ind3 = i; }
+        // the 30 bins in one LDS read (lane = bin), then three wave maxima of (count, 31 - bin): the
+        // sequential scan's first-max-wins order is the smallest bin among equal counts
+        const int hv = lane < 30 ? s_hist[lane] : 0;
+        uint32_t key = lane < 30 && hv > 0 ? ((uint32_t)hv << 5) | (uint32_t)(31 - lane) : 0u;
+        int ind[3] = {-1, -1, -1}, mx[3] = {0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            uint32_t m = key;
+            m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0xB1, 0xF, 0xF, true));
+            m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x4E, 0xF, 0xF, true));
+            m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x141, 0xF, 0xF, true));
+            m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x140, 0xF, 0xF, true));
+            m = max(max((uint32_t)__builtin_amdgcn_readlane((int)m, 0), (uint32_t)__builtin_amdgcn_readlane((int)m, 16)),
+                    max((uint32_t)__builtin_amdgcn_readlane((int)m, 32), (uint32_t)__builtin_amdgcn_readlane((int)m, 48)));
+            if (m) {
+                ind[r] = 31 - (int)(m & 31u);
+                mx[r] = (int)(m >> 5);
+                if (key == m) key = 0u;
+            }
         }
+        int ind1 = ind[0], ind2 = ind[1], ind3 = ind[2];
+        const int max1 = mx[0], max2 = mx[1], max3 = mx[2];
         if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
         for (int i = lane; i < n10; i += 64) {
@@ -850,14 +865,26 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    int nmatches = 0;
-    for (int i = lane; i < n10; i += 64) {
-        const int v = (int)m12[i];
-        out[i] = v;
-        nmatches += v >= 0;
-        if (pv && v >= 0) pv[i] = make_float2(k2[v].x, k2[v].y);   // update vbPrevMatched (:580-584)
+    int nmatches = 0;   // wave-uniform: ballot counts
+    for (int i0 = 0; i0 < n10; i0 += 256) {   // four rows of 64 at a time: their k2 loads in flight together
+        int v[4];
+        float2 kp[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + lane;
+            v[u] = i < n10 ? (int)m12[i] : -1;
+            if (pv && v[u] >= 0) kp[u] = make_float2(k2[v[u]].x, k2[v[u]].y);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 64 * u + lane;
+            if (i < n10) {
+                out[i] = v[u];
+                if (pv && v[u] >= 0) pv[i] = kp[u];   // update vbPrevMatched (:580-584)
+            }
+            nmatches += __popcll(__ballot(v[u] >= 0));
+        }
     }
-    for (int o = 32; o > 0; o >>= 1) nmatches += __shfl_xor(nmatches, o);
     if (lane == 0) nm_out[pair] = nmatches;
 #ifdef ORBX_SI_PROF
     const long long pt3 = clock64();
