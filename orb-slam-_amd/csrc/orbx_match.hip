@@ -680,6 +680,9 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
         }
         return !scan && bd <= 50 && (float)bd < (float)bd2 * nnratio;   // TH_LOW, mfNNratio
     };
+#ifdef ORBX_SI_PROF
+    int prof_chunks = 0, prof_scans = 0;   // exact-prefix chunks and full-window scans of the greedy pass
+#endif
     uint32_t stamp = 0;   // round stamp of the writer tables (tables start at 0)
     int base = 0;
     while (base < n10) {
@@ -758,6 +761,10 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
         }
         wave_lds_sync();
         base += lim;
+#ifdef ORBX_SI_PROF
+        prof_chunks += 1;
+        prof_scans += sm ? 1 : 0;
+#endif
         if (sm) {
             // step `base`: re-enumerate its window (global grid of frame fb) and scan it with
             // the current mdist: lane-local best (first min) and second, best = min (dist,
@@ -889,6 +896,8 @@ __global__ __launch_bounds__(256) void k_si_greedy(const orbx_keypoint* __restri
 #ifdef ORBX_SI_PROF
     const long long pt3 = clock64();
     if (lane == 0) {   // phase cycles (staging, greedy loop, bins+filter+output) over the unused tail
+        out[cap - 6] = prof_chunks;
+        out[cap - 5] = prof_scans;
         out[cap - 4] = (int)(pt1 - pt0);
         out[cap - 3] = (int)(pt2 - pt1);
         out[cap - 2] = (int)(pt3 - pt2);

@@ -21,6 +21,8 @@ for it in range(3):
     m12, nm = m.search_for_initialization_batch(kps, desc, counts, pa, pb, 376, 1241, 100, stream=s)
 ex.sync(s)
 t = m12.view(B - 1, cap)[:, cap - 4:].cpu().numpy()
+c = m12.view(B - 1, cap)[:, cap - 6:cap - 4].cpu().numpy()
+print("chunks, full-window scans per pair:", c[:6].tolist(), "mean", c.mean(axis=0).tolist())
 print("staging cycles, loop cycles, post cycles, n10 (per pair):")
 print(t[:6])
 print("loop cycles per step: %.0f" % (t[:, 1] / t[:, 3]).mean())
