@@ -1053,10 +1053,10 @@ template <int QT_NT, int QT_KPT, bool kG>
 #define ORBX_QT0_WPE 4
 #endif
 #ifndef ORBX_QT1_WPE
-#define ORBX_QT1_WPE 5
+#define ORBX_QT1_WPE 4
 #endif
 #ifndef ORBX_QT2_WPE
-#define ORBX_QT2_WPE 6
+#define ORBX_QT2_WPE 5
 #endif
 // Minimum waves per SIMD (HIP's second __launch_bounds__ argument), i.e. a VGPR budget per template:
 //   <512,16> (level 0) 4: 128 VGPRs (7 dwords spilled) instead of the compiler's 172, so two workgroups
@@ -1064,6 +1064,8 @@ template <int QT_NT, int QT_KPT, bool kG>
 //   <512,8>  (level 1) 5: 96 VGPRs (5 spilled) instead of 128: 43.8 -> 42.5 us;
 //   <256,4>  (levels 2-7) 6: 80 VGPRs (3 spilled) instead of 100: 88 -> 70 us.
 // Smaller workgroups also find room beside describe's sooner under the pipeline (+1.5% frames/s together).
+// Round 3: levels 1 and 2-7 at 128 / 96 VGPRs (4 / 5 waves per SIMD, no spill): their occupancy is set by
+// LDS and workgroup waves anyway (2 and 5 workgroups per CU), quadtree 0.165 -> 0.164 ms.
 // FAST at 5 (94 VGPRs, no spill) measured slower (485 -> 495 us) and keeps the compiler's choice.
 //
 // kG: the node arrays live in the level's global region (LevelGeom::qtg_off) instead of LDS, with 32-bit
