@@ -121,6 +121,7 @@ struct orbx_handle {
     Cell* d_cells = nullptr;
     int2* d_xtab = nullptr;
     int2* d_ytab = nullptr;
+    int4* d_pyrbt = nullptr;   // K1 small-batch band tables
 
     // batch workspace
     int batch_cap = 0;
@@ -315,6 +316,8 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         L.patch_size = (float)(int)(31 * t.scale[l]);   // :1013
     }
     g.ncells = (int)cells.size();
+    std::vector<int4> pyrbt;
+    if (!pyr_plan(g, yt.data(), pyrbt)) return ORBX_EINVAL;
     fast_groups(g);
     g.slots_per_frame = slot;
     g.out_per_frame = out;
@@ -330,7 +333,7 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
 
     // once per image size: the tables go up on the handle's own stream (never the legacy null stream)
     if (!dalloc(h, h->d_geom, 1) || !dalloc(h, h->d_cells, cells.size()) || !dalloc(h, h->d_xtab, xt.size()) ||
-        !dalloc(h, h->d_ytab, yt.size()))
+        !dalloc(h, h->d_ytab, yt.size()) || !dalloc(h, h->d_pyrbt, pyrbt.size()))
         return ORBX_ENOMEM;
     // on a pooled host-call stream (high priority, orbx_host.hip), so that a handle used only through
     // orbx_extract_batch_device never creates a stream of its own (each takes one of the process's
@@ -343,6 +346,8 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         hipMemcpyAsync(h->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice, s);
         if (!xt.empty()) hipMemcpyAsync(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice, s);
         if (!yt.empty()) hipMemcpyAsync(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice, s);
+        if (!pyrbt.empty())
+            hipMemcpyAsync(h->d_pyrbt, pyrbt.data(), sizeof(int4) * pyrbt.size(), hipMemcpyHostToDevice, s);
         if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
     }
     h->geom = g;
@@ -379,6 +384,7 @@ ExtractBufs bufs(orbx_handle* h)
     b.cells = h->d_cells;
     b.xtab = h->d_xtab;
     b.ytab = h->d_ytab;
+    b.pyr_bands = h->d_pyrbt;
     b.slots = h->d_slots;
     b.cell_counts = h->d_cell_counts;
     b.spill = h->d_spill;
@@ -496,6 +502,7 @@ void orbx_destroy(orbx_handle* h)
     dfree(h->d_cells);
     dfree(h->d_xtab);
     dfree(h->d_ytab);
+    dfree(h->d_pyrbt);
     dfree(h->d_pyr);
     dfree(h->d_slots);
     dfree(h->d_cell_counts);
@@ -552,7 +559,13 @@ orbx_status orbx_debug_launches(orbx_handle* h, int rows, int cols, int batch, i
     QtGroup grp[kQtMaxGroups];
     // the pyramid's launches each read one level (counts[4]: bit mask): one launch per level from the one
     // before it
-    const int c[5] = {g.nlevels - 1, fast, qt_plan(g, batch, grp), 1, (1 << (g.nlevels - 1)) - 1};
+    const bool fused = batch <= kLatencyMaxBatch && g.pyr_ngroups > 0;   // launch_pyramid's choice
+    int srcmask = (1 << (g.nlevels - 1)) - 1;
+    if (fused) {
+        srcmask = 0;
+        for (int i = 0; i < g.pyr_ngroups; ++i) srcmask |= 1 << g.pg[i].s;
+    }
+    const int c[5] = {fused ? g.pyr_ngroups : g.nlevels - 1, fast, qt_plan(g, batch, grp), 1, srcmask};
     for (int i = 0; i < n; ++i) counts[i] = i < 5 ? c[i] : 0;
     return ORBX_OK;
 }

@@ -226,8 +226,318 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
     }
 }
 
+// ---------------------------------------------------------------------------
+// K1 for small batches (the per-frame host path, batch <= kLatencyMaxBatch): levels s+1..s+n from level s
+// in one launch, so a single frame's pyramid is one or two launches instead of a chain of seven (each
+// ~4.6 us of launch latency for a 640x480 frame).  Large batches keep one launch per level: there the
+// kernel is VALU-bound and the bands' halo rows would add work.
+// ---------------------------------------------------------------------------
+constexpr int kPyrMaxNT = 512;
+
+constexpr int kPyrChunk = 8;   // output rows per work item (unrolled; their row-table entries loaded up front)
+
+// Rows [e.x, e.y] of level D from the source rows held in LDS (row r of the source level at LDS byte
+// (r - sfirst) * slp + ((ssh0 + (r - sfirst) * ssp) & 15)), into LDS (dst, pitch dlp, from row e.x; unless
+// `last`) and, for the rows this block owns ([e.z, e.w]), into the level's global image.
+__device__ __forceinline__ void pyr_rows(const LevelGeom& Dg, const int2* __restrict__ xtab,
+                                         const int2* __restrict__ ytab, const uint8_t* S, int slp, int sfirst,
+                                         uint32_t ssh0, uint32_t ssp, uint8_t* dst, int dlp, int4 e, bool last,
+                                         uint8_t* gimg, int nt, int split, int wave, int lane)
+{
+    // the level's fields in registers: the stores below could alias the geometry as far as the compiler
+    // knows, which would reload them after every store
+    const int w = Dg.w, pitch = Dg.pitch, xoff = Dg.xtab_off, yoff = Dg.ytab_off, win = Dg.pyr_win;
+    auto rowb = [&](int r) -> uint32_t {
+        const int k = r - sfirst;
+        return (uint32_t)(k * slp) + ((ssh0 + (uint32_t)k * ssp) & 15u);
+    };
+    // work items: (chunk of up to kPyrChunk rows, 4-column group), a wave's 64 groups in one chunk, so
+    // every wave walks its rows in lock-step (row tables by scalar loads); on narrow levels the threads
+    // beyond the first chunk take further chunks instead of idling
+    const int q = (w + 3) >> 2, qp = (q + 63) & ~63;
+    const int nrows = e.y - e.x + 1;
+    const int nch = max((nrows + kPyrChunk - 1) / kPyrChunk, split ? min(nrows, nt / qp) : 1);
+    const int rpc = (nrows + nch - 1) / nch;   // <= kPyrChunk
+    const int items = qp * nch;
+    for (int w0 = wave * 64; w0 < items; w0 += nt) {
+        const int c = w0 / qp;
+        const int g = w0 - c * qp + lane;
+        const int r0 = e.x + c * rpc, nr = min(e.y - r0 + 1, rpc);
+        if (g >= q || nr <= 0) continue;
+        const int dx0 = g * 4;
+        int2 yt[kPyrChunk];
+#pragma unroll
+        for (int k = 0; k < kPyrChunk; ++k) yt[k] = ytab[yoff + r0 + min(k, nr - 1)];
+        // every product fits a 24 x 24 -> 32-bit multiply (v_mul_u32_u24, full rate; the compiler
+        // otherwise emits the quarter-rate v_mul_lo_u32 for h * b).  The two taps keep separate
+        // addresses: byte reads at x0 and x0 + 1 merge into an unaligned ds_read_u16, which
+        // measured 3.5x slower for the whole kernel.
+        int x0[4], x1[4];
+        uint32_t a0[4], a1[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int2 xt = xtab[xoff + min(dx0 + k, w - 1)];
+            x0[k] = xt.x & 0xFFFF;
+            x1[k] = (int)((uint32_t)xt.x >> 16);
+            a0[k] = (uint32_t)xt.y & 0xFFFFu;
+            a1[k] = (uint32_t)xt.y >> 16;
+        }
+        auto put = [&](int rr, uint32_t packed) {
+            if (!last) *reinterpret_cast<uint32_t*>(dst + (rr - e.x) * dlp + dx0) = packed;
+            // columns past the level width land in the row's pitch padding (pitch = align64(w))
+            if (rr >= e.z && rr <= e.w) *reinterpret_cast<uint32_t*>(gimg + (size_t)rr * pitch + dx0) = packed;
+        };
+        if (win) {   // block-uniform
+            // The group's 8 taps lie in the 8 bytes from x0[0] (LevelGeom::pyr_win, checked on the host):
+            // per source row three dword reads, realigned to x0[0] by two alignbytes; each column's tap
+            // pair is one v_perm into a u16 pair and one v_dot2_u32_u16 with (a0, a1)
+            uint32_t sel[4], ak[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                sel[k] = (uint32_t)(x0[k] - x0[0]) | 0x0C00u | ((uint32_t)(x1[k] - x0[0]) << 16) | 0x0C000000u;
+                ak[k] = a0[k] | (a1[k] << 16);
+            }
+            auto hrow = [&](int r, uint32_t h[4]) {
+                const uint32_t A = rowb(r) + (uint32_t)x0[0];
+                const uint32_t* qd = (const uint32_t*)(S + (A & ~3u));
+                const uint32_t d0 = qd[0], d1 = qd[1], d2 = qd[2], wo = A & 3u;
+                const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, wo), e1 = __builtin_amdgcn_alignbyte(d2, d1, wo);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    h[k] = __builtin_amdgcn_udot2(as_us2(__builtin_amdgcn_perm(e1, e0, sel[k])), as_us2(ak[k]), 0u,
+                                                  false);
+            };
+            // Output rows in order; consecutive rows share a source row (lo(y + 1) == hi(y)) at scale
+            // factors up to 2, and that row's horizontal sums are kept instead of recomputed.  The
+            // vertical sum is taken x4, (4 (h0 b0 + h1 b1) + 2^23) >> 24 = (h0 b0 + h1 b1 + 2^21) >> 22,
+            // so each result is byte 3 of its sum and two v_perm pack four of them; the host checks that
+            // the coefficient sums keep 4 * 255 * sum(a) * sum(b) + 2^23 below 2^32, which also makes
+            // every result <= 255 (no saturation).
+            int cr = -1;
+            uint32_t hc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < kPyrChunk; ++k) {
+                if (k >= nr) break;
+                const int lo = yt[k].x & 0xFFFF, hi = (int)((uint32_t)yt[k].x >> 16);
+                const uint32_t b0 = ((uint32_t)yt[k].y & 0xFFFFu) << 2, b1 = ((uint32_t)yt[k].y >> 16) << 2;
+                uint32_t h0[4], h1[4];
+                if (lo == cr) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) h0[t] = hc[t];
+                } else {
+                    hrow(lo, h0);
+                }
+                if (hi == lo) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) h1[t] = h0[t];
+                } else {
+                    hrow(hi, h1);
+                }
+                uint32_t acc[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[t] = __umul24(h1[t], b1) + (__umul24(h0[t], b0) + (1u << 23));
+                put(r0 + k, __builtin_amdgcn_perm(acc[1], acc[0], 0x0C0C0703u) |
+                                __builtin_amdgcn_perm(acc[3], acc[2], 0x07030C0Cu));
+                cr = hi;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) hc[t] = h1[t];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kPyrChunk; ++k) {
+                if (k >= nr) break;
+                const uint8_t* p0 = S + rowb(yt[k].x & 0xFFFF);
+                const uint8_t* p1 = S + rowb((int)((uint32_t)yt[k].x >> 16));
+                const uint32_t b0 = (uint32_t)yt[k].y & 0xFFFFu, b1 = (uint32_t)yt[k].y >> 16;
+                uint32_t packed = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t h0 = __umul24(p0[x0[t]], a0[t]) + __umul24(p0[x1[t]], a1[t]);
+                    const uint32_t h1 = __umul24(p1[x0[t]], a0[t]) + __umul24(p1[x1[t]], a1[t]);
+                    const uint32_t v = (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
+                    packed |= min(v, 255u) << (8 * t);
+                }
+                put(r0 + k, packed);
+            }
+        }
+    }
+}
+
+// One block per (frame, band): a band is `rows` rows of the group's last level; its band-table entries
+// (Geometry::pg, pyr_plan) name the rows of every level of the group it computes and the rows it owns.
+// Level s's rows arrive in LDS by LDS-DMA (global_load_lds_dwordx4 of the 16-byte chunks that hold each
+// row, so row r sits at LDS byte r * lp + sh_r with sh_r = its start address & 15; 0 for levels >= 1,
+// whose pitch is a multiple of 64).  A chunk is fetched only if it holds a byte of its row: it then lies
+// in the row's own 16-byte aligned span, which cannot cross a page boundary, so no read leaves the
+// caller's allocation.  Levels s+1 .. s+n-1 stay in LDS (two row buffers) for the next level, and each
+// block writes the rows it owns to the pyramid.  Blocks recompute the few rows their neighbours share
+// (about one per level at each band edge) instead of synchronising.
+__global__ __launch_bounds__(kPyrMaxNT) void k_pyramid_fused(const Geometry* __restrict__ G, FramePtrs P, int gi,
+                                                    const int2* __restrict__ xtab, const int2* __restrict__ ytab,
+                                                    const int4* __restrict__ bands)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
+    const PyrGroup& PG = G->pg[gi];
+    const int nt = blockDim.x;
+    const int lb = xcd_block(blockIdx.y + blockIdx.z * gridDim.y, gridDim.y * gridDim.z);
+    const int f = lb / gridDim.y, band = lb - f * gridDim.y;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int s = PG.s, n = PG.n;
+    const int4* B = bands + PG.bt_off + (size_t)band * (n + 1);
+    const int4 e0 = B[0];
+    const int sw = G->lv[s].w;
+    int spitch;
+    const uint8_t* src = level_base(P, G, f, s, spitch);
+    const int lp0 = ((sw + 30) >> 4) << 4;   // the 16-byte chunks spanning a row at any start alignment
+    const int nc = lp0 >> 4;
+    const uintptr_t ra = (uintptr_t)src + (size_t)e0.x * spitch;
+    const uint8_t* gb = (const uint8_t*)(ra & ~(uintptr_t)15);
+    const uint32_t sh0 = (uint32_t)(ra & 15);
+    // row r's offset from gb: sh0 + r * spitch; the chunk split uses the float reciprocal of nc
+    // ((i + 0.5) / nc sits 0.5 / nc from any integer: exact for i < 2^22)
+    const int total = (e0.y - e0.x + 1) * nc;
+    const float inv_nc = 1.0f / (float)nc;
+    for (int i0 = wave * 64; i0 < total; i0 += nt) {
+        const int i = i0 + lane;
+        const int r = (int)(((float)i + 0.5f) * inv_nc), c = i - __mul24(r, nc);
+        const uint32_t ro = sh0 + __umul24((uint32_t)r, (uint32_t)spitch);
+        const uint32_t co = (ro & ~15u) + 16u * (uint32_t)c;
+        if (i < total && co < ro + (uint32_t)sw)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(gb + co),
+                                             (__attribute__((address_space(3))) void*)(s_src + 4 * i0), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint8_t* X = (uint8_t*)s_src;
+    uint8_t* Y = X + PG.lds_x;
+    const uint8_t* S = X;
+    int slp = lp0, sfirst = e0.x;
+    uint32_t ssh0 = sh0, ssp = (uint32_t)spitch;
+    for (int i = 1; i <= n; ++i) {
+        const LevelGeom& D = G->lv[s + i];
+        const int4 e = B[i];
+        const bool last = i == n;
+        uint8_t* dst = (i & 1) ? Y : X;
+        const int dlp = ((D.w + 15) >> 4) << 4;
+        uint8_t* gimg = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off;
+        pyr_rows(D, xtab, ytab, S, slp, sfirst, ssh0, ssp, dst, dlp, e, last, gimg, nt, PG.split, wave, lane);
+        if (last) break;
+        __syncthreads();   // level s+i is whole in LDS; the buffer it was made from is free
+        S = dst;
+        slp = dlp;
+        sfirst = e.x;
+        ssh0 = 0;
+        ssp = 0;
+    }
+}
+
+bool pyr_plan(Geometry& g, const int2* yt, std::vector<int4>& bands)
+{
+    bands.clear();
+    g.pyr_ngroups = 0;
+    if (g.nlevels < 2) return true;
+    if (const char* v = getenv("ORBX_PYR_FUSED"))   // A/B knob: 0 = per-level launches for every batch
+        if (atoi(v) == 0) return true;
+    // group starts (first computed level of each launch): ORBX_PYR_SPLIT="1,4" (A/B knob), default 1,4;
+    // band height (rows of a group's last level per block): ORBX_PYR_BAND, default 4
+    std::vector<int> st;
+    const char* env = getenv("ORBX_PYR_SPLIT");
+    if (env && *env) {
+        for (const char* p = env; *p;) {
+            char* e = nullptr;
+            const long v = strtol(p, &e, 10);
+            if (e == p) break;
+            if (v >= 1 && v < g.nlevels) st.push_back((int)v);
+            p = *e ? e + 1 : e;
+        }
+    } else {
+        st = {1, 4};   // two launches (640x480 host path: 0.147 against 0.150-0.156 ms for 1 or 3 launches)
+    }
+    st.push_back(1);
+    std::sort(st.begin(), st.end());
+    st.erase(std::unique(st.begin(), st.end()), st.end());
+    while (!st.empty() && st.back() >= g.nlevels) st.pop_back();
+    const char* benv = getenv("ORBX_PYR_BAND");
+    const int R = std::max(1, benv && *benv ? atoi(benv) : 4);
+    auto lo = [&](int j, int y) { return yt[g.lv[j].ytab_off + y].x & 0xFFFF; };
+    auto hi = [&](int j, int y) { return (int)((uint32_t)yt[g.lv[j].ytab_off + y].x >> 16); };
+    auto lds_pitch = [&](int j, bool staged) { return staged ? ((g.lv[j].w + 30) >> 4) << 4 : ((g.lv[j].w + 15) >> 4) << 4; };
+    for (size_t gi = 0; gi < st.size(); ++gi) {
+        const int s = st[gi] - 1, b = gi + 1 < st.size() ? st[gi + 1] - 1 : g.nlevels - 1, n = b - s;
+        const int K = (g.lv[b].h + R - 1) / R;
+        // start[j - s][k]: first row of level j owned by band k (k = K: the level height)
+        std::vector<std::vector<int>> start(n + 1, std::vector<int>(K + 1));
+        for (int k = 0; k <= K; ++k) start[n][k] = std::min(k * R, g.lv[b].h);
+        for (int j = b - 1; j > s; --j) {
+            start[j - s][0] = 0;
+            start[j - s][K] = g.lv[j].h;
+            for (int k = 1; k < K; ++k) start[j - s][k] = std::max(start[j - s][k - 1], lo(j + 1, start[j + 1 - s][k]));
+        }
+        PyrGroup& P = g.pg[g.pyr_ngroups];
+        P.s = s;
+        P.n = n;
+        P.rows = R;
+        P.nbands = K;
+        P.bt_off = (int)bands.size();
+        P.lds_x = P.lds_y = 0;
+        int qmax = 0;
+        for (int j = s + 1; j <= b; ++j) qmax = std::max(qmax, (g.lv[j].w + 3) >> 2);
+        P.nt = qmax > 256 ? std::min(kPyrMaxNT, (qmax + 63) & ~63) : 256;
+        // A/B knobs: ORBX_PYR_NT (threads per block), ORBX_PYR_SPLITROWS=0 (no extra row chunks on
+        // narrow levels)
+        if (const char* v = getenv("ORBX_PYR_NT")) P.nt = std::min(kPyrMaxNT, std::max(64, (atoi(v) + 63) & ~63));
+        P.split = 1;
+        if (const char* v = getenv("ORBX_PYR_SPLITROWS")) P.split = atoi(v) != 0;
+        std::vector<int4> e(n + 1);
+        for (int k = 0; k < K; ++k) {
+            e[n] = make_int4(start[n][k], start[n][k + 1] - 1, start[n][k], start[n][k + 1] - 1);
+            for (int j = b - 1; j > s; --j) {
+                const int of = start[j - s][k], ol = start[j - s][k + 1] - 1;
+                int f0 = lo(j + 1, e[j + 1 - s].x), l0 = hi(j + 1, e[j + 1 - s].y);
+                if (of <= ol) {
+                    f0 = std::min(f0, of);
+                    l0 = std::max(l0, ol);
+                }
+                e[j - s] = make_int4(f0, l0, of, ol);
+            }
+            e[0] = make_int4(lo(s + 1, e[1].x), hi(s + 1, e[1].y), 0, -1);
+            for (int i = 0; i <= n; ++i) {
+                if (e[i].y < e[i].x) {   // (cannot happen for a shrinking pyramid) per-level launches
+                    g.pyr_ngroups = 0;
+                    bands.clear();
+                    return true;
+                }
+                const int bytes = (e[i].y - e[i].x + 1) * lds_pitch(s + i, i == 0);
+                if (i % 2 == 0) P.lds_x = std::max(P.lds_x, bytes);
+                else if (i < n) P.lds_y = std::max(P.lds_y, bytes);
+            }
+            bands.insert(bands.end(), e.begin(), e.end());
+        }
+        // + 16 bytes: the window path's third dword of a group at the end of the last row; a group whose rows
+        // outgrow a workgroup's LDS (very wide images) leaves the small-batch path on the per-level launches
+        if (P.lds_x + P.lds_y + 16 > 160 * 1024) {
+            g.pyr_ngroups = 0;
+            bands.clear();
+            return true;
+        }
+        ++g.pyr_ngroups;
+    }
+    return true;
+}
+
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
+    if (batch <= kLatencyMaxBatch && g.pyr_ngroups > 0) {
+        for (int i = 0; i < g.pyr_ngroups; ++i) {
+            const PyrGroup& P = g.pg[i];
+            const size_t smem = (size_t)P.lds_x + P.lds_y + 16;
+            if (smem > 64 * 1024)
+                hipFuncSetAttribute((const void*)k_pyramid_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipLaunchKernelGGL(k_pyramid_fused, dim3(1, P.nbands, batch), dim3(P.nt), smem, s, b.geom, p, i, b.xtab,
+                               b.ytab, b.pyr_bands);
+        }
+        return;
+    }
     for (int l = 1; l < g.nlevels; ++l) {
         const int h = g.lv[l].h;
         // source rows per block: kPyrRows * (src/dst scale) + 2, bounded by the level ratio

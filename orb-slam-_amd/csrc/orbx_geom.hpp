@@ -48,6 +48,17 @@ struct LevelGeom {
     long long qtg_off, qtg_bytes;
 };
 
+// K1 small-batch launch group: levels s+1 .. s+n resized from level s in one launch (k_pyramid_fused).  A
+// block makes `rows` rows of level s+n and every row of the levels before it that those need; its band-table
+// entries (n + 1 int4 per band from bt_off: {first, last, own first, own last} for levels s .. s+n) say which.
+struct PyrGroup {
+    int s, n, rows, nbands;
+    int bt_off;
+    int lds_x, lds_y;   // LDS bytes of the two row buffers (levels s, s+2, ... / s+1, s+3, ...)
+    int nt;             // threads per block
+    int split;          // narrow levels: threads past the first row chunk take further chunks
+};
+
 struct Geometry {
     int rows, cols, nlevels;
     int ini_th, min_th;
@@ -66,6 +77,8 @@ struct Geometry {
     int qt_kpt0;              // level-0 quadtree keypoints per thread (16, or 24 for large frames)
     long long pyr_bytes;      // bytes per frame for levels 1..L-1
     long long qtg_per_frame;  // K3 global node block per frame (0: every level's node list fits LDS)
+    int pyr_ngroups;          // K1 small-batch launches (0: per-level launches for every batch)
+    PyrGroup pg[kMaxLevels];
     int umax[16];
     LevelGeom lv[kMaxLevels];
 };

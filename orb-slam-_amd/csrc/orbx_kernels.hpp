@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "../../include/orbx.h"
 #include "orbx_geom.hpp"
 
@@ -22,6 +24,7 @@ struct ExtractBufs {
     const Cell* cells;          // device cell table
     const int2* xtab;           // resize tables (levels >= 1)
     const int2* ytab;
+    const int4* pyr_bands;      // K1 small-batch band tables (Geometry::pg)
     uint32_t* slots;            // [B][slots_per_frame] FAST candidates
     int* cell_counts;           // [B][ncells]
     uint32_t* spill;            // [B][spill_per_frame] quadtree overflow (packed kp)
@@ -85,6 +88,8 @@ __host__ __device__ inline int qt_kpt(const Geometry& g, int l)
 }
 __host__ __device__ inline int qt_regcap(const Geometry& g, int l) { return qt_nt(g, l) * qt_kpt(g, l); }
 
+// host: K1 small-batch launch groups and their band tables (Geometry::pg) from the resize row tables
+bool pyr_plan(Geometry& g, const int2* yt, std::vector<int4>& bands);
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
 void fast_groups(Geometry& g);   // host: FAST launch groups (cell ranges, LDS sizes)
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
