@@ -556,6 +556,7 @@ orbx_status orbx_debug_launches(orbx_handle* h, int rows, int cols, int batch, i
     const Geometry& g = h->geom;
     int fast = 0;
     for (int i = 0; i < g.fast_groups; ++i) fast += g.fast_cb[i + 1] > g.fast_cb[i];
+    if (batch <= kLatencyMaxBatch) fast = std::min(fast, 1);   // launch_fast: one launch for small batches
     QtGroup grp[kQtMaxGroups];
     // the pyramid's launches each read one level (counts[4]: bit mask): one launch per level from the one
     // before it

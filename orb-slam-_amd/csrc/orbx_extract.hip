@@ -1161,6 +1161,20 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
 {
     // small batches (the per-frame host path) are latency-bound: one cell per wave, 3x the waves
     const int cpw = batch <= kLatencyMaxBatch ? 1 : kCellsPerWave;
+    // small batches: every cell in one launch sized for the largest ROI (one launch latency fewer; the
+    // occupancy split only pays when the chip is full).  ORBX_FAST_ONE=0: the groups as for large batches.
+    static const int one = getenv("ORBX_FAST_ONE") ? atoi(getenv("ORBX_FAST_ONE")) : 1;
+    if (one && batch <= kLatencyMaxBatch && g.fast_groups > 1) {
+        const int rw = std::max(g.fast_rw[0], g.fast_rw[1]), rh = std::max(g.fast_rh[0], g.fast_rh[1]);
+        const int rpp = 64 / (fast_tile_pitch(rw) / 4 + 1), ld = (rh + rpp - 1) / rpp;
+        if (fast_tile_pitch(rw) == 40) {
+            if (ld <= 8) fast_launch<40, 8>(b, p, 0, g.ncells, rw, rh, cpw, batch, s);
+            else fast_launch<40, 10>(b, p, 0, g.ncells, rw, rh, cpw, batch, s);
+        } else {
+            fast_launch<68, 10>(b, p, 0, g.ncells, rw, rh, cpw, batch, s);
+        }
+        return;
+    }
     for (int i = 0; i < g.fast_groups; ++i) {
         const int cb = g.fast_cb[i], ce = g.fast_cb[i + 1];
         if (ce <= cb) continue;
