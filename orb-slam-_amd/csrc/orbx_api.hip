@@ -571,6 +571,20 @@ orbx_status orbx_debug_launches(orbx_handle* h, int rows, int cols, int batch, i
     return ORBX_OK;
 }
 
+// Host-path copies between the pinned staging block and device memory as kernels on the extraction's own
+// queue: an SDMA copy (hipMemcpy*Async) costs its own ~11 us for a 640x480 image plus ~11 us before the
+// compute queue sees it has finished; a kernel reading or writing the mapped pinned block over PCIe needs
+// neither.  Two (src, dst, 16-byte units) regions per launch.
+__global__ __launch_bounds__(256) void k_host_copy(const uint4* __restrict__ s0, uint4* __restrict__ d0, size_t n0,
+                                                   const uint4* __restrict__ s1, uint4* __restrict__ d1, size_t n1)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += stride) {
+        if (i < n0) d0[i] = s0[i];
+        else d1[i - n0] = s1[i - n0];
+    }
+}
+
 orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols, size_t step, orbx_keypoint* kps,
                          int cap, uint8_t* desc, int* n_out)
 {
@@ -595,8 +609,8 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
         if (!dalloc(h, h->d_out, kp_b + (size_t)ocap * 32)) return ORBX_ENOMEM;
         h->single_cap = ocap;
     }
-    // pinned staging: [image rows x cols][status, count][keypoints ocap][descriptors ocap x 32]
-    const size_t img_b = ((size_t)rows * cols + 63) & ~(size_t)63;
+    // pinned staging: [image rows x pitch][status, count (16 bytes)][keypoints ocap][descriptors ocap x 32]
+    const size_t img_b = need;   // pitch * rows, a multiple of 64
     const size_t kp_off = img_b + 64, ds_off = kp_off + kp_b;
     const size_t pin_need = ds_off + (size_t)ocap * 32;
     if (pin_need > h->pin_bytes) {   // retired, not freed (see orbx_handle::caps)
@@ -607,7 +621,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
         if (hipHostMalloc((void**)&h->h_pin, want, hipHostMallocDefault) != hipSuccess) return ORBX_ENOMEM;
         h->pin_bytes = want;
     }
-    for (int r = 0; r < rows; ++r) std::memcpy(h->h_pin + (size_t)r * cols, img + (size_t)r * step, (size_t)cols);
+    for (int r = 0; r < rows; ++r) std::memcpy(h->h_pin + (size_t)r * pitch, img + (size_t)r * step, (size_t)cols);
     hipStream_t s = own_stream(h);
     FramePtrs P{h->d_img, need, pitch, h->d_pyr, (size_t)h->geom.pyr_bytes};
     int* phdr = (int*)(h->h_pin + img_b);   // [0] status, [1] count
@@ -617,11 +631,30 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     // H2D image, the kernels, then one round trip: status, count and the whole output capacity
     // a timed handle (orbx_set_timing) launches directly, recording the stage events
     const hipEvent_t* ev = h->timing ? next_stage_events(h) : nullptr;
+    // the pinned block's device address (the same pointer under unified addressing)
+    void* dpin = nullptr;
+    if (hipHostGetDevicePointer(&dpin, h->h_pin, 0) != hipSuccess) dpin = nullptr;
+    static const int copyk = getenv("ORBX_HOST_COPYK") ? atoi(getenv("ORBX_HOST_COPYK")) : 1;   // 0: SDMA copies
+    const bool kcopy = copyk && dpin;
+    uint8_t* dp = (uint8_t*)dpin;
+    const size_t out_b = kp_b + (size_t)ocap * 32;   // multiple of 32
     auto enqueue = [&]() {
-        hipMemcpy2DAsync(h->d_img, pitch, h->h_pin, cols, cols, rows, hipMemcpyHostToDevice, s);
+        if (kcopy) {   // the image rows at the device pitch, so the copy is whole 16-byte units
+            hipLaunchKernelGGL(k_host_copy, dim3(std::min<size_t>((need / 16 + 255) / 256, 1024)), dim3(256), 0, s,
+                               (const uint4*)dp, (uint4*)h->d_img, need / 16, (const uint4*)nullptr, (uint4*)nullptr,
+                               (size_t)0);
+        } else {
+            hipMemcpyAsync(h->d_img, h->h_pin, need, hipMemcpyHostToDevice, s);
+        }
         enqueue_pipeline(h, P, 1, d_kps, d_desc, d_count, ocap, s, ev);
-        hipMemcpyAsync(phdr, h->d_status, 2 * sizeof(int), hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(h->h_pin + kp_off, h->d_out, kp_b + (size_t)ocap * 32, hipMemcpyDeviceToHost, s);
+        if (kcopy) {   // status + count (the status block's first 16 bytes) and the whole output capacity
+            hipLaunchKernelGGL(k_host_copy, dim3(std::min<size_t>((out_b / 16 + 1 + 255) / 256, 1024)), dim3(256), 0, s,
+                               (const uint4*)h->d_status, (uint4*)(dp + img_b), (size_t)1, (const uint4*)h->d_out,
+                               (uint4*)(dp + kp_off), out_b / 16);
+        } else {
+            hipMemcpyAsync(phdr, h->d_status, 2 * sizeof(int), hipMemcpyDeviceToHost, s);
+            hipMemcpyAsync(h->h_pin + kp_off, h->d_out, out_b, hipMemcpyDeviceToHost, s);
+        }
     };
     // Replayed as a hipGraph: one submission instead of ~17 (launch overhead is most of a 640x480 frame's
     // latency).  The graph is re-captured when any buffer or size it holds changes.
