@@ -190,6 +190,8 @@ def main():
     ap.add_argument("--streams", type=int, default=3, help="pipeline depth (batches in flight per GPU); "
                     "GPU_MAX_HW_QUEUES=4 leaves 3 besides the default stream")
     ap.add_argument("--iso-steps", type=int, default=3, help="untimed one-stream steps for roofline_isolated")
+    ap.add_argument("--match-stream", action="store_true",
+                    help="SearchForInitialization on the default stream beside the extraction streams")
     ap.add_argument("--instrument-timed", action="store_true",
                     help="record the per-stage events inside the timed region (default: a separate pass)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -231,6 +233,10 @@ def main():
     m12 = [torch.empty((B - 1, cap), dtype=torch.int32, device=dev) for _ in range(P)]
     nm = [torch.empty((B - 1,), dtype=torch.int32, device=dev) for _ in range(P)]
     streams = [torch.cuda.Stream(device=dev) for _ in range(P)]
+    # --match-stream: SearchForInitialization of every batch on the default stream (a hardware queue of its
+    # own), ordered after its batch's extraction by an event, so the extraction streams do not wait for it
+    mstream = torch.cuda.default_stream(dev) if args.match_stream else None
+    pl_done = {}   # payload -> event after the last match that read it
     ev_m = []
 
     def step(k, timed=False, j=None):
@@ -239,14 +245,26 @@ def main():
         s = streams[j]
         with torch.cuda.stream(s):
             pl = hands[j].next_payload()
+        if mstream is not None and id(pl) in pl_done:
+            s.wait_event(pl_done[id(pl)])   # the match that read this payload is done before it is rewritten
         exs[j].extract_batch_device(frames[base:base + B], pl.kps, pl.desc, pl.counts, s)
+        ms = s
+        if mstream is not None:
+            ex_done = torch.cuda.Event()
+            ex_done.record(s)
+            mstream.wait_event(ex_done)
+            ms = mstream
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-        matcher.search_for_initialization_batch(pl.kps, pl.desc, pl.counts, pa, pb, H, W, WINDOW, m12[j], nm[j], s)
+            e0.record(ms)
+        matcher.search_for_initialization_batch(pl.kps, pl.desc, pl.counts, pa, pb, H, W, WINDOW, m12[j], nm[j], ms)
         if timed:
-            e1.record(s)
+            e1.record(ms)
             ev_m.append((e0, e1))
+        if mstream is not None:
+            d = torch.cuda.Event()
+            d.record(mstream)
+            pl_done[id(pl)] = d
         with torch.cuda.stream(s):
             hands[j].send()
         last_payload[0] = pl
