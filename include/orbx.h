@@ -122,7 +122,8 @@ orbx_status orbx_sync(orbx_handle* h, void* stream);
 /* Per-stage device timing (ms, HIP events recorded on the launch stream between
  * the stage kernels).  orbx_set_timing(h, 1) starts a new accumulation window;
  * orbx_get_stage_times returns the per-stage sums over every extract since then, host
- * (orbx_extract, launched directly instead of as a graph while timing is on) and batched.
+ * (orbx_extract, launched directly instead of as a graph while timing is on), batched and
+ * stage-split (orbx_extract_stage_device: each stage timed on its own stream).
  * Stages: 0 pyramid (all levels), 1 fast, 2 quadtree, 3 describe. */
 orbx_status orbx_set_timing(orbx_handle* h, int enable);
 orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n);

@@ -112,7 +112,7 @@ struct orbx_handle {
     orbx_params params{};
     Tables tab;
 
-    // geometry (per rows x cols)
+    // geometry (per rows x cols): the current size's host copy and device tables
     bool geom_ok = false;
     int grows = -1, gcols = -1;
     Geometry geom{};
@@ -122,6 +122,20 @@ struct orbx_handle {
     int2* d_xtab = nullptr;
     int2* d_ytab = nullptr;
     int4* d_pyrbt = nullptr;   // K1 small-batch band tables
+    // Every size seen keeps its own immutable device tables: a size switch selects another block
+    // instead of rewriting the tables that kernels of an earlier call (still queued on the caller's
+    // stream) are reading.  Bounded by the number of distinct image sizes.
+    struct GeomBlock {
+        int rows, cols;
+        Geometry geom;
+        std::vector<Cell> cells;
+        Geometry* d_geom;
+        Cell* d_cells;
+        int2* d_xtab;
+        int2* d_ytab;
+        int4* d_pyrbt;
+    };
+    std::vector<GeomBlock> geom_blocks;
 
     // batch workspace
     int batch_cap = 0;
@@ -150,6 +164,14 @@ struct orbx_handle {
     std::vector<const void*> graph_key;
     bool graph_failed = false;
 
+    // The handle's device work is ordered across streams: its workspace (pyramid, candidate slots,
+    // quadtree buffers) is shared by every call, so a call on another stream than the last one waits
+    // for that call's completion event first (a host extract while a batch is still queued on the
+    // caller's stream, or batches of one handle on alternating streams).
+    hipEvent_t done_ev = nullptr;
+    hipStream_t done_stream = nullptr;
+    bool done_pending = false;
+
     // last batch (for pyramid / debug readback)
     FramePtrs last{};
     int last_batch = 0;
@@ -160,6 +182,11 @@ struct orbx_handle {
     bool timing = false;
     std::vector<hipEvent_t> ev;
     int ev_used = 0;
+    // stage-split extractions (orbx_extract_stage_device): one (start, end) event pair per timed stage
+    // call, on that stage's own stream
+    std::vector<hipEvent_t> sev;
+    std::vector<int> sev_stage;
+    int sev_used = 0;
 
     // Buffers only grow, and an outgrown one is retired until orbx_destroy rather than freed:
     // hipFree / hipHostFree wait for the whole device, which would stall every other stream of the
@@ -212,10 +239,42 @@ hipStream_t own_stream(orbx_handle* h)
     return h->stream;
 }
 
+void select_geometry(orbx_handle* h, const orbx_handle::GeomBlock& b)
+{
+    h->geom = b.geom;
+    h->cells = b.cells;
+    h->d_geom = b.d_geom;
+    h->d_cells = b.d_cells;
+    h->d_xtab = b.d_xtab;
+    h->d_ytab = b.d_ytab;
+    h->d_pyrbt = b.d_pyrbt;
+    h->grows = b.rows;
+    h->gcols = b.cols;
+    h->geom_ok = true;
+    h->batch_cap = 0;   // re-size the workspace for this geometry (buffers only grow)
+    h->single_cap = 0;
+}
+
+template <class T>
+bool dalloc_exact(T*& p, size_t count)
+{
+    p = nullptr;
+    if (hipMalloc((void**)&p, sizeof(T) * (count ? count : 1)) != hipSuccess) {
+        p = nullptr;
+        return false;
+    }
+    return true;
+}
+
 orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
 {
     if (h->geom_ok && h->grows == rows && h->gcols == cols) return ORBX_OK;
     if (rows <= 0 || cols <= 0 || rows > kMaxDim || cols > kMaxDim) return ORBX_EINVAL;
+    for (const auto& b : h->geom_blocks)
+        if (b.rows == rows && b.cols == cols) {
+            select_geometry(h, b);
+            return ORBX_OK;
+        }
     const Tables& t = h->tab;
     Geometry g{};
     g.rows = rows;
@@ -331,32 +390,37 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     for (int l = 0; l < t.nlevels; ++l) spill += std::max(0, g.lv[l].slot_cap - qt_regcap(g, l));
     g.spill_per_frame = std::max(spill, 1);
 
-    // once per image size: the tables go up on the handle's own stream (never the legacy null stream)
-    if (!dalloc(h, h->d_geom, 1) || !dalloc(h, h->d_cells, cells.size()) || !dalloc(h, h->d_xtab, xt.size()) ||
-        !dalloc(h, h->d_ytab, yt.size()) || !dalloc(h, h->d_pyrbt, pyrbt.size()))
+    // once per image size, into fresh buffers that nothing queued can be reading
+    orbx_handle::GeomBlock b{rows, cols, g, std::move(cells), nullptr, nullptr, nullptr, nullptr, nullptr};
+    auto release = [&b] { dfree(b.d_geom); dfree(b.d_cells); dfree(b.d_xtab); dfree(b.d_ytab); dfree(b.d_pyrbt); };
+    if (!dalloc_exact(b.d_geom, 1) || !dalloc_exact(b.d_cells, b.cells.size()) || !dalloc_exact(b.d_xtab, xt.size()) ||
+        !dalloc_exact(b.d_ytab, yt.size()) || !dalloc_exact(b.d_pyrbt, pyrbt.size())) {
+        release();
         return ORBX_ENOMEM;
+    }
     // on a pooled host-call stream (high priority, orbx_host.hip), so that a handle used only through
     // orbx_extract_batch_device never creates a stream of its own (each takes one of the process's
     // few hardware queues); the copies are complete before any later launch on any stream
     {
         HostCall c(h->device);
         hipStream_t s = c.stream();
-        if (!s) return ORBX_EDEVICE;
-        hipMemcpyAsync(h->d_geom, &g, sizeof(g), hipMemcpyHostToDevice, s);
-        hipMemcpyAsync(h->d_cells, cells.data(), sizeof(Cell) * cells.size(), hipMemcpyHostToDevice, s);
-        if (!xt.empty()) hipMemcpyAsync(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice, s);
-        if (!yt.empty()) hipMemcpyAsync(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice, s);
+        if (!s) {
+            release();
+            return ORBX_EDEVICE;
+        }
+        hipMemcpyAsync(b.d_geom, &b.geom, sizeof(Geometry), hipMemcpyHostToDevice, s);
+        hipMemcpyAsync(b.d_cells, b.cells.data(), sizeof(Cell) * b.cells.size(), hipMemcpyHostToDevice, s);
+        if (!xt.empty()) hipMemcpyAsync(b.d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice, s);
+        if (!yt.empty()) hipMemcpyAsync(b.d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice, s);
         if (!pyrbt.empty())
-            hipMemcpyAsync(h->d_pyrbt, pyrbt.data(), sizeof(int4) * pyrbt.size(), hipMemcpyHostToDevice, s);
-        if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+            hipMemcpyAsync(b.d_pyrbt, pyrbt.data(), sizeof(int4) * pyrbt.size(), hipMemcpyHostToDevice, s);
+        if (hipStreamSynchronize(s) != hipSuccess) {
+            release();
+            return ORBX_EDEVICE;
+        }
     }
-    h->geom = g;
-    h->cells = std::move(cells);
-    h->grows = rows;
-    h->gcols = cols;
-    h->geom_ok = true;
-    h->batch_cap = 0;   // force workspace re-allocation
-    h->single_cap = 0;
+    h->geom_blocks.push_back(std::move(b));
+    select_geometry(h, h->geom_blocks.back());
     return ORBX_OK;
 }
 
@@ -394,6 +458,24 @@ ExtractBufs bufs(orbx_handle* h)
     b.qt_cnt = h->d_qt_cnt;
     b.status = h->d_status;
     return b;
+}
+
+// stream s waits for the handle's last device call when that call was queued on another stream
+void order_after_last(orbx_handle* h, hipStream_t s)
+{
+    if (h->done_pending && h->done_stream != s) hipStreamWaitEvent(s, h->done_ev, 0);
+}
+
+// the handle's latest device work is the work queued so far on s
+void mark_last(orbx_handle* h, hipStream_t s)
+{
+    if (!h->done_ev && hipEventCreateWithFlags(&h->done_ev, hipEventDisableTiming) != hipSuccess) {
+        h->done_ev = nullptr;
+        return;
+    }
+    hipEventRecord(h->done_ev, s);
+    h->done_stream = s;
+    h->done_pending = true;
 }
 
 // the next set of 5 stage-boundary events of a timed handle (orbx_set_timing)
@@ -498,11 +580,13 @@ void orbx_destroy(orbx_handle* h)
     if (h->h_status) hipHostFree(h->h_status);
     for (void* p : h->retired_pin) hipHostFree(p);
     for (void* p : h->retired_dev) (void)hipFree(p);
-    dfree(h->d_geom);
-    dfree(h->d_cells);
-    dfree(h->d_xtab);
-    dfree(h->d_ytab);
-    dfree(h->d_pyrbt);
+    for (auto& b : h->geom_blocks) {
+        dfree(b.d_geom);
+        dfree(b.d_cells);
+        dfree(b.d_xtab);
+        dfree(b.d_ytab);
+        dfree(b.d_pyrbt);
+    }
     dfree(h->d_pyr);
     dfree(h->d_slots);
     dfree(h->d_cell_counts);
@@ -516,7 +600,10 @@ void orbx_destroy(orbx_handle* h)
     dfree(h->d_out);
     for (auto& e : h->ev)
         if (e) hipEventDestroy(e);
+    for (auto& e : h->sev)
+        if (e) hipEventDestroy(e);
     if (h->host_graph) hipGraphExecDestroy(h->host_graph);
+    if (h->done_ev) hipEventDestroy(h->done_ev);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -623,6 +710,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     }
     for (int r = 0; r < rows; ++r) std::memcpy(h->h_pin + (size_t)r * pitch, img + (size_t)r * step, (size_t)cols);
     hipStream_t s = own_stream(h);
+    order_after_last(h, s);
     FramePtrs P{h->d_img, need, pitch, h->d_pyr, (size_t)h->geom.pyr_bytes};
     int* phdr = (int*)(h->h_pin + img_b);   // [0] status, [1] count
     int* d_count = h->d_status + 1;
@@ -660,7 +748,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     // latency).  The graph is re-captured when any buffer or size it holds changes.
     const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
                                           h->d_spill_node, h->d_qt_nodes, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
-                                          h->d_cells, h->d_xtab, h->d_ytab, (const void*)(uintptr_t)rows,
+                                          h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
     bool launched = false;
     if (!ev && !h->graph_failed && !getenv("ORBX_NO_GRAPH")) {
@@ -692,6 +780,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     h->last_batch = 1;
     std::fill(h->level_cached.begin(), h->level_cached.end(), false);
     if (hipStreamSynchronize(s) != hipSuccess) return ORBX_EDEVICE;
+    h->done_pending = false;   // everything the handle queued has completed
     if (phdr[0] & kStatusCapOverflow) return ORBX_ENOSPC;
     if (phdr[0]) return ORBX_EDEVICE;
     const int n = phdr[1];
@@ -721,6 +810,7 @@ orbx_status orbx_get_level(orbx_handle* h, int level, const uint8_t** data, int*
             src = h->last.pyr + L.pyr_off;
             sp = (size_t)L.pitch;
         }
+        order_after_last(h, own_stream(h));
         if (hipMemcpy2DAsync(v.data(), L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, own_stream(h)) != hipSuccess ||
             hipStreamSynchronize(own_stream(h)) != hipSuccess)
             return ORBX_EDEVICE;
@@ -744,8 +834,11 @@ orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int
     if (st != ORBX_OK) return st;
     if ((st = ensure_batch(h, batch)) != ORBX_OK) return st;
     hipStream_t s = (hipStream_t)stream;   // taken literally: NULL is the HIP null stream
+    order_after_last(h, s);
     FramePtrs P{d_imgs, frame_stride, (int)step, h->d_pyr, (size_t)h->geom.pyr_bytes};
-    return run_pipeline(h, P, batch, d_kps, d_desc, d_counts, cap, s);
+    st = run_pipeline(h, P, batch, d_kps, d_desc, d_counts, cap, s);
+    mark_last(h, s);
+    return st;
 }
 
 orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* d_imgs, int batch, int rows, int cols,
@@ -767,6 +860,19 @@ orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* 
     const Geometry& g = h->geom;
     ExtractBufs b = bufs(h);
     FramePtrs P{d_imgs, frame_stride, (int)step, h->d_pyr, (size_t)g.pyr_bytes};
+    hipEvent_t* tev = nullptr;   // a timed handle: this stage's (start, end) events
+    if (h->timing) {
+        if ((size_t)(h->sev_used + 1) * 2 > h->sev.size()) {
+            const size_t old = h->sev.size();
+            h->sev.resize(old + 2 * 64);
+            h->sev_stage.resize(h->sev.size() / 2);
+            for (size_t i = old; i < h->sev.size(); ++i) hipEventCreate(&h->sev[i]);
+        }
+        h->sev_stage[h->sev_used] = stage;
+        tev = &h->sev[(size_t)(h->sev_used++) * 2];
+        hipEventRecord(tev[0], s);
+    }
+    if (stage == 0) order_after_last(h, s);   // the previous batch's describe (the caller orders the rest)
     switch (stage) {
     case 0:
         hipMemsetAsync(d_counts, 0, sizeof(int) * batch, s);
@@ -784,8 +890,10 @@ orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* 
         h->last = P;
         h->last_batch = batch;
         std::fill(h->level_cached.begin(), h->level_cached.end(), false);
+        mark_last(h, s);
         break;
     }
+    if (tev) hipEventRecord(tev[1], s);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 
@@ -803,14 +911,22 @@ orbx_status orbx_set_timing(orbx_handle* h, int enable)
     if (!h) return ORBX_EINVAL;
     h->timing = enable != 0;
     h->ev_used = 0;   // (re)start accumulation
+    h->sev_used = 0;
     return ORBX_OK;
 }
 
 orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n)
 {
-    if (!h || !ms || h->ev_used == 0) return ORBX_EINVAL;
-    if (hipEventSynchronize(h->ev[(size_t)h->ev_used * 5 - 1]) != hipSuccess) return ORBX_EDEVICE;
+    if (!h || !ms || (h->ev_used == 0 && h->sev_used == 0)) return ORBX_EINVAL;
     for (int i = 0; i < n && i < 4; ++i) ms[i] = 0.f;
+    for (int c = 0; c < h->sev_used; ++c) {   // stage-split calls (their streams may differ)
+        const hipEvent_t* e = &h->sev[(size_t)c * 2];
+        float t = 0.f;
+        if (hipEventSynchronize(e[1]) != hipSuccess) return ORBX_EDEVICE;
+        hipEventElapsedTime(&t, e[0], e[1]);
+        if (h->sev_stage[c] < n) ms[h->sev_stage[c]] += t;
+    }
+    if (h->ev_used > 0 && hipEventSynchronize(h->ev[(size_t)h->ev_used * 5 - 1]) != hipSuccess) return ORBX_EDEVICE;
     for (int c = 0; c < h->ev_used; ++c) {
         const hipEvent_t* e = &h->ev[(size_t)c * 5];
         for (int i = 0; i < n && i < 4; ++i) {
@@ -826,6 +942,7 @@ orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t o
 {
     if (!h || !out || frame < 0 || frame >= h->last_batch) return ORBX_EINVAL;
     DeviceGuard guard(h->device);
+    order_after_last(h, own_stream(h));
     size_t o = 0;
     for (int l = 0; l < h->geom.nlevels; ++l) {
         const LevelGeom& L = h->geom.lv[l];
@@ -849,6 +966,7 @@ orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys
 {
     if (!h || !n || frame < 0 || frame >= h->last_batch || level < 0 || level >= h->geom.nlevels) return ORBX_EINVAL;
     DeviceGuard guard(h->device);
+    order_after_last(h, own_stream(h));
     const Geometry& g = h->geom;
     std::vector<int> cnt(g.ncells);
     std::vector<uint32_t> sl(g.slots_per_frame);
@@ -968,6 +1086,7 @@ orbx_status orbx_stereo_batch_device(orbx_handle* h, const orbx_keypoint* d_kps,
     if (npairs == 0) return ORBX_OK;
     DeviceGuard guard(h->device);
     hipStream_t s = (hipStream_t)stream;
+    order_after_last(h, s);   // the batch's pyramids
     int* dsad = nullptr;
     if (hipMallocAsync((void**)&dsad, sizeof(int) * (size_t)npairs * cap, s) != hipSuccess) return ORBX_ENOMEM;
     float maxD;

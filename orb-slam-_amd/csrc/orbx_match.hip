@@ -222,6 +222,13 @@ void launch_allpairs_full(const uint8_t* q, int nq, const uint8_t* t, int nt, ui
 constexpr int kGridCols = 64, kGridRows = 48;
 constexpr int SI_BUILD_NT = 256;
 constexpr int SI_TOPK = 4;
+constexpr int kSiCells = kGridCols * kGridRows;
+constexpr int kSiRankMax = 4096;   // k_si_grid: rank sort up to this many level-0 keypoints, counting sort above
+
+__host__ __device__ inline size_t si_grid_smem(int cap)
+{
+    return (size_t)((cap + 3) & ~3) * 4 + (cap > kSiRankMax ? (size_t)(kSiCells + 4) * 4 : 0);
+}
 
 // min over the 64 lanes with DPP row permutations + 4 readlanes (all lanes active)
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
@@ -297,18 +304,73 @@ __global__ __launch_bounds__(256) void k_si_grid(const orbx_keypoint* __restrict
     }
     __syncthreads();
     const int n0 = s_n0;
-    const int n4 = (n0 + 3) >> 2;
-    const uint4* k4 = (const uint4*)keys;
-    for (int i = tid; i < n0; i += 256) {
-        const uint32_t key = keys[i];
-        if (key == 0xFFFFFFFFu) continue;
-        int r = 0;
-        for (int j4 = 0; j4 < n4; ++j4) {
-            const uint4 v = k4[j4];
-            r += (int)(v.x < key) + (int)(v.y < key) + (int)(v.z < key) + (int)(v.w < key);
+    if (n0 > kSiRankMax) {
+        // large frames: a stable counting sort over the 3072 cells, O(n) instead of the rank's O(n^2)
+        // LDS reads.  Per-cell counts by LDS atomics (arrival slots unordered), an exclusive scan, a
+        // scatter of the indices into their cell segments, then each key's stable place = the number
+        // of lower indices in its own segment (a few entries).  gxy holds the scratch words until the
+        // last step: even word i = key i's arrival slot, then its sorted position; odd word p = the
+        // index scattered to position p.
+        uint32_t* start = keys + ((cap + 3) & ~3);   // [kSiCells + 1]
+        uint32_t* tmp = (uint32_t*)(gxy + (size_t)f * cap);
+        for (int c = tid; c <= kSiCells; c += 256) start[c] = 0u;
+        __syncthreads();
+        for (int i = tid; i < n0; i += 256) {
+            const uint32_t key = keys[i];
+            if (key != 0xFFFFFFFFu) tmp[2 * i] = atomicAdd(&start[key >> 16], 1u);
         }
-        gkeys[(size_t)f * cap + r] = key;
-        gxy[(size_t)f * cap + r] = make_float2(k[i].x, k[i].y);
+        __syncthreads();
+        if (tid < 64) {   // exclusive scan of the 3072 counts by one wave, 48 per lane
+            constexpr int kPer = kSiCells / 64;
+            uint32_t sum = 0;
+            for (int j = 0; j < kPer; ++j) sum += start[lane * kPer + j];
+            uint32_t incl = sum;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            uint32_t base = incl - sum;
+            for (int j = 0; j < kPer; ++j) {
+                const uint32_t c = start[lane * kPer + j];
+                start[lane * kPer + j] = base;
+                base += c;
+            }
+            if (lane == 63) start[kSiCells] = base;
+        }
+        __syncthreads();
+        for (int i = tid; i < n0; i += 256) {
+            const uint32_t key = keys[i];
+            if (key != 0xFFFFFFFFu) tmp[2 * (start[key >> 16] + tmp[2 * i]) + 1] = (uint32_t)i;
+        }
+        __syncthreads();
+        for (int i = tid; i < n0; i += 256) {
+            const uint32_t key = keys[i];
+            if (key == 0xFFFFFFFFu) continue;
+            const int s0 = (int)start[key >> 16], s1 = (int)start[(key >> 16) + 1];
+            int r = 0;
+            for (int j = s0; j < s1; ++j) r += tmp[2 * j + 1] < (uint32_t)i;
+            gkeys[(size_t)f * cap + s0 + r] = key;
+            keys[i] = (uint32_t)(s0 + r);   // read only by this thread below
+        }
+        __syncthreads();
+        for (int i = tid; i < n0; i += 256) {
+            const uint32_t pos = keys[i];
+            if (pos < (uint32_t)cap) gxy[(size_t)f * cap + pos] = make_float2(k[i].x, k[i].y);
+        }
+    } else {
+        const int n4 = (n0 + 3) >> 2;
+        const uint4* k4 = (const uint4*)keys;
+        for (int i = tid; i < n0; i += 256) {
+            const uint32_t key = keys[i];
+            if (key == 0xFFFFFFFFu) continue;
+            int r = 0;
+            for (int j4 = 0; j4 < n4; ++j4) {
+                const uint4 v = k4[j4];
+                r += (int)(v.x < key) + (int)(v.y < key) + (int)(v.z < key) + (int)(v.w < key);
+            }
+            gkeys[(size_t)f * cap + r] = key;
+            gxy[(size_t)f * cap + r] = make_float2(k[i].x, k[i].y);
+        }
     }
     if (tid == 0) {
         gn[2 * f] = n0;
@@ -942,8 +1004,8 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     int* gn = (int*)carve((size_t)nframes * 2 * 4);
     int* qcnt = (int*)carve((size_t)npairs * cap * 4);
     uint4* qtop = (uint4*)carve((size_t)npairs * cap * 16);
-    hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), (size_t)((cap + 3) & ~3) * 4, s, kps, counts, cap, G, gkeys,
-                       gxy, gn);
+    hipFuncSetAttribute((const void*)k_si_grid, hipFuncAttributeMaxDynamicSharedMemorySize, (int)si_grid_smem(cap));
+    hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), si_grid_smem(cap), s, kps, counts, cap, G, gkeys, gxy, gn);
     const size_t bsmem = si_build_smem_bytes();
     // query slices per pair: about 8 waves per SIMD over the chip, at least 4 queries per wave
     // (ORBX_SI_QSPLIT: A/B knob)

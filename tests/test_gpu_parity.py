@@ -385,3 +385,74 @@ def test_stage_times_cover_host_calls(orbref, cuda):
     ex.set_timing(False)
     kps, desc = ex(img)   # back on the graph
     assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "untimed again")
+
+
+def test_size_switch_while_a_batch_is_queued(orbref, cuda):
+    """A batch at one size queued behind a long kernel on a side stream, then capacity() and a host-path
+    extract at another size on the same handle, then a second batch at the first size on the default stream.
+    The geometry tables of each size are separate device blocks (a switch never rewrites tables queued
+    kernels read), and a call on another stream waits for the handle's last call (the workspace is shared),
+    so every result equals the oracle's."""
+    import torch
+    import orbx
+    import orbx_synth
+    ex = _extractor(2000)
+    kitti = orbx_synth.kitti_sequence(4, start=3)
+    B, H, W = kitti.shape
+    imgs = torch.from_numpy(np.ascontiguousarray(kitti)).to(cuda)
+    cap = ex.capacity(H, W)
+    side = torch.cuda.Stream(device=cuda)
+    outs = []
+    for _ in range(2):
+        outs.append((torch.empty((B, cap, 7), dtype=torch.int32, device=cuda),
+                     torch.empty((B, cap, 32), dtype=torch.uint8, device=cuda),
+                     torch.empty((B,), dtype=torch.int32, device=cuda)))
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(200_000_000)   # ~0.1 s: the batch is still queued when the host calls run
+        ex.extract_batch_device(imgs, *outs[0], stream=side)
+    small = orbx_synth.gen_image(5, 640, 480)
+    assert ex.capacity(480, 640) > 0
+    kps_s, desc_s = ex(small)
+    ex.extract_batch_device(imgs, *outs[1])   # back to the first size, on the default stream
+    torch.cuda.synchronize()
+    p = orbref.make_params(2000, 1.2, 8, 20, 7)
+    ref_s = orbref.extract(small, p, want_pyramid=False)
+    assert_same_keypoints(kps_s, ref_s.keypoints, desc_s, ref_s.descriptors, "host call at 640x480")
+    refs = [orbref.extract(kitti[f], p, want_pyramid=False) for f in range(B)]
+    for r, (kps, desc, counts) in enumerate(outs):
+        klist = orbx.keypoints_from_device(kps, counts)
+        d = desc.cpu().numpy()
+        for f in range(B):
+            n = len(refs[f].keypoints)
+            assert_same_keypoints(klist[f], refs[f].keypoints, d[f, :n], refs[f].descriptors, "batch %d frame %d" % (r, f))
+
+
+def test_stage_times_cover_stage_split_calls(orbref, cuda):
+    """Stage-split extraction (orbx_extract_stage_device) on a timed handle: each stage is timed on its
+    own stream and stage_times() includes it."""
+    import torch
+    import orbx
+    import orbx_synth
+    ex = _extractor(2000)
+    kitti = orbx_synth.kitti_sequence(2, start=7)
+    B, H, W = kitti.shape
+    imgs = torch.from_numpy(np.ascontiguousarray(kitti)).to(cuda)
+    cap = ex.capacity(H, W)
+    kps = torch.empty((B, cap, 7), dtype=torch.int32, device=cuda)
+    desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=cuda)
+    counts = torch.empty((B,), dtype=torch.int32, device=cuda)
+    ex.set_timing(True)
+    for stage in range(4):
+        ex.extract_stage_device(stage, imgs, kps, desc, counts)
+    ex.sync(torch.cuda.current_stream())
+    ms = ex.stage_times()
+    assert ms.shape == (4,) and (ms > 0).all() and ms.sum() < 1000, ms
+    ex.set_timing(False)
+    klist = orbx.keypoints_from_device(kps, counts)
+    d = desc.cpu().numpy()
+    p = orbref.make_params(2000, 1.2, 8, 20, 7)
+    for f in range(B):
+        ref = orbref.extract(kitti[f], p, want_pyramid=False)
+        n = len(ref.keypoints)
+        assert_same_keypoints(klist[f], ref.keypoints, d[f, :n], ref.descriptors, "stage-split frame %d" % f)
