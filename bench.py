@@ -34,6 +34,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import orbx  # noqa: E402
+
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from srchash import kernel_sources_sha256  # noqa: E402
 import orbx_dist  # noqa: E402
 import orbx_synth  # noqa: E402
 
@@ -446,11 +449,11 @@ def main():
         launches = {"pyramid": n_launch["pyramid"], "fast": n_launch["fast"]}.get(dom, 1)
         t_launch = st[dom] / launches * 1e-3
         achieved = alg[dom] / launches / t_launch / 1e9
-        kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_quadtree<512,16|512,8|256,4>",
+        kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": "k_qt_paths<512,16|512,8|256,4>",
                  "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
         # stages made of several kernels: their per-launch counters add up
         PARTS = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"],
-                 "quadtree": ["k_quadtree<512, 16", "k_quadtree<512, 8", "k_quadtree<256, 4"]}
+                 "quadtree": ["k_qt_paths<512, 16", "k_qt_paths<512, 8", "k_qt_paths<256, 4"]}
 
         def per_launch(K, dom, kname, field):
             """A counter per launch from a per-kernel table keyed by full names (template arguments
@@ -464,12 +467,17 @@ def main():
             return sum(K[k][field] * K[k]["dispatches"] for k in ks) / nd
         # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
         # same command (tools/collect_pmc.sh -> tools/pmc_summary.py); null when absent
+        # Both counter files carry the kernel-source hash of the tree they were measured on; a file from
+        # another tree is reported as stale and its figures are not used.
         traffic = None
+        src_sha = kernel_sources_sha256()
+        counters = {"kernel_sources_sha256": src_sha}
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
                 d = json.load(open(pmc))
-                if d.get("batch") == B:
+                counters["pmc_traffic_sha256"] = d.get("kernel_sources_sha256")
+                if d.get("batch") == B and d.get("kernel_sources_sha256") == src_sha:
                     traffic = int(per_launch(d["kernels"], dom, kname, "bytes_per_launch"))
             except Exception:
                 traffic = None
@@ -483,7 +491,8 @@ def main():
         if os.path.exists(sq):
             try:
                 d = json.load(open(sq))
-                if d.get("batch") == B:
+                counters["sq_counters_sha256"] = d.get("kernel_sources_sha256")
+                if d.get("batch") == B and d.get("kernel_sources_sha256") == src_sha:
                     ins = per_launch(d["per_dispatch_averages"], dom, kname, "SQ_INSTS_VALU")
                     rate = ins / t_launch / 1e9
                     pk, pins, p2 = valu_peak(kname)
@@ -497,6 +506,9 @@ def main():
                                 "VALU pipe is its limiter (DESIGN.md section 6)"}
             except Exception:
                 pass
+        counters["current"] = (counters.get("pmc_traffic_sha256") == src_sha and
+                               counters.get("sq_counters_sha256") == src_sha)
+        r["counters"] = counters
         return r
 
     out = {

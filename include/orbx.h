@@ -95,7 +95,8 @@ orbx_status orbx_get_level(orbx_handle* h, int level, const uint8_t** data, int*
                            size_t* step);
 
 /* Batched device-resident replay (config 2/4): `batch` frames of rows x cols u8 at
- * d_imgs + f*frame_stride (row pitch `step`), already in HBM.  Outputs per frame f:
+ * d_imgs + f*frame_stride (row pitch `step`; frame_stride is not read when batch == 1), already in HBM.
+ * Outputs per frame f:
  * d_kps[f*cap + i], d_desc[(f*cap + i)*32], d_counts[f].  Asynchronous on `stream`
  * (a hipStream_t taken literally: NULL is the HIP null stream). */
 orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int batch, int rows,

@@ -122,6 +122,7 @@ struct orbx_handle {
     int2* d_xtab = nullptr;
     int2* d_ytab = nullptr;
     int4* d_pyrbt = nullptr;   // K1 small-batch band tables
+    uint32_t* d_qpt = nullptr; // K3 path tables
     // Every size seen keeps its own immutable device tables: a size switch selects another block
     // instead of rewriting the tables that kernels of an earlier call (still queued on the caller's
     // stream) are reading.  Bounded by the number of distinct image sizes.
@@ -134,6 +135,7 @@ struct orbx_handle {
         int2* d_xtab;
         int2* d_ytab;
         int4* d_pyrbt;
+        uint32_t* d_qpt;
     };
     std::vector<GeomBlock> geom_blocks;
 
@@ -142,6 +144,7 @@ struct orbx_handle {
     uint8_t* d_pyr = nullptr;
     uint32_t* d_slots = nullptr;
     int* d_cell_counts = nullptr;
+    uint32_t* d_cell_addr = nullptr;
     uint32_t* d_spill = nullptr;
     uint32_t* d_spill_node = nullptr;
     uint8_t* d_qt_nodes = nullptr;
@@ -248,6 +251,7 @@ void select_geometry(orbx_handle* h, const orbx_handle::GeomBlock& b)
     h->d_xtab = b.d_xtab;
     h->d_ytab = b.d_ytab;
     h->d_pyrbt = b.d_pyrbt;
+    h->d_qpt = b.d_qpt;
     h->grows = b.rows;
     h->gcols = b.cols;
     h->geom_ok = true;
@@ -326,6 +330,8 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
         if (nCols <= 0 || nRows <= 0) return ORBX_EINVAL;
         const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+        L.qp_wc = wCell;
+        L.qp_hc = hCell;
         L.cell_begin = (int)cells.size();
         L.slot_begin = slot;
         for (int i = 0; i < nRows; i++) {
@@ -389,12 +395,22 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     if (!qt_prepare(g)) return ORBX_EINVAL;
     for (int l = 0; l < t.nlevels; ++l) spill += std::max(0, g.lv[l].slot_cap - qt_regcap(g, l));
     g.spill_per_frame = std::max(spill, 1);
+    std::vector<uint32_t> qpt;
+    qp_tables(g, qpt);
 
     // once per image size, into fresh buffers that nothing queued can be reading
-    orbx_handle::GeomBlock b{rows, cols, g, std::move(cells), nullptr, nullptr, nullptr, nullptr, nullptr};
-    auto release = [&b] { dfree(b.d_geom); dfree(b.d_cells); dfree(b.d_xtab); dfree(b.d_ytab); dfree(b.d_pyrbt); };
+    orbx_handle::GeomBlock b{rows, cols, g, std::move(cells), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    auto release = [&b] {
+        dfree(b.d_geom);
+        dfree(b.d_cells);
+        dfree(b.d_xtab);
+        dfree(b.d_ytab);
+        dfree(b.d_pyrbt);
+        dfree(b.d_qpt);
+    };
     if (!dalloc_exact(b.d_geom, 1) || !dalloc_exact(b.d_cells, b.cells.size()) || !dalloc_exact(b.d_xtab, xt.size()) ||
-        !dalloc_exact(b.d_ytab, yt.size()) || !dalloc_exact(b.d_pyrbt, pyrbt.size())) {
+        !dalloc_exact(b.d_ytab, yt.size()) || !dalloc_exact(b.d_pyrbt, pyrbt.size()) ||
+        !dalloc_exact(b.d_qpt, qpt.size())) {
         release();
         return ORBX_ENOMEM;
     }
@@ -414,6 +430,7 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         if (!yt.empty()) hipMemcpyAsync(b.d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice, s);
         if (!pyrbt.empty())
             hipMemcpyAsync(b.d_pyrbt, pyrbt.data(), sizeof(int4) * pyrbt.size(), hipMemcpyHostToDevice, s);
+        if (!qpt.empty()) hipMemcpyAsync(b.d_qpt, qpt.data(), sizeof(uint32_t) * qpt.size(), hipMemcpyHostToDevice, s);
         if (hipStreamSynchronize(s) != hipSuccess) {
             release();
             return ORBX_EDEVICE;
@@ -430,7 +447,7 @@ orbx_status ensure_batch(orbx_handle* h, int batch)
     const Geometry& g = h->geom;
     const size_t B = (size_t)batch;
     if (!dalloc(h, h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h, h->d_slots, (size_t)g.slots_per_frame * B) ||
-        !dalloc(h, h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h, h->d_spill, (size_t)g.spill_per_frame * B) ||
+        !dalloc(h, h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h, h->d_cell_addr, (size_t)g.ncells * B) || !dalloc(h, h->d_spill, (size_t)g.spill_per_frame * B) ||
         !dalloc(h, h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h, h->d_qt_out, (size_t)g.out_per_frame * B) ||
         !dalloc(h, h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h, h->d_status, 16) ||
         !dalloc(h, h->d_qt_nodes, (size_t)g.qtg_per_frame * B)) {
@@ -449,8 +466,10 @@ ExtractBufs bufs(orbx_handle* h)
     b.xtab = h->d_xtab;
     b.ytab = h->d_ytab;
     b.pyr_bands = h->d_pyrbt;
+    b.qpt = h->d_qpt;
     b.slots = h->d_slots;
     b.cell_counts = h->d_cell_counts;
+    b.cell_addr = h->d_cell_addr;
     b.spill = h->d_spill;
     b.spill_node = h->d_spill_node;
     b.qt_nodes = h->d_qt_nodes;
@@ -586,10 +605,12 @@ void orbx_destroy(orbx_handle* h)
         dfree(b.d_xtab);
         dfree(b.d_ytab);
         dfree(b.d_pyrbt);
+        dfree(b.d_qpt);
     }
     dfree(h->d_pyr);
     dfree(h->d_slots);
     dfree(h->d_cell_counts);
+    dfree(h->d_cell_addr);
     dfree(h->d_spill);
     dfree(h->d_spill_node);
     dfree(h->d_qt_nodes);
@@ -746,9 +767,9 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     };
     // Replayed as a hipGraph: one submission instead of ~17 (launch overhead is most of a 640x480 frame's
     // latency).  The graph is re-captured when any buffer or size it holds changes.
-    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
+    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_cell_addr, h->d_spill,
                                           h->d_spill_node, h->d_qt_nodes, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
-                                          h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, (const void*)(uintptr_t)rows,
+                                          h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, h->d_qpt, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
     bool launched = false;
     if (!ev && !h->graph_failed && !getenv("ORBX_NO_GRAPH")) {
@@ -828,7 +849,7 @@ orbx_status orbx_extract_batch_device(orbx_handle* h, const uint8_t* d_imgs, int
                                       int* d_counts, int cap, void* stream)
 {
     if (!h || !d_imgs || batch <= 0 || !d_kps || !d_desc || !d_counts || cap <= 0) return ORBX_EINVAL;
-    if (step < (size_t)cols || frame_stride < step * (size_t)rows) return ORBX_EINVAL;
+    if (step < (size_t)cols || (batch > 1 && frame_stride < step * (size_t)rows)) return ORBX_EINVAL;
     DeviceGuard guard(h->device);
     orbx_status st = ensure_geometry(h, rows, cols);
     if (st != ORBX_OK) return st;
@@ -847,7 +868,7 @@ orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* 
 {
     if (!h || stage < 0 || stage > 3 || !d_imgs || batch <= 0 || !d_kps || !d_desc || !d_counts || cap <= 0)
         return ORBX_EINVAL;
-    if (step < (size_t)cols || frame_stride < step * (size_t)rows) return ORBX_EINVAL;
+    if (step < (size_t)cols || (batch > 1 && frame_stride < step * (size_t)rows)) return ORBX_EINVAL;
     DeviceGuard guard(h->device);
     orbx_status st;
     if (stage == 0) {   // sizes the geometry and workspace; later stages must match them
@@ -969,8 +990,11 @@ orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys
     order_after_last(h, own_stream(h));
     const Geometry& g = h->geom;
     std::vector<int> cnt(g.ncells);
+    std::vector<uint32_t> addr(g.ncells);
     std::vector<uint32_t> sl(g.slots_per_frame);
     hipMemcpyAsync(cnt.data(), h->d_cell_counts + (size_t)frame * g.ncells, sizeof(int) * g.ncells,
+                   hipMemcpyDeviceToHost, own_stream(h));
+    hipMemcpyAsync(addr.data(), h->d_cell_addr + (size_t)frame * g.ncells, sizeof(uint32_t) * g.ncells,
                    hipMemcpyDeviceToHost, own_stream(h));
     hipMemcpyAsync(sl.data(), h->d_slots + (size_t)frame * g.slots_per_frame, sizeof(uint32_t) * g.slots_per_frame,
                    hipMemcpyDeviceToHost, own_stream(h));
@@ -979,7 +1003,7 @@ orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys
     int k = 0;
     for (int c = L.cell_begin; c < L.cell_begin + L.ncells; ++c) {
         for (int i = 0; i < cnt[c]; ++i) {
-            const uint32_t v = sl[h->cells[c].slot_base + i];
+            const uint32_t v = sl[addr[c] + i];
             if (k < cap && xys) {
                 xys[3 * k] = (int)(v & 0xFFF);
                 xys[3 * k + 1] = (int)((v >> 12) & 0xFFF);

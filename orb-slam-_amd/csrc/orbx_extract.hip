@@ -796,8 +796,8 @@ __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builti
 template <int TP, int LD>
 __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                    const Cell* __restrict__ cells, uint32_t* __restrict__ slots,
-                                                   int* __restrict__ cell_counts, int cb, int ce, int rw, int rh,
-                                                   int cpw)
+                                                   int* __restrict__ cell_counts, uint32_t* __restrict__ cell_addr,
+                                                   int cb, int ce, int rw, int rh, int cpw)
 {
     // cells [cb, ce); LDS sized from the group's largest cell ROI (rw x rh)
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
@@ -813,16 +813,18 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     uint32_t* obuf = (uint32_t*)((uint8_t*)list + fast_list_bytes(rw, rh));
     const int lcap = fast_list_cap(rw, rh);
     uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
-    // lane i: the wave's cell c0 + i -- its candidate count, and for a buffered cell its obuf offset and
-    // slot base; cells [fb0, current) are in obuf
-    int cnt_all = 0, c_off = 0, c_cnt = 0, c_slot = 0;
+    // lane i: the wave's cell c0 + i -- its candidate count, slot base, obuf offset (buffered cells) and the
+    // slot its candidates start at.  Buffered cells [fb0, current) go to HBM together, packed from the
+    // first one's slot base (their slot regions are consecutive and each holds its cell's count), so a
+    // wave's candidates form one run of whole lines for the quadtree's gather (cell_addr tells it where).
+    int cnt_all = 0, c_off = 0, c_slot = 0, c_addr = 0;
     int obn = 0, fb0 = 0;
     auto flush = [&](int fb1) {
-        for (int i = fb0; i < fb1; ++i) {
-            const int n = __builtin_amdgcn_readlane(c_cnt, i);
-            const int o = __builtin_amdgcn_readlane(c_off, i);
-            uint32_t* out = fslots + __builtin_amdgcn_readlane(c_slot, i);
-            for (int e = lane; e < n; e += 64) out[e] = obuf[o + e];
+        if (fb1 > fb0) {
+            const int base = __builtin_amdgcn_readlane(c_slot, fb0);
+            uint32_t* out = fslots + base;
+            for (int e = lane; e < obn; e += 64) out[e] = obuf[e];
+            if (lane >= fb0 && lane < fb1) c_addr = base + c_off;
         }
         obn = 0;
         fb0 = fb1;
@@ -877,6 +879,10 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     for (int c = c0; c < c1; ++c) {
         const int dw = C.roi_w - 6, dh = C.roi_h - 6;
         const Cell Cc = C;
+        if (lane == c - c0) {
+            c_slot = Cc.slot_base;
+            c_addr = Cc.slot_base;
+        }
         FP_STAMP(7);
         fast_commit(F, S, M, 0, tile);
         for (int u0 = LD; u0 * FastLaneMap<TP>::kRPP < S.rh; u0 += LD) {   // ROIs beyond LD passes
@@ -1049,11 +1055,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const int ci = c - c0;
             if (kept_n <= kFastObCap) {
                 if (obn + kept_n > kFastObCap) flush(ci);   // rare: the buffered cells go out first
-                if (lane == ci) {
-                    c_off = obn;
-                    c_cnt = kept_n;
-                    c_slot = Cc.slot_base;
-                }
+                if (lane == ci) c_off = obn;
                 uint32_t* dst = obuf + obn;
                 while (bits) {
                     const int jj = __builtin_ctzll(bits);
@@ -1062,7 +1064,9 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                     dst[idx++] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + lane), (uint32_t)(sc - 1));
                 }
                 obn += kept_n;
-            } else {
+            } else {   // rare: more than obuf holds; the buffered run ends before this cell's region
+                flush(ci);
+                fb0 = ci + 1;
                 uint32_t* dst = fslots + Cc.slot_base;
                 while (bits) {
                     const int jj = __builtin_ctzll(bits);
@@ -1080,7 +1084,10 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
 #endif
     }
     flush(c1 - c0);
-    if (lane < c1 - c0) cell_counts[(size_t)f * G->ncells + c0 + lane] = cnt_all;
+    if (lane < c1 - c0) {
+        cell_counts[(size_t)f * G->ncells + c0 + lane] = cnt_all;
+        cell_addr[(size_t)f * G->ncells + c0 + lane] = (uint32_t)c_addr;
+    }
 #ifdef ORBX_FAST_PROF
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_fast_prof[k], (unsigned long long)fp_acc[k]);
@@ -1154,7 +1161,7 @@ static void fast_launch(const ExtractBufs& b, const FramePtrs& p, int cb, int ce
     const size_t smem = fast_wave_bytes(rw, rh);
     hipFuncSetAttribute((const void*)k_fast_cells<TP, LD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_fast_cells<TP, LD>), grid, dim3(64), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
-                       cb, ce, rw, rh, cpw);
+                       b.cell_addr, cb, ce, rw, rh, cpw);
 }
 
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
@@ -1372,7 +1379,6 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
     }
 }
 
-template <int QT_NT, int QT_KPT, bool kG>
 #ifndef ORBX_QT0_WPE
 #define ORBX_QT0_WPE 4
 #endif
@@ -1391,31 +1397,33 @@ template <int QT_NT, int QT_KPT, bool kG>
 // Round 3: levels 1 and 2-7 at 128 / 96 VGPRs (4 / 5 waves per SIMD, no spill): their occupancy is set by
 // LDS and workgroup waves anyway (2 and 5 workgroups per CU), quadtree 0.165 -> 0.164 ms.
 // FAST at 5 (94 VGPRs, no spill) measured slower (485 -> 495 us) and keeps the compiler's choice.
+#define ORBX_QT_WPE(NT, KPT, G) ((G) ? 1                                          \
+                                 : ((NT) == 512 && (KPT) == 16) ? ORBX_QT0_WPE  \
+                                 : ((NT) == 512 && (KPT) == 8) ? ORBX_QT1_WPE   \
+                                 : ((NT) == 256) ? ORBX_QT2_WPE : 1)
 //
+// The node-list form of DistributeOctTree, one workgroup per (frame l's level l), used for the levels the
+// path-code kernel (k_qt_paths) does not take: node lists in global memory (kG), keys too wide for its
+// packed sort key, and more candidates than it holds.
 // kG: the node arrays live in the level's global region (LevelGeom::qtg_off) instead of LDS, with 32-bit
 // node indices, for budgets whose node list outgrows a workgroup's LDS (e.g. Tracking's
 // 2 * nFeatures initialisation extractor, src/Tracking.cc:133, at 4000 features).  The algorithm and its
 // order of operations are the same; only the wave totals and the shared scalars stay in LDS.
-__global__ __launch_bounds__(QT_NT, kG ? 1
-                                    : (QT_NT == 512 && QT_KPT == 16) ? ORBX_QT0_WPE
-                                    : (QT_NT == 512 && QT_KPT == 8) ? ORBX_QT1_WPE
-                                    : (QT_NT == 256) ? ORBX_QT2_WPE : 1) void k_quadtree(int level0, const Geometry* __restrict__ G,
-                                                   const Cell* __restrict__ cells,
-                                                   const uint32_t* __restrict__ slots,
-                                                   const int* __restrict__ cell_counts,
-                                                   uint32_t* __restrict__ spill,
-                                                   uint32_t* __restrict__ spill_node,
-                                                   uint8_t* __restrict__ gnodes,
-                                                   uint32_t* __restrict__ qt_out, int* __restrict__ qt_cnt,
-                                                   int* __restrict__ frame_counts, int* __restrict__ status,
-                                                   int lcap, int cellcap)
+template <int QT_NT, int QT_KPT, bool kG>
+__device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometry* __restrict__ G,
+                                         const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
+                                         const int* __restrict__ cell_counts, const uint32_t* __restrict__ cell_addr,
+                                         uint32_t* __restrict__ spill,
+                                         uint32_t* __restrict__ spill_node, uint8_t* __restrict__ gnodes,
+                                         uint32_t* __restrict__ qt_out, int* __restrict__ qt_cnt,
+                                         int* __restrict__ frame_counts, int* __restrict__ status, int lcap,
+                                         int cellcap)
 {
     // node index type; kNoneI marks "no node" (and compares above every valid rank)
     using Ix = typename std::conditional<kG, uint32_t, uint16_t>::type;
     constexpr Ix kNoneI = (Ix)~(Ix)0;
     constexpr uint32_t kPosMask = kG ? 0xFFFFFFFFu : 0xFFFFu;   // node position bits of a keypoint's node word
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int l = level0 + blockIdx.x, f = blockIdx.y;
     const int tid = threadIdx.x;
 #ifdef ORBX_QT_PROF
     const long long qt_t0 = clock64();
@@ -1459,7 +1467,7 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
     const bool gb_ok = !kG && ncl <= 65536 && (size_t)4 * ncl <= gregion;   // block-uniform
     for (int c = tid; c < ncl; c += QT_NT) {
         scan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
-        if (gb_ok) gbase[c] = (uint32_t)cells[cb + c].slot_base;
+        if (gb_ok) gbase[c] = cell_addr[(size_t)f * G->ncells + cb + c];
     }
     __syncthreads();
     const int n = (int)block_scan_excl<QT_NT>(scan, ncl, wsum);
@@ -1500,7 +1508,7 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
             const int mid = (lo + hi + 1) >> 1;
             if ((int)scan[mid] <= i) lo = mid; else hi = mid - 1;
         }
-        return fslots[cells[cb + lo].slot_base + (i - (int)scan[lo])];
+        return fslots[cell_addr[(size_t)f * G->ncells + cb + lo] + (i - (int)scan[lo])];
     };
     uint32_t kp[kKpL ? 1 : QT_KPT], nd[QT_KPT];
     // register slot r's keypoint (candidate tid + r * QT_NT)
@@ -1516,7 +1524,7 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
     if (staged) {
         for (int c = tid; c < ncl; c += QT_NT) {
             const int base = (int)scan[c], cnt = (c + 1 < ncl ? (int)scan[c + 1] : n) - base;
-            const uint32_t* src = fslots + cells[cb + c].slot_base;
+            const uint32_t* src = fslots + cell_addr[(size_t)f * G->ncells + cb + c];
             // 8 loads in flight per batch instead of one dependent HBM round trip per candidate
             for (int j0 = 0; j0 < cnt; j0 += 8) {
                 uint32_t v[8];
@@ -1978,15 +1986,570 @@ __global__ __launch_bounds__(QT_NT, kG ? 1
     }
 }
 
+template <int QT_NT, int QT_KPT, bool kG>
+__global__ __launch_bounds__(QT_NT, ORBX_QT_WPE(QT_NT, QT_KPT, kG)) void k_quadtree(
+    int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
+    const int* __restrict__ cell_counts, const uint32_t* __restrict__ cell_addr, uint32_t* __restrict__ spill,
+    uint32_t* __restrict__ spill_node, uint8_t* __restrict__ gnodes, uint32_t* __restrict__ qt_out,
+    int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap)
+{
+    qt_nodes<QT_NT, QT_KPT, kG>(level0 + blockIdx.x, blockIdx.y, G, cells, slots, cell_counts, cell_addr, spill,
+                                spill_node, gnodes, qt_out, qt_cnt, frame_counts, status, lcap, cellcap);
+}
+
+// ---------------------------------------------------------------------------
+// K3 on path codes (k_qt_paths): DistributeOctTree, src/ORBextractor.cc:644-907, one workgroup per
+// (frame, level), restated in tests/test_qt_pathcode.py (which checks it against the oracle).
+//
+// Every split halves a node's x range at UL.x + ceil((UR.x - UL.x) / 2) and its y range likewise
+// (ExtractorNode::DivideNode, :569-629), independently, so a keypoint's whole path down the tree is a
+// function of its x (and root, x / hX, :679) and of its y: two per-level tables (qp_tables) give it as a
+// sort key, root and the interleaved (right, bottom) digits above the FAST score.  Sorted by that key the
+// keypoints of any node at any depth are one contiguous run, and
+//   1. sort: a counting sort on the key's top bits (LDS atomics, one per run of equal bins in consecutive
+//      lanes), then each key's rank inside its bin;
+//   2. phase 1 (:710-803) needs no rounds: with fd(i) = the first depth at which sorted keys i - 1 and i
+//      lie in different cells, the node count after round d is #{fd <= d} and the expandable count
+//      #{fd <= d} - #{max(fd(i), fd(i + 1)) <= d}, two histograms of fd settle where phase 1 stops, and
+//      the list after round D is reverse(B_D) ++ S_{D-1} ++ ... ++ S_0 (children of round D in reverse
+//      creation order, then the single-keypoint nodes of each earlier round): a rank of per-node keys;
+//   3. phase 2 (:805-874) runs on nodes as in the node-list kernel, a split's four children being the
+//      digit runs inside its key range (binary searches instead of a pass over the keypoints);
+//   4. retain (:882-906): per node the highest score, ties to the first candidate in reference order
+//      (cell row, cell column, y, x).
+// Levels the packed key cannot hold (root bits + 2 digits per depth + 8 > 32), node lists in global memory
+// and more candidates than NT * KPT run the node-list body (qt_nodes) instead.
+// ---------------------------------------------------------------------------
+struct QpLayout {
+    size_t a, b, bins, cscan, cbase, wsum, sh, hist;
+    size_t nst, ncnt, ndep, srank, npos, snode, ccnt, cpos, vprev, vnew, skey, scan, scan2, zst, lkey;
+    size_t total;
+};
+
+__host__ __device__ inline QpLayout qp_layout(int ncap, int lcap, int cellcap, int nbins)
+{
+    QpLayout L;
+    size_t q = 0;   // node arrays, laid over the scatter array once the sort is done
+    auto sub = [&](size_t bytes) {
+        const size_t r = q;
+        q += (bytes + 15) & ~(size_t)15;
+        return r;
+    };
+    L.nst = sub(sizeof(uint32_t) * 2 * lcap);
+    L.ncnt = sub(sizeof(uint32_t) * 2 * lcap);
+    L.ndep = sub(2 * (size_t)lcap);
+    L.srank = sub(sizeof(uint16_t) * lcap);
+    L.npos = sub(sizeof(uint16_t) * lcap);
+    L.snode = sub(sizeof(uint16_t) * lcap);
+    L.ccnt = sub(sizeof(uint32_t) * 4 * lcap);    // the list keys (u64) before phase 2
+    L.cpos = sub(sizeof(uint16_t) * 4 * lcap + 4);   // the depth-D run starts (u32, lcap + 1) before phase 2
+    L.vprev = sub(sizeof(uint16_t) * lcap);
+    L.vnew = sub(sizeof(uint16_t) * lcap);
+    L.skey = sub(sizeof(uint32_t) * (lcap + 4));
+    L.scan = sub(sizeof(uint32_t) * (lcap + 1));
+    L.scan2 = sub(sizeof(uint32_t) * (lcap + 1));
+    L.lkey = L.ccnt;
+    L.zst = L.cpos;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t r = o;
+        o += (bytes + 15) & ~(size_t)15;
+        return r;
+    };
+    L.a = take(q > (size_t)4 * ncap ? q : (size_t)4 * ncap);
+    L.nst += L.a;
+    L.ncnt += L.a;
+    L.ndep += L.a;
+    L.srank += L.a;
+    L.npos += L.a;
+    L.snode += L.a;
+    L.ccnt += L.a;
+    L.cpos += L.a;
+    L.vprev += L.a;
+    L.vnew += L.a;
+    L.skey += L.a;
+    L.scan += L.a;
+    L.scan2 += L.a;
+    L.lkey += L.a;
+    L.zst += L.a;
+    L.b = take((size_t)4 * ncap);
+    L.bins = take(sizeof(uint32_t) * (nbins + 1));
+    L.cscan = take(sizeof(uint32_t) * cellcap);
+    L.cbase = take(sizeof(uint32_t) * cellcap);
+    L.wsum = take(sizeof(uint32_t) * 17);
+    L.sh = take(sizeof(int) * 16);
+    L.hist = take(sizeof(uint32_t) * 32);
+    L.total = o;
+    return L;
+}
+
+// ctr[key] += 1 for every lane with key >= 0, one LDS atomic per run of equal keys in consecutive lanes;
+// returns the lane's arrival slot (the counter before its own increment).  Called by whole waves.
+__device__ __forceinline__ uint32_t wave_run_slot(uint32_t* ctr, int key)
+{
+    const int lane = threadIdx.x & 63;
+    const int prev = __builtin_amdgcn_update_dpp(-2, key, 0x138, 0xF, 0xF, false);   // wave_shr:1, lane 0 <- -2
+    const unsigned long long heads = __ballot(key != prev);
+    uint32_t base = 0;
+    if (key >= 0 && key != prev) {
+        const unsigned long long later = lane == 63 ? 0ull : heads >> (lane + 1);
+        const int len = later ? (int)__builtin_ctzll(later) + 1 : 64 - lane;
+        base = atomicAdd(&ctr[key], (uint32_t)len);
+    }
+    const unsigned long long upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    const int head = 63 - (int)__builtin_clzll(upto);   // this lane's run head
+    base = (uint32_t)__shfl((int)base, head);
+    return base + (uint32_t)(lane - head);
+}
+
+// hist[v] += 1 for every active lane: one LDS atomic per distinct value in the wave.  Whole waves.
+__device__ __forceinline__ void wave_hist_add(uint32_t* hist, int v, bool act)
+{
+    const int lane = threadIdx.x & 63;
+    bool pending = act;
+    for (;;) {
+        const unsigned long long m = __ballot(pending);
+        if (!m) break;
+        const int first = (int)__builtin_ctzll(m);
+        const int val = __builtin_amdgcn_readlane(v, first);
+        const unsigned long long same = __ballot(pending && v == val);
+        if (lane == first) atomicAdd(&hist[val], (uint32_t)__popcll(same));
+        pending = pending && v != val;
+    }
+}
+
+__device__ __forceinline__ uint32_t compact_even(uint32_t x)   // bits 0, 2, 4, ... -> 0, 1, 2, ...
+{
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    x = (x | (x >> 8)) & 0x0000FFFFu;
+    return x;
+}
+
+template <int NT, int KPT>
+__global__ __launch_bounds__(NT, ORBX_QT_WPE(NT, KPT, false)) void k_qt_paths(
+    int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
+    const int* __restrict__ cell_counts, const uint32_t* __restrict__ cell_addr, const uint32_t* __restrict__ qpt,
+    uint32_t* __restrict__ spill,
+    uint32_t* __restrict__ spill_node, uint32_t* __restrict__ qt_out, int* __restrict__ qt_cnt,
+    int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap, int nbins)
+{
+    constexpr int NCAP = NT * KPT;
+    constexpr int NW = NT / 64;
+    constexpr uint16_t kNone = 0xFFFF;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int l = level0 + blockIdx.x, f = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const LevelGeom& LG = G->lv[l];
+    if (!LG.qp_ok) {   // level-uniform
+        qt_nodes<NT, KPT, false>(l, f, G, cells, slots, cell_counts, cell_addr, spill, spill_node, nullptr, qt_out,
+                                 qt_cnt, frame_counts, status, lcap, cellcap);
+        return;
+    }
+    const QpLayout Ly = qp_layout(NCAP, lcap, cellcap, nbins);
+    uint32_t* A = (uint32_t*)(smem + Ly.a);
+    uint32_t* B = (uint32_t*)(smem + Ly.b);
+    uint32_t* bins = (uint32_t*)(smem + Ly.bins);
+    uint32_t* cscan = (uint32_t*)(smem + Ly.cscan);
+    uint32_t* cbase = (uint32_t*)(smem + Ly.cbase);
+    uint32_t* wsum = (uint32_t*)(smem + Ly.wsum);
+    int* sh = (int*)(smem + Ly.sh);
+    uint32_t* hist = (uint32_t*)(smem + Ly.hist);
+    const int ncl = LG.ncells, cb = LG.cell_begin;
+    const int D = LG.qp_D, RB = LG.qp_rb;
+    const int bshift = 8 + RB + 2 * D - LG.qp_bb;
+    const int NB = 1 << LG.qp_bb;
+
+    // ---- 1. candidate counts and slot bases of the level's cells -----------------
+    for (int c = tid; c < ncl; c += NT) {
+        cscan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
+        cbase[c] = cell_addr[(size_t)f * G->ncells + cb + c];
+    }
+    for (int b = tid; b < NB; b += NT) bins[b] = 0u;
+    if (tid < 32) hist[tid] = 0u;
+    __syncthreads();
+    const int n = (int)block_scan_excl<NT>(cscan, ncl, wsum);
+    if (n > NCAP) {   // block-uniform: more candidates than this workgroup holds
+        qt_nodes<NT, KPT, false>(l, f, G, cells, slots, cell_counts, cell_addr, spill, spill_node, nullptr, qt_out,
+                                 qt_cnt, frame_counts, status, lcap, cellcap);
+        return;
+    }
+    uint32_t* out = qt_out + (size_t)f * G->out_per_frame + LG.out_off;
+    int L = 0, cur = 0;
+    bool ok = true;
+    if (n > 0) {   // block-uniform
+        // ---- 2. gather in reference order, keys, bin counts ------------------------------
+        uint16_t* owner = (uint16_t*)B;   // candidate -> cell (the sorted keys take B later)
+        for (int c = tid; c < ncl; c += NT) {
+            const int base = (int)cscan[c], cnt = (c + 1 < ncl ? (int)cscan[c + 1] : n) - base;
+            for (int j = 0; j < cnt; ++j) owner[base + j] = (uint16_t)c;
+        }
+        __syncthreads();
+        const uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
+        uint32_t v[KPT];
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const int ii = min(tid + r * NT, n - 1);
+            const int c = owner[ii];
+            v[r] = fslots[cbase[c] + (uint32_t)(ii - (int)cscan[c])];
+        }
+        const uint32_t* xk = qpt + LG.qp_xk;
+        const uint32_t* yk = qpt + LG.qp_yk;
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) v[r] = xk[v[r] & 0xFFFu] | yk[(v[r] >> 12) & 0xFFFu] | (v[r] >> 24);
+        uint32_t bs[KPT];
+        const int wave_i0 = tid - lane;
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            if (wave_i0 + r * NT >= n) break;   // wave-uniform
+            const int bin = tid + r * NT < n ? (int)(v[r] >> bshift) : -1;
+            bs[r] = ((uint32_t)bin << 16) | wave_run_slot(bins, bin);
+        }
+        __syncthreads();
+        block_scan_excl<NT>(bins, NB, wsum);
+        if (tid == 0) bins[NB] = (uint32_t)n;
+#pragma unroll
+        for (int r = 0; r < KPT; ++r)
+            if (tid + r * NT < n) A[bins[bs[r] >> 16] + (bs[r] & 0xFFFFu)] = v[r];
+        __syncthreads();
+        // ---- 3. rank inside the bin -> B sorted -------------------------------------------
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            const int p = tid + r * NT;
+            if (p < n) {
+                const uint32_t key = A[p];
+                const uint32_t b = key >> bshift;
+                const int s0 = (int)bins[b], s1 = (int)bins[b + 1];
+                int rk = 0;
+                for (int q = s0; q < s1; ++q) rk += A[q] < key;
+                B[s0 + rk] = key;
+            }
+        }
+        __syncthreads();
+        // ---- 4. phase 1 by the fd histograms ---------------------------------------------
+        auto fd = [&](int i) -> int {
+            if (i <= 0 || i >= n) return 0;
+            const uint32_t t = (B[i - 1] ^ B[i]) >> 8;
+            const int hb = 31 - (int)__builtin_clz(t);
+            return hb >= 2 * D ? 0 : D - (hb >> 1);
+        };
+#pragma unroll
+        for (int r = 0; r < KPT; ++r) {
+            if (wave_i0 + r * NT >= n) break;   // wave-uniform
+            const int i = tid + r * NT;
+            const bool act = i < n;
+            const int a = act ? fd(i) : 0, a1 = act ? fd(i + 1) : 0;
+            wave_hist_add(hist, a, act);
+            wave_hist_add(hist, 16 + (a > a1 ? a : a1), act);
+        }
+        __syncthreads();
+        const int N = LG.nfeat;
+        int Dp = D, ph2 = 0;
+        {
+            int cumL = (int)hist[0], cumM = (int)hist[16];
+            for (int d = 1; d <= D + 1; ++d) {   // :710-803 (round 1 always runs)
+                const int Ld = cumL + (d <= D ? (int)hist[d] : 0), Md = cumM + (d <= D ? (int)hist[16 + d] : 0);
+                if (Ld >= N || Ld == cumL) {
+                    Dp = d;
+                    break;
+                }
+                if (Ld + 3 * (Ld - Md) > N) {
+                    Dp = d;
+                    ph2 = 1;
+                    break;
+                }
+                cumL = Ld;
+                cumM = Md;
+            }
+            Dp = Dp < D ? Dp : D;   // past D every run is one keypoint: nothing changes
+        }
+        // ---- 5. the depth-Dp runs (the nodes) in key order ---------------------------------
+        uint32_t* zst = (uint32_t*)(smem + Ly.zst);
+        unsigned long long* lkey = (unsigned long long*)(smem + Ly.lkey);
+        {
+            const int per = (n + NT - 1) / NT;
+            const int b0 = tid * per, e0 = min(n, b0 + per);
+            uint32_t local = 0;
+            for (int i = b0; i < e0; ++i) local += fd(i) <= Dp ? 1u : 0u;
+            const uint32_t inc = wave_incl_scan(local);
+            if (lane == 63) wsum[tid >> 6] = inc;
+            __syncthreads();
+            uint32_t run = inc - local, total = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t t = wsum[w];
+                run += w < (tid >> 6) ? t : 0u;
+                total += t;
+            }
+            for (int i = b0; i < e0; ++i)
+                if (fd(i) <= Dp) zst[run++] = (uint32_t)i;
+            L = (int)total;
+            if (tid == 0) zst[L] = (uint32_t)n;
+        }
+        __syncthreads();
+        // list keys: group Dp - b (b = the round that created the node), then the first b digits with
+        // reverse(B_b)'s directions (digit j ascending iff b - j is odd, the root like digit 1)
+        for (int id = tid; id < L; id += NT) {
+            const int s = (int)zst[id], c = (int)zst[id + 1] - s;
+            int b = Dp;
+            if (c == 1) {
+                const int f0 = fd(s), f1 = fd(s + 1);
+                b = f0 > f1 ? f0 : f1;
+            }
+            const uint32_t path = B[s] >> 8;
+            uint32_t root = path >> (2 * D);
+            uint32_t pd = (path & ((1u << (2 * D)) - 1u)) >> (2 * (D - b));
+            if (b & 1) root ^= (1u << RB) - 1u;
+            pd ^= 0x33333333u & ((1u << (2 * b)) - 1u);
+            const uint32_t tk = ((root << (2 * b)) | pd) << (2 * (D - b));
+            lkey[id] = ((unsigned long long)(Dp - b) << 32) | tk;
+        }
+        __syncthreads();
+        uint32_t* nst0 = (uint32_t*)(smem + Ly.nst);
+        uint32_t* ncnt0 = (uint32_t*)(smem + Ly.ncnt);
+        uint8_t* ndep0 = smem + Ly.ndep;
+        uint32_t* scan = (uint32_t*)(smem + Ly.scan);
+        {
+            const int L2 = (L + 1) >> 1;
+            const ulonglong2* k2 = (const ulonglong2*)lkey;
+            for (int id = tid; id < L; id += NT) {
+                const unsigned long long key = lkey[id];
+                int pos = 0;
+                for (int j = 0; j < L2; ++j) {
+                    const ulonglong2 u = k2[j];
+                    pos += (int)(u.x < key) + (int)(2 * j + 1 < L && u.y < key);
+                }
+                const int s = (int)zst[id], c = (int)zst[id + 1] - s;
+                nst0[pos] = (uint32_t)s;
+                ncnt0[pos] = (uint32_t)c;
+                ndep0[pos] = (uint8_t)Dp;
+                scan[pos] = (key >> 32) == 0 && c > 1 ? 1u : 0u;   // phase 2's first vPrev (group 0, expandable)
+            }
+        }
+        __syncthreads();
+        // ---- 6. phase 2 on nodes (:805-874) ---------------------------------------------------
+        if (ph2) {   // block-uniform
+            uint16_t* vprev = (uint16_t*)(smem + Ly.vprev);
+            uint16_t* vnew = (uint16_t*)(smem + Ly.vnew);
+            uint16_t* srank = (uint16_t*)(smem + Ly.srank);
+            uint16_t* npos = (uint16_t*)(smem + Ly.npos);
+            uint16_t* snode = (uint16_t*)(smem + Ly.snode);
+            uint32_t* ccnt = (uint32_t*)(smem + Ly.ccnt);
+            uint16_t* cpos = (uint16_t*)(smem + Ly.cpos);
+            uint32_t* skey = (uint32_t*)(smem + Ly.skey);
+            uint32_t* scan2 = (uint32_t*)(smem + Ly.scan2);
+            // vPrev in creation order = group 0's expandable nodes in descending list position
+            const uint32_t m0 = block_scan_fn<NT>(scan2, L, wsum, [&](int p) { return scan[p]; });
+            for (int p = tid; p < L; p += NT)
+                if (scan[p]) vprev[m0 - 1 - scan2[p]] = (uint16_t)p;
+            if (tid == 0) {
+                sh[SH_L] = L;
+                sh[SH_M] = (int)m0;
+                sh[SH_DONE] = 0;
+                sh[SH_ERR] = 0;
+            }
+            while (true) {
+                __syncthreads();
+                if (sh[SH_DONE]) break;
+                const int Lc = sh[SH_L];
+                const int m = sh[SH_M];
+                uint32_t* stc = (uint32_t*)(smem + Ly.nst) + (size_t)cur * lcap;
+                uint32_t* stn = (uint32_t*)(smem + Ly.nst) + (size_t)(cur ^ 1) * lcap;
+                uint32_t* cntc = (uint32_t*)(smem + Ly.ncnt) + (size_t)cur * lcap;
+                uint32_t* cntn = (uint32_t*)(smem + Ly.ncnt) + (size_t)(cur ^ 1) * lcap;
+                uint8_t* dpc = smem + Ly.ndep + (size_t)cur * lcap;
+                uint8_t* dpn = smem + Ly.ndep + (size_t)(cur ^ 1) * lcap;
+                const uint16_t* vin = cur ? vnew : vprev;
+                uint16_t* vout = cur ? vprev : vnew;
+                // A: vPrev ranked by (size, creation) descending (unique keys: one barrier); the ranking
+                // thread also finds the candidate's four child runs (digit dp + 1 inside its key range)
+                const int m4 = (m + 3) >> 2;
+                for (int k = tid; k < 4 * m4; k += NT) skey[k] = k < m ? (cntc[vin[k]] << 16) | (uint32_t)k : 0u;
+                for (int p = tid; p < Lc; p += NT) srank[p] = kNone;
+                if (tid == 0) sh[SH_KK] = m;
+                __syncthreads();
+                {
+                    const uint4* k4 = (const uint4*)skey;
+                    for (int k = tid; k < m; k += NT) {
+                        const uint32_t key = skey[k];
+                        int j = 0;
+                        for (int i4 = 0; i4 < m4; ++i4) {
+                            const uint4 u = k4[i4];
+                            j += (int)(u.x > key) + (int)(u.y > key) + (int)(u.z > key) + (int)(u.w > key);
+                        }
+                        const int p = vin[k];
+                        srank[p] = (uint16_t)j;
+                        snode[j] = (uint16_t)p;
+                        const int s = (int)stc[p], c = (int)cntc[p];
+                        const int sd = 8 + 2 * (D - (dpc[p] + 1));   // the child digit's bit position
+                        int lo = s;
+                        for (int q = 0; q < 3; ++q) {   // first key with digit > q
+                            int a = lo, e = s + c;
+                            while (a < e) {
+                                const int mid = (a + e) >> 1;
+                                if ((int)((B[mid] >> sd) & 3u) <= q) a = mid + 1; else e = mid;
+                            }
+                            ccnt[4 * p + q] = (uint32_t)(a - lo);
+                            lo = a;
+                        }
+                        ccnt[4 * p + 3] = (uint32_t)(s + c - lo);
+                    }
+                }
+                __syncthreads();
+                // C: children (low half) and expandable children (high half) per split rank
+                const int S = m;
+                auto kids = [&](int s) -> uint32_t {
+                    const int p = snode[s];
+                    uint32_t v2 = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t c = ccnt[4 * p + q];
+                        v2 += (c > 0 ? 1u : 0u) + (c > 1 ? 0x10000u : 0u);
+                    }
+                    return v2;
+                };
+                const uint32_t T = block_scan_fn<NT>(scan, S, wsum, kids);
+                // how many candidates are split: the size after splitting j grows with j (a split node
+                // leaves >= 1 child), so the one j that crosses N writes (:843-845)
+                for (int j = tid; j < S; j += NT) {
+                    const int cs = (int)(kids(j) & 0xFFFFu), sj = (int)(scan[j] & 0xFFFFu);
+                    if (Lc + sj + cs - (j + 1) >= N && Lc + sj - j < N) sh[SH_KK] = j + 1;
+                }
+                __syncthreads();
+                const int kk = sh[SH_KK];
+                const uint32_t pre = kk < S ? scan[kk] : T;
+                block_scan_fn<NT>(scan2, Lc, wsum, [&](int p) {
+                    return (srank[p] != kNone && (int)srank[p] < kk) ? 1u : 0u;
+                });
+                const int Ctot = (int)(pre & 0xFFFFu), nexp = (int)(pre >> 16);
+                const int newL = Ctot + (Lc - kk);
+                if (newL > lcap) {
+                    if (tid == 0) {
+                        sh[SH_ERR] |= kStatusListOverflow;
+                        sh[SH_DONE] = 1;
+                    }
+                    continue;
+                }
+                // D: the new list: children of split rank s at Ctot - prefix(s) - children(s) (later splits
+                // in front, n4..n1), the rest after them in order; expandable children in creation order
+                for (int s = tid; s < kk; s += NT) {
+                    const int p = snode[s];
+                    const uint32_t ps = scan[s];
+                    uint32_t c4[4];
+                    int cs = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        c4[q] = ccnt[4 * p + q];
+                        cs += c4[q] > 0;
+                    }
+                    const int pos0 = Ctot - (int)(ps & 0xFFFFu) - cs;
+                    int e = (int)(ps >> 16);
+                    int np = pos0 + cs;   // n1 lands last (it was pushed first)
+                    uint32_t st = stc[p];
+                    const uint8_t dch = (uint8_t)(dpc[p] + 1);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t c = c4[q];
+                        if (c == 0) continue;
+                        --np;
+                        stn[np] = st;
+                        cntn[np] = c;
+                        dpn[np] = dch;
+                        st += c;
+                        if (c > 1) vout[e++] = (uint16_t)np;   // creation order: split rank, then n1..n4
+                    }
+                }
+                for (int p = tid; p < Lc; p += NT) {
+                    const bool split = srank[p] != kNone && (int)srank[p] < kk;
+                    if (!split) {
+                        const int np = Ctot + p - (int)scan2[p];
+                        stn[np] = stc[p];
+                        cntn[np] = cntc[p];
+                        dpn[np] = dpc[p];
+                    }
+                }
+                if (tid == 0) {
+                    sh[SH_L] = newL;
+                    if (newL >= N || newL == Lc) sh[SH_DONE] = 1;
+                    sh[SH_M] = nexp;
+                }
+                __syncthreads();
+                cur ^= 1;
+                (void)npos;
+                (void)cpos;
+            }
+            __syncthreads();
+            L = sh[SH_L];
+            ok = sh[SH_ERR] == 0;
+        }
+        // ---- 7. retain the best keypoint per node (:882-906) ------------------------------------
+        const uint32_t* stf = (uint32_t*)(smem + Ly.nst) + (size_t)cur * lcap;
+        const uint32_t* cntf = (uint32_t*)(smem + Ly.ncnt) + (size_t)cur * lcap;
+        const int outn = ok ? (L < LG.cap ? L : LG.cap) : 0;
+        const uint32_t* xinv = qpt + LG.qp_xi;
+        const uint32_t* yinv = qpt + LG.qp_yi;
+        const uint32_t dmask = (1u << (2 * D)) - 1u;
+        for (int p = tid; p < outn; p += NT) {
+            const int s = (int)stf[p], c = (int)cntf[p];
+            uint32_t ms = 0;
+            for (int j = s; j < s + c; ++j) ms = max(ms, B[j] & 0xFFu);
+            unsigned long long bo = ~0ull;
+            uint32_t bx = 0, by = 0;
+            for (int j = s; j < s + c; ++j) {
+                const uint32_t k = B[j];
+                if ((k & 0xFFu) != ms) continue;
+                const uint32_t path = k >> 8, dg = path & dmask;
+                const uint32_t x = xinv[((path >> (2 * D)) << D) | compact_even(dg)];
+                const uint32_t y = yinv[compact_even(dg >> 1)];
+                // reference order: cell row, cell column (src/ORBextractor.cc:952-1000), then cv::FAST's
+                // row-major order inside the cell
+                const unsigned long long o = ((unsigned long long)((y - 3) / (uint32_t)LG.qp_hc) << 40) |
+                                             ((unsigned long long)((x - 3) / (uint32_t)LG.qp_wc) << 24) |
+                                             ((unsigned long long)y << 12) | x;
+                if (o < bo) {
+                    bo = o;
+                    bx = x;
+                    by = y;
+                }
+            }
+            out[p] = pack_kp(bx + kMinBorder, by + kMinBorder, ms);
+        }
+        if (!ok) L = 0;
+        if (tid == 0) {
+            const int on = outn;
+            qt_cnt[(size_t)f * G->nlevels + l] = on;
+            atomicAdd(&frame_counts[f], on);
+            int err = ok ? 0 : kStatusListOverflow;
+            if (ok && L > LG.cap) err |= kStatusOutOverflow;
+            if (err) atomicOr(status, err);
+        }
+        return;
+    }
+    if (tid == 0) qt_cnt[(size_t)f * G->nlevels + l] = 0;
+}
+
 template <int NT, int KPT, bool kG>
 static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
                       hipStream_t s)
 {
-    const size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap, 2, qt_kpn(NT, KPT, 0)).total;
+    size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap, 2, qt_kpn(NT, KPT, 0)).total;
+    if constexpr (!kG) {
+        if (q.nbins > 0 && !getenv("ORBX_QT_NODES")) {   // the path-code kernel (its fallback body needs smem too)
+            smem = std::max(smem, qp_layout(NT * KPT, q.lcap, q.cellcap, q.nbins).total);
+            hipFuncSetAttribute((const void*)k_qt_paths<NT, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)smem);
+            hipLaunchKernelGGL((k_qt_paths<NT, KPT>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
+                               b.slots, b.cell_counts, b.cell_addr, b.qpt, b.spill, b.spill_node, b.qt_out,
+                               b.qt_cnt, frame_counts, b.status, q.lcap, q.cellcap, q.nbins);
+            return;
+        }
+    }
     hipFuncSetAttribute((const void*)k_quadtree<NT, KPT, kG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_quadtree<NT, KPT, kG>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
-                       b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt, frame_counts,
-                       b.status, q.lcap, q.cellcap);
+                       b.slots, b.cell_counts, b.cell_addr, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt,
+                       frame_counts, b.status, q.lcap, q.cellcap);
 }
 
 // Launch groups.  A group's node capacity is the largest cap + 4 of its levels: a level's list never holds
@@ -1998,9 +2561,11 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
     auto caps = [&](QtGroup& q) {
         q.lcap = 8;
         q.cellcap = 1;
+        q.nbins = 0;   // 0: no level of the group takes the path-code kernel
         for (int l = q.l0; l < q.l0 + q.nl; ++l) {
             q.lcap = std::max(q.lcap, g.lv[l].cap + 4);
             q.cellcap = std::max(q.cellcap, g.lv[l].ncells);
+            if (g.lv[l].qp_ok) q.nbins = std::max(q.nbins, 1 << g.lv[l].qp_bb);
         }
     };
     bool anyg = false;
@@ -2009,7 +2574,7 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
     // the levels run concurrently instead of as dependent launches (latency, not throughput).
     // A level run with more register capacity than qt_regcap(g, l) spills less than its region holds.
     if (batch <= kQtMergedMaxBatch && !anyg) {
-        QtGroup q{0, g.nlevels, 512, g.qt_kpt0, 0, 0, 0};
+        QtGroup q{0, g.nlevels, 512, g.qt_kpt0, 0, 0, 0, 0};
         caps(q);
         if (qt_layout(q.lcap, q.cellcap, 2, qt_kpn(q.nt, q.kpt, 0)).total <= kQtLdsMax) {
             out[0] = q;
@@ -2023,7 +2588,7 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
         const int nt = qt_nt(g, l0), kpt = qt_kpt(g, l0), gl = g.lv[l0].qt_glob;
         int l1 = l0 + 1;
         while (l1 < g.nlevels && qt_nt(g, l1) == nt && qt_kpt(g, l1) == kpt && g.lv[l1].qt_glob == gl) ++l1;
-        QtGroup q{l0, l1 - l0, nt, kpt, gl, 0, 0};
+        QtGroup q{l0, l1 - l0, nt, kpt, gl, 0, 0, 0};
         caps(q);
         out[n++] = q;
         l0 = l1;
@@ -2067,6 +2632,81 @@ bool qt_prepare(Geometry& g)
         }
         g.qtg_per_frame = off;
         return true;
+    }
+}
+
+// K3 path tables (tests/test_qt_pathcode.py restates them).  DivideNode (src/ORBextractor.cc:569-629) splits
+// an axis range [lo, hi] at lo + ceil((hi - lo) / 2), keypoints below the midline going to the first half;
+// the roots are [(int)(hX * i), (int)(hX * (i + 1))] x [0, qh] (:663-675), a keypoint's root (int)(x / hX)
+// (:681).  D = the depth at which every root range and the y range are down to single coordinates.
+static int qp_depth(int npts)
+{
+    if (npts <= 1) return 0;
+    const int h = (int)std::ceil((float)(npts - 1) / 2);
+    return 1 + std::max(qp_depth(h), qp_depth(npts - h));
+}
+
+void qp_tables(Geometry& g, std::vector<uint32_t>& tab)
+{
+    tab.clear();
+    for (int l = 0; l < g.nlevels; ++l) {
+        LevelGeom& L = g.lv[l];
+        L.qp_ok = 0;
+        const int nIni = L.nIni;
+        const float hX = L.hX;
+        std::vector<int> rx0(nIni), rx1(nIni);
+        int D = qp_depth(L.qh + 1);
+        for (int i = 0; i < nIni; ++i) {
+            rx0[i] = (int)(hX * (float)i);
+            rx1[i] = (int)(hX * (float)(i + 1));
+            D = std::max(D, qp_depth(rx1[i] - rx0[i] + 1));
+        }
+        int rb = 1;
+        while ((1 << rb) < nIni) ++rb;
+        if (L.qt_glob || rb + 2 * D + 8 > 32 || D < 1) continue;
+        int bb = 0;   // sort bins: about four candidates per bin when the workgroup is full
+        while ((8 << bb) <= qt_regcap(g, l)) ++bb;
+        L.qp_ok = 1;
+        L.qp_D = D;
+        L.qp_rb = rb;
+        L.qp_bb = std::min(bb, rb + 2 * D);
+        L.qp_xk = (int)tab.size();
+        tab.resize(tab.size() + L.w);
+        L.qp_yk = (int)tab.size();
+        tab.resize(tab.size() + L.h);
+        L.qp_xi = (int)tab.size();
+        tab.resize(tab.size() + ((size_t)nIni << D), 0xFFFFFFFFu);
+        L.qp_yi = (int)tab.size();
+        tab.resize(tab.size() + ((size_t)1 << D), 0xFFFFFFFFu);
+        for (int x = 0; x < L.w; ++x) {
+            const int r = std::min((int)((float)x / hX), nIni - 1);
+            int x0 = rx0[r], x1 = rx1[r];
+            uint32_t code = (uint32_t)r, bits = 0;
+            for (int j = 0; j < D; ++j) {
+                const int mid = x0 + (int)std::ceil((float)(x1 - x0) / 2);
+                const uint32_t bit = x >= mid ? 1u : 0u;
+                code = (code << 2) | bit;
+                bits = (bits << 1) | bit;
+                if (bit) x0 = mid; else x1 = mid;
+            }
+            tab[L.qp_xk + x] = code << 8;
+            uint32_t& inv = tab[L.qp_xi + (((size_t)r << D) | bits)];
+            if (inv == 0xFFFFFFFFu) inv = (uint32_t)x;   // the smallest coordinate of a code is the keypoints'
+        }
+        for (int y = 0; y < L.h; ++y) {
+            int y0 = 0, y1 = L.qh;
+            uint32_t code = 0, bits = 0;
+            for (int j = 0; j < D; ++j) {
+                const int mid = y0 + (int)std::ceil((float)(y1 - y0) / 2);
+                const uint32_t bit = y >= mid ? 1u : 0u;
+                code = (code << 2) | (bit << 1);
+                bits = (bits << 1) | bit;
+                if (bit) y0 = mid; else y1 = mid;
+            }
+            tab[L.qp_yk + y] = code << 8;
+            uint32_t& inv = tab[L.qp_yi + bits];
+            if (inv == 0xFFFFFFFFu) inv = (uint32_t)y;
+        }
     }
 }
 

@@ -16,7 +16,7 @@ import csv, sys, collections
 d = collections.defaultdict(list)
 for r in csv.DictReader(open(sys.argv[1])):
     n = r["Kernel_Name"].split("(")[0].replace("void ", "")
-    if "pyramid" in n or "fast" in n or "quadtree" in n:
+    if "pyramid" in n or "fast" in n or "quadtree" in n or "qt_" in n:
         d[(n, int(r.get("Grid_Size_X", r.get("Grid_Size", 0))) * int(r.get("Grid_Size_Y", 1)) * int(r.get("Grid_Size_Z", 1)),
            int(r.get("LDS_Block_Size", r.get("Lds_Size", 0)) or 0))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k in sorted(d):

@@ -14,7 +14,11 @@ import csv
 import glob
 import json
 import os
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from srchash import kernel_sources_sha256  # noqa: E402
 
 
 def load(counter_dir, counter):
@@ -52,7 +56,7 @@ def main():
         doc = {"batch": a.batch, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
                "python3 bench.py --steps 5 --warmup 1 --no-cpu --batch %d" % a.batch,
                "bytes_per_launch": "2 x FETCH_SIZE + WRITE_SIZE (KiB x 1024), averaged over dispatches",
-               "kernels": out}
+               "kernel_sources_sha256": kernel_sources_sha256(), "kernels": out}
         json.dump(doc, open(a.profiles, "w"), indent=1)
 
 

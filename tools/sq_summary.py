@@ -29,6 +29,9 @@ for k, c in sorted(vals.items()):
 
 if save:
     import json
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from srchash import kernel_sources_sha256
     out = {}
     for k, c in vals.items():
         if k.startswith("k_"):
@@ -36,5 +39,6 @@ if save:
             out[k]["dispatches"] = len(next(iter(c.values())))
     json.dump({"batch": 384, "source": "rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU "
                "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -- python3 bench.py --steps 3 "
-               "--warmup 1 --no-cpu --streams 1 --iso-steps 0 (tools/gpu_sq.sh)", "per_dispatch_averages": out},
+               "--warmup 1 --no-cpu --streams 1 --iso-steps 0 (tools/gpu_sq.sh)",
+               "kernel_sources_sha256": kernel_sources_sha256(), "per_dispatch_averages": out},
               open(save, "w"), indent=1)
