@@ -793,6 +793,9 @@ __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builti
 #ifndef ORBX_FAST_SPT
 #define ORBX_FAST_SPT 1   // strength entries per lane per trip
 #endif
+#ifndef ORBX_FAST_P1
+#define ORBX_FAST_P1 2    // pass 1: 2 = compile-time column width, unchecked full trips; 1 = round 3's loop
+#endif
 template <int TP, int LD>
 __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                    const Cell* __restrict__ cells, uint32_t* __restrict__ slots,
@@ -813,22 +816,15 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     uint32_t* obuf = (uint32_t*)((uint8_t*)list + fast_list_bytes(rw, rh));
     const int lcap = fast_list_cap(rw, rh);
     uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
-    // lane i: the wave's cell c0 + i -- its candidate count, slot base, obuf offset (buffered cells) and the
-    // slot its candidates start at.  Buffered cells [fb0, current) go to HBM together, packed from the
-    // first one's slot base (their slot regions are consecutive and each holds its cell's count), so a
-    // wave's candidates form one run of whole lines for the quadtree's gather (cell_addr tells it where).
-    int cnt_all = 0, c_off = 0, c_slot = 0, c_addr = 0;
-    int obn = 0, fb0 = 0;
-    auto flush = [&](int fb1) {
-        if (fb1 > fb0) {
-            const int base = __builtin_amdgcn_readlane(c_slot, fb0);
-            uint32_t* out = fslots + base;
-            for (int e = lane; e < obn; e += 64) out[e] = obuf[e];
-            if (lane >= fb0 && lane < fb1) c_addr = base + c_off;
-        }
-        obn = 0;
-        fb0 = fb1;
-    };
+    // lane i: the wave's cell c0 + i -- its candidate count, obuf offset (buffered cells) and the slot its
+    // candidates start at.  The wave's first cells are buffered in obuf and go to HBM together after its
+    // last cell, packed from the first cell's slot base (consecutive slot regions, each holding its cell's
+    // count), so a wave's candidates form one run of whole lines for the quadtree's gather (cell_addr says
+    // where each cell's start).  A cell that does not fit writes straight to its own slot region, and so do
+    // the wave's later cells: the packed run then ends before that region.
+    int cnt_all = 0, c_off = -1, c_addr = 0;   // c_off >= 0: the lane's cell is buffered
+    int obn = 0;
+    bool direct = false;   // wave-uniform
     // kept-pixel bitmask, one u64 per window row: aliases the tile, which is dead once every strength
     // of the cell is known
     unsigned long long* kept = (unsigned long long*)tile;
@@ -879,10 +875,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     for (int c = c0; c < c1; ++c) {
         const int dw = C.roi_w - 6, dh = C.roi_h - 6;
         const Cell Cc = C;
-        if (lane == c - c0) {
-            c_slot = Cc.slot_base;
-            c_addr = Cc.slot_base;
-        }
+        if (lane == c - c0) c_addr = Cc.slot_base;
         FP_STAMP(7);
         fast_commit(F, S, M, 0, tile);
         for (int u0 = LD; u0 * FastLaneMap<TP>::kRPP < S.rh; u0 += LD) {   // ROIs beyond LD passes
@@ -910,6 +903,38 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         // and are masked out.  Pixels are named by their window index m = i * TP + j: the pixel's tile
         // value is tile[m + 3 * TP + 3] and its map byte map[m + TP + 1], so every ring, compass and
         // neighbour access is (tile or map) + m plus a non-negative immediate offset.
+        int nf = 0, nb = 0;   // front / back entries
+#if ORBX_FAST_P1 == 2
+        // Exec for the list writes comes straight from the scalar masks (inverse ballot: no per-lane flag
+        // in a VGPR, no VALU compare to rebuild it).  The order of entries inside a list does not matter
+        // (survivors are emitted through the row bitmask), so a trip's back entries take
+        // [lcap - nb - count, lcap - nb) in lane order.  (Tried: a compile-time column width with immediate
+        // second-row offsets and unchecked full trips: 85-95 VGPRs instead of 80, 6 -> 5 waves per SIMD.)
+        const int cw_shift = dw <= 32 ? 5 : 6;
+        const int col = lane & ((1 << cw_shift) - 1);
+        const int rstep = 64 >> cw_shift;
+        const int rlane = lane >> cw_shift;
+        const unsigned long long colmask = ballot64(col < dw);
+        int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
+        for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {
+            const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
+            const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
+            const unsigned long long va = colmask & ballot64(rlane < dh - r0);
+            const unsigned long long vb = colmask & ballot64(rlane < dh - r0 - rstep);
+            const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
+            const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
+            const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
+            if (__builtin_amdgcn_inverse_ballot_w64(mfa)) list[nf + lanes_below(mfa)] = (uint16_t)t;
+            nf += __popcll(mfa);
+            if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
+            nf += __popcll(mfb);
+            nb += __popcll(mba);
+            if (__builtin_amdgcn_inverse_ballot_w64(mba)) list[lcap - nb + lanes_below(mba)] = (uint16_t)t;
+            nb += __popcll(mbb);
+            if (__builtin_amdgcn_inverse_ballot_w64(mbb)) list[lcap - nb + lanes_below(mbb)] = (uint16_t)(t + rstep * TP);
+            t += 2 * rstep * TP;
+        }
+#else
         const int cw_shift = dw <= 32 ? 5 : 6;
         const int col = lane & ((1 << cw_shift) - 1);
         const int rstep = 64 >> cw_shift;
@@ -917,7 +942,6 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         const bool col_ok = col < dw;
         const unsigned long long colmask = ballot64(col_ok);
         int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
-        int nf = 0, nb = 0;   // front / back entries
         for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {
             const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
             const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
@@ -941,6 +965,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             nb += __popcll(mbb);
             t += 2 * rstep * TP;
         }
+#endif
         wave_lds_sync();
         FP_STAMP(2);
 
@@ -1053,8 +1078,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             unsigned long long bits = rowbits;
             int idx = base;
             const int ci = c - c0;
-            if (kept_n <= kFastObCap) {
-                if (obn + kept_n > kFastObCap) flush(ci);   // rare: the buffered cells go out first
+            if (!direct && obn + kept_n <= kFastObCap) {
                 if (lane == ci) c_off = obn;
                 uint32_t* dst = obuf + obn;
                 while (bits) {
@@ -1064,9 +1088,8 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                     dst[idx++] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + lane), (uint32_t)(sc - 1));
                 }
                 obn += kept_n;
-            } else {   // rare: more than obuf holds; the buffered run ends before this cell's region
-                flush(ci);
-                fb0 = ci + 1;
+            } else {   // rare: more than obuf holds
+                direct = true;
                 uint32_t* dst = fslots + Cc.slot_base;
                 while (bits) {
                     const int jj = __builtin_ctzll(bits);
@@ -1083,7 +1106,14 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         fp_acc[6] += 1;
 #endif
     }
-    flush(c1 - c0);
+    if (obn > 0) {   // the buffered cells, packed from the wave's first cell's slot base
+        const int base = cells[c0].slot_base;
+        uint32_t* out = fslots + base;
+        if (lane < obn) out[lane] = obuf[lane];
+        if (lane + 64 < obn) out[lane + 64] = obuf[lane + 64];
+        static_assert(kFastObCap <= 128, "two stores per lane");
+        if (c_off >= 0) c_addr = base + c_off;
+    }
     if (lane < c1 - c0) {
         cell_counts[(size_t)f * G->ncells + c0 + lane] = cnt_all;
         cell_addr[(size_t)f * G->ncells + c0 + lane] = (uint32_t)c_addr;
@@ -1380,7 +1410,7 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 }
 
 #ifndef ORBX_QT0_WPE
-#define ORBX_QT0_WPE 4
+#define ORBX_QT0_WPE 3   // round 4: the path-code kernel's fallback; 3 keeps it free of scratch (168 VGPRs)
 #endif
 #ifndef ORBX_QT1_WPE
 #define ORBX_QT1_WPE 4
@@ -1991,8 +2021,11 @@ __global__ __launch_bounds__(QT_NT, ORBX_QT_WPE(QT_NT, QT_KPT, kG)) void k_quadt
     int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
     const int* __restrict__ cell_counts, const uint32_t* __restrict__ cell_addr, uint32_t* __restrict__ spill,
     uint32_t* __restrict__ spill_node, uint8_t* __restrict__ gnodes, uint32_t* __restrict__ qt_out,
-    int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap)
+    int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap,
+    int only_flagged)
 {
+    // only_flagged: the path-code kernel's fallback launch, for the (frame, level)s it left (count -1)
+    if (only_flagged && qt_cnt[(size_t)blockIdx.y * G->nlevels + level0 + blockIdx.x] != -1) return;
     qt_nodes<QT_NT, QT_KPT, kG>(level0 + blockIdx.x, blockIdx.y, G, cells, slots, cell_counts, cell_addr, spill,
                                 spill_node, gnodes, qt_out, qt_cnt, frame_counts, status, lcap, cellcap);
 }
@@ -2021,59 +2054,63 @@ __global__ __launch_bounds__(QT_NT, ORBX_QT_WPE(QT_NT, QT_KPT, kG)) void k_quadt
 // and more candidates than NT * KPT run the node-list body (qt_nodes) instead.
 // ---------------------------------------------------------------------------
 struct QpLayout {
-    size_t a, b, bins, cscan, cbase, wsum, sh, hist;
-    size_t nst, ncnt, ndep, srank, npos, snode, ccnt, cpos, vprev, vnew, skey, scan, scan2, zst, lkey;
+    size_t k, x, cscan, cbase, wsum, sh, hist;
+    // inside x, once the sort is done: the node arrays, then the fd bytes (later the inverse tables)
+    size_t nst, ncnt, ndep, srank, snode, ccnt, vprev, vnew, skey, scan, scan2, zst, lkey, fdv;
     size_t total;
 };
 
-__host__ __device__ inline QpLayout qp_layout(int ncap, int lcap, int cellcap, int nbins)
+// k: the candidates' keys (gather: owner map and key tables; then sorted in place).  x: the sort bins, then
+// the node arrays and the fd bytes / inverse tables.  ncap: candidates a workgroup holds; ninv: the largest
+// level's inverse-table entries (u32); nbins: the largest level's sort bins.
+__host__ __device__ inline QpLayout qp_layout(int ncap, int lcap, int cellcap, int ninv, int nbins)
 {
     QpLayout L;
-    size_t q = 0;   // node arrays, laid over the scatter array once the sort is done
+    size_t q = 0;
     auto sub = [&](size_t bytes) {
         const size_t r = q;
         q += (bytes + 15) & ~(size_t)15;
         return r;
     };
-    L.nst = sub(sizeof(uint32_t) * 2 * lcap);
-    L.ncnt = sub(sizeof(uint32_t) * 2 * lcap);
+    const size_t l4 = ((size_t)lcap + 3) & ~(size_t)3;
+    L.nst = sub(sizeof(uint16_t) * 2 * lcap);
+    L.ncnt = sub(sizeof(uint16_t) * 2 * lcap);
     L.ndep = sub(2 * (size_t)lcap);
     L.srank = sub(sizeof(uint16_t) * lcap);
-    L.npos = sub(sizeof(uint16_t) * lcap);
     L.snode = sub(sizeof(uint16_t) * lcap);
-    L.ccnt = sub(sizeof(uint32_t) * 4 * lcap);    // the list keys (u64) before phase 2
-    L.cpos = sub(sizeof(uint16_t) * 4 * lcap + 4);   // the depth-D run starts (u32, lcap + 1) before phase 2
+    // child counts (u16 x 4 per node); before phase 2 the list keys (u32, padded to 4) and the run starts
+    L.ccnt = sub(std::max(sizeof(uint16_t) * 4 * lcap, sizeof(uint32_t) * (2 * l4 + 4)));
     L.vprev = sub(sizeof(uint16_t) * lcap);
     L.vnew = sub(sizeof(uint16_t) * lcap);
     L.skey = sub(sizeof(uint32_t) * (lcap + 4));
     L.scan = sub(sizeof(uint32_t) * (lcap + 1));
     L.scan2 = sub(sizeof(uint32_t) * (lcap + 1));
     L.lkey = L.ccnt;
-    L.zst = L.cpos;
+    L.zst = L.ccnt + sizeof(uint32_t) * l4;
+    L.fdv = q;
+    q += std::max((size_t)ncap + 16, 4 * (size_t)ninv + 16);
     size_t o = 0;
     auto take = [&](size_t bytes) {
         const size_t r = o;
         o += (bytes + 15) & ~(size_t)15;
         return r;
     };
-    L.a = take(q > (size_t)4 * ncap ? q : (size_t)4 * ncap);
-    L.nst += L.a;
-    L.ncnt += L.a;
-    L.ndep += L.a;
-    L.srank += L.a;
-    L.npos += L.a;
-    L.snode += L.a;
-    L.ccnt += L.a;
-    L.cpos += L.a;
-    L.vprev += L.a;
-    L.vnew += L.a;
-    L.skey += L.a;
-    L.scan += L.a;
-    L.scan2 += L.a;
-    L.lkey += L.a;
-    L.zst += L.a;
-    L.b = take((size_t)4 * ncap);
-    L.bins = take(sizeof(uint32_t) * (nbins + 1));
+    L.x = take(std::max(q, sizeof(uint32_t) * (size_t)nbins));
+    L.nst += L.x;
+    L.ncnt += L.x;
+    L.ndep += L.x;
+    L.srank += L.x;
+    L.snode += L.x;
+    L.ccnt += L.x;
+    L.vprev += L.x;
+    L.vnew += L.x;
+    L.skey += L.x;
+    L.scan += L.x;
+    L.scan2 += L.x;
+    L.lkey += L.x;
+    L.zst += L.x;
+    L.fdv += L.x;
+    L.k = take(sizeof(uint32_t) * (size_t)ncap);
     L.cscan = take(sizeof(uint32_t) * cellcap);
     L.cbase = take(sizeof(uint32_t) * cellcap);
     L.wsum = take(sizeof(uint32_t) * 17);
@@ -2102,20 +2139,15 @@ __device__ __forceinline__ uint32_t wave_run_slot(uint32_t* ctr, int key)
     return base + (uint32_t)(lane - head);
 }
 
-// hist[v] += 1 for every active lane: one LDS atomic per distinct value in the wave.  Whole waves.
-__device__ __forceinline__ void wave_hist_add(uint32_t* hist, int v, bool act)
+// wave sum of a u32 (DPP row reductions, then the four rows by readlane; all lanes active)
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 {
-    const int lane = threadIdx.x & 63;
-    bool pending = act;
-    for (;;) {
-        const unsigned long long m = __ballot(pending);
-        if (!m) break;
-        const int first = (int)__builtin_ctzll(m);
-        const int val = __builtin_amdgcn_readlane(v, first);
-        const unsigned long long same = __ballot(pending && v == val);
-        if (lane == first) atomicAdd(&hist[val], (uint32_t)__popcll(same));
-        pending = pending && v != val;
-    }
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true);   // row_half_mirror
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true);   // row_mirror
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
 __device__ __forceinline__ uint32_t compact_even(uint32_t x)   // bits 0, 2, 4, ... -> 0, 1, 2, ...
@@ -2128,13 +2160,16 @@ __device__ __forceinline__ uint32_t compact_even(uint32_t x)   // bits 0, 2, 4, 
     return x;
 }
 
+// minimum waves per SIMD by workgroup size: 1024 threads, two per CU (LDS); 256, three per CU; 64 (one wave,
+// its barriers free), five per CU
+#define ORBX_QP_WPE(NT) ((NT) >= 1024 ? 8 : (NT) >= 512 ? 4 : (NT) >= 256 ? 4 : 2)
 template <int NT, int KPT>
-__global__ __launch_bounds__(NT, ORBX_QT_WPE(NT, KPT, false)) void k_qt_paths(
+__global__ __launch_bounds__(NT, ORBX_QP_WPE(NT)) void k_qt_paths(
     int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
     const int* __restrict__ cell_counts, const uint32_t* __restrict__ cell_addr, const uint32_t* __restrict__ qpt,
-    uint32_t* __restrict__ spill,
-    uint32_t* __restrict__ spill_node, uint32_t* __restrict__ qt_out, int* __restrict__ qt_cnt,
-    int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap, int nbins)
+    uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_node, uint32_t* __restrict__ qt_out,
+    int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap,
+    int ninv, int nbins)
 {
     constexpr int NCAP = NT * KPT;
     constexpr int NW = NT / 64;
@@ -2143,413 +2178,576 @@ __global__ __launch_bounds__(NT, ORBX_QT_WPE(NT, KPT, false)) void k_qt_paths(
     const int l = level0 + blockIdx.x, f = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63;
     const LevelGeom& LG = G->lv[l];
-    if (!LG.qp_ok) {   // level-uniform
-        qt_nodes<NT, KPT, false>(l, f, G, cells, slots, cell_counts, cell_addr, spill, spill_node, nullptr, qt_out,
-                                 qt_cnt, frame_counts, status, lcap, cellcap);
+    if (!LG.qp_ok) {   // level-uniform: the node-list kernel's fallback launch takes it
+        if (tid == 0) qt_cnt[(size_t)f * G->nlevels + l] = -1;
         return;
     }
-    const QpLayout Ly = qp_layout(NCAP, lcap, cellcap, nbins);
-    uint32_t* A = (uint32_t*)(smem + Ly.a);
-    uint32_t* B = (uint32_t*)(smem + Ly.b);
-    uint32_t* bins = (uint32_t*)(smem + Ly.bins);
+    const QpLayout Ly = qp_layout(NCAP, lcap, cellcap, ninv, nbins);
+    uint32_t* K = (uint32_t*)(smem + Ly.k);
+    uint32_t* bins = (uint32_t*)(smem + Ly.x);
     uint32_t* cscan = (uint32_t*)(smem + Ly.cscan);
     uint32_t* cbase = (uint32_t*)(smem + Ly.cbase);
     uint32_t* wsum = (uint32_t*)(smem + Ly.wsum);
     int* sh = (int*)(smem + Ly.sh);
     uint32_t* hist = (uint32_t*)(smem + Ly.hist);
+    uint8_t* fdv = smem + Ly.fdv;
     const int ncl = LG.ncells, cb = LG.cell_begin;
-    const int D = LG.qp_D, RB = LG.qp_rb;
-    const int bshift = 8 + RB + 2 * D - LG.qp_bb;
+    const int D = LG.qp_D, RB = LG.qp_rb, PB = RB + 2 * D;
+    const int bshift = 8 + PB - LG.qp_bb;
     const int NB = 1 << LG.qp_bb;
+#ifdef ORBX_QT_PROF
+    unsigned long long qt_acc[16] = {};
+    long long qt_t = clock64();
+#define QP_STAMP(slot)                                             \
+    do {                                                           \
+        __syncthreads();                                           \
+        const long long t1_ = clock64();                           \
+        qt_acc[slot] += (unsigned long long)(t1_ - qt_t);          \
+        qt_t = t1_;                                                \
+    } while (0)
+#define QP_STAMP1(slot)                                            \
+    do {                                                           \
+        const long long t1_ = clock64();                           \
+        qt_acc[slot] += (unsigned long long)(t1_ - qt_t);          \
+        qt_t = t1_;                                                \
+    } while (0)
+#else
+#define QP_STAMP(slot) ((void)0)
+#define QP_STAMP1(slot) ((void)0)
+#endif
 
-    // ---- 1. candidate counts and slot bases of the level's cells -----------------
+    // ---- 1. candidate counts and run starts of the level's cells; the key tables into LDS ----------
     for (int c = tid; c < ncl; c += NT) {
         cscan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
         cbase[c] = cell_addr[(size_t)f * G->ncells + cb + c];
+    }
+    // xkey[w], ykey[h] staged in K's high half (free until the scatter; the owner map takes the low half)
+    // when they fit: the keys then cost an LDS lookup instead of an L2 round trip behind the candidate loads
+    const bool tab_lds = LG.w + LG.h <= NCAP / 2;   // block-uniform
+    const uint32_t* xk = qpt + LG.qp_xk;
+    const uint32_t* yk = qpt + LG.qp_yk;
+    if (tab_lds) {
+        uint32_t* tk = K + NCAP / 2;
+        for (int i = tid; i < LG.w + LG.h; i += NT) tk[i] = i < LG.w ? xk[i] : yk[i - LG.w];
+        xk = tk;
+        yk = tk + LG.w;
     }
     for (int b = tid; b < NB; b += NT) bins[b] = 0u;
     if (tid < 32) hist[tid] = 0u;
     __syncthreads();
     const int n = (int)block_scan_excl<NT>(cscan, ncl, wsum);
-    if (n > NCAP) {   // block-uniform: more candidates than this workgroup holds
-        qt_nodes<NT, KPT, false>(l, f, G, cells, slots, cell_counts, cell_addr, spill, spill_node, nullptr, qt_out,
-                                 qt_cnt, frame_counts, status, lcap, cellcap);
+    QP_STAMP(0);
+    if (n > NCAP) {   // block-uniform: more candidates than this workgroup holds (the fallback launch)
+        if (tid == 0) qt_cnt[(size_t)f * G->nlevels + l] = -1;
         return;
     }
     uint32_t* out = qt_out + (size_t)f * G->out_per_frame + LG.out_off;
-    int L = 0, cur = 0;
-    bool ok = true;
-    if (n > 0) {   // block-uniform
-        // ---- 2. gather in reference order, keys, bin counts ------------------------------
-        uint16_t* owner = (uint16_t*)B;   // candidate -> cell (the sorted keys take B later)
-        for (int c = tid; c < ncl; c += NT) {
-            const int base = (int)cscan[c], cnt = (c + 1 < ncl ? (int)cscan[c + 1] : n) - base;
-            for (int j = 0; j < cnt; ++j) owner[base + j] = (uint16_t)c;
+    if (n == 0) {   // block-uniform
+        if (tid == 0) qt_cnt[(size_t)f * G->nlevels + l] = 0;
+        return;
+    }
+    // ---- 2. gather in reference order, keys, bin counts --------------------------------------------
+    uint16_t* owner = (uint16_t*)K;   // candidate -> cell (K's low half)
+    for (int c = tid; c < ncl; c += NT) {
+        const int base = (int)cscan[c], cnt = (c + 1 < ncl ? (int)cscan[c + 1] : n) - base;
+        for (int j = 0; j < cnt; ++j) owner[base + j] = (uint16_t)c;
+    }
+    __syncthreads();
+    const uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
+    uint32_t v[KPT];
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) {
+        const int ii = min(tid + r * NT, n - 1);
+        const int c = owner[ii];
+        v[r] = fslots[cbase[c] + (uint32_t)(ii - (int)cscan[c])];
+    }
+    QP_STAMP(1);
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) v[r] = xk[v[r] & 0xFFFu] | yk[(v[r] >> 12) & 0xFFFu] | (v[r] >> 24);
+    uint32_t ps[KPT];   // arrival slot in the bin; after the scan: bin start << 16 | bin size
+    const int wave_i0 = tid - lane;
+    // bin counts: one LDS atomic per run of equal bins in consecutive lanes (run heads), every slot's
+    // atomic issued before any result is used; then each lane's slot = its head's result + its offset
+    auto bin_of = [&](int r) { return tid + r * NT < n ? (int)(v[r] >> bshift) : -1; };
+#pragma unroll
+    for (int r = 0; r < KPT; ++r) {
+        if (wave_i0 + r * NT >= n) break;   // wave-uniform
+        const int bin = bin_of(r);
+        const int prev = __builtin_amdgcn_update_dpp(-2, bin, 0x138, 0xF, 0xF, false);   // wave_shr:1
+        const unsigned long long heads = __ballot(bin != prev);
+        uint32_t base = 0;
+        if (bin >= 0 && bin != prev) {
+            const unsigned long long later = lane == 63 ? 0ull : heads >> (lane + 1);
+            const int len = later ? (int)__builtin_ctzll(later) + 1 : 64 - lane;
+            base = atomicAdd(&bins[bin], (uint32_t)len);
         }
-        __syncthreads();
-        const uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
-        uint32_t v[KPT];
+        ps[r] = base;
+    }
 #pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const int ii = min(tid + r * NT, n - 1);
-            const int c = owner[ii];
-            v[r] = fslots[cbase[c] + (uint32_t)(ii - (int)cscan[c])];
+    for (int r = 0; r < KPT; ++r) {
+        if (wave_i0 + r * NT >= n) break;   // wave-uniform
+        const int bin = bin_of(r);
+        const int prev = __builtin_amdgcn_update_dpp(-2, bin, 0x138, 0xF, 0xF, false);
+        const unsigned long long heads = __ballot(bin != prev);
+        const unsigned long long upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+        const int head = 63 - (int)__builtin_clzll(upto);
+        ps[r] = (uint32_t)__shfl((int)ps[r], head) + (uint32_t)(lane - head);
+    }
+    __syncthreads();
+    QP_STAMP(2);
+    block_scan_excl<NT>(bins, NB, wsum);
+#pragma unroll
+    for (int r = 0; r < KPT; ++r)
+        if (tid + r * NT < n) {
+            const uint32_t bin = v[r] >> bshift;
+            const uint32_t s0 = bins[bin], e0 = (int)bin + 1 < NB ? bins[bin + 1] : (uint32_t)n;
+            K[s0 + ps[r]] = v[r];
+            ps[r] = (s0 << 16) | (e0 - s0);
         }
-        const uint32_t* xk = qpt + LG.qp_xk;
-        const uint32_t* yk = qpt + LG.qp_yk;
+    __syncthreads();
+    QP_STAMP(3);
+    // ---- 3. each key's rank inside its bin (the run it was scattered into); the keys then move to their
+    // sorted places in K (a barrier between: every rank reads the bin as scattered) --------------------
+    // (bins are small: a lone key needs no reads; the others read their run four keys at a time)
 #pragma unroll
-        for (int r = 0; r < KPT; ++r) v[r] = xk[v[r] & 0xFFFu] | yk[(v[r] >> 12) & 0xFFFu] | (v[r] >> 24);
-        uint32_t bs[KPT];
-        const int wave_i0 = tid - lane;
+    for (int r = 0; r < KPT; ++r) {
+        if (tid + r * NT < n) {
+            const uint32_t key = v[r];
+            const int s0 = (int)(ps[r] >> 16), cnt = (int)(ps[r] & 0xFFFFu);
+            int rk = 0;
+            for (int q0 = 0; q0 < cnt; q0 += 4) {
+                uint32_t u[4];
 #pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            if (wave_i0 + r * NT >= n) break;   // wave-uniform
-            const int bin = tid + r * NT < n ? (int)(v[r] >> bshift) : -1;
-            bs[r] = ((uint32_t)bin << 16) | wave_run_slot(bins, bin);
-        }
-        __syncthreads();
-        block_scan_excl<NT>(bins, NB, wsum);
-        if (tid == 0) bins[NB] = (uint32_t)n;
+                for (int k = 0; k < 4; ++k) u[k] = K[s0 + min(q0 + k, cnt - 1)];
 #pragma unroll
-        for (int r = 0; r < KPT; ++r)
-            if (tid + r * NT < n) A[bins[bs[r] >> 16] + (bs[r] & 0xFFFFu)] = v[r];
-        __syncthreads();
-        // ---- 3. rank inside the bin -> B sorted -------------------------------------------
-#pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const int p = tid + r * NT;
-            if (p < n) {
-                const uint32_t key = A[p];
-                const uint32_t b = key >> bshift;
-                const int s0 = (int)bins[b], s1 = (int)bins[b + 1];
-                int rk = 0;
-                for (int q = s0; q < s1; ++q) rk += A[q] < key;
-                B[s0 + rk] = key;
+                for (int k = 0; k < 4; ++k) rk += (q0 + k < cnt) & (u[k] < key);
             }
+            ps[r] = (uint32_t)(s0 + rk);
         }
-        __syncthreads();
-        // ---- 4. phase 1 by the fd histograms ---------------------------------------------
-        auto fd = [&](int i) -> int {
-            if (i <= 0 || i >= n) return 0;
-            const uint32_t t = (B[i - 1] ^ B[i]) >> 8;
-            const int hb = 31 - (int)__builtin_clz(t);
-            return hb >= 2 * D ? 0 : D - (hb >> 1);
-        };
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < KPT; ++r)
+        if (tid + r * NT < n) K[ps[r]] = v[r];
+    __syncthreads();
+    QP_STAMP(4);
+    // ---- 4. phase 1 (:710-803) from the fd histograms ----------------------------------------------
+    // fd(i): the first depth at which sorted keys i - 1 and i lie in different cells (0: another root)
+    auto fd = [&](int i) -> int {
+        if (i <= 0 || i >= n) return 0;
+        const uint32_t t = (K[i - 1] ^ K[i]) >> 8;
+        const int hb = 31 - (int)__builtin_clz(t);
+        return hb >= 2 * D ? 0 : D - (hb >> 1);
+    };
+    {
+        // per-thread byte histograms of fd(i) (L) and max(fd(i), fd(i + 1)) (M), values <= 15, then
+        // widened to 16-bit pairs and summed over the wave
+        unsigned long long hl0 = 0, hl1 = 0, hm0 = 0, hm1 = 0;
 #pragma unroll
         for (int r = 0; r < KPT; ++r) {
-            if (wave_i0 + r * NT >= n) break;   // wave-uniform
             const int i = tid + r * NT;
-            const bool act = i < n;
-            const int a = act ? fd(i) : 0, a1 = act ? fd(i + 1) : 0;
-            wave_hist_add(hist, a, act);
-            wave_hist_add(hist, 16 + (a > a1 ? a : a1), act);
-        }
-        __syncthreads();
-        const int N = LG.nfeat;
-        int Dp = D, ph2 = 0;
-        {
-            int cumL = (int)hist[0], cumM = (int)hist[16];
-            for (int d = 1; d <= D + 1; ++d) {   // :710-803 (round 1 always runs)
-                const int Ld = cumL + (d <= D ? (int)hist[d] : 0), Md = cumM + (d <= D ? (int)hist[16 + d] : 0);
-                if (Ld >= N || Ld == cumL) {
-                    Dp = d;
-                    break;
-                }
-                if (Ld + 3 * (Ld - Md) > N) {
-                    Dp = d;
-                    ph2 = 1;
-                    break;
-                }
-                cumL = Ld;
-                cumM = Md;
+            if (i < n) {
+                const int a = fd(i), a1 = fd(i + 1), m = a > a1 ? a : a1;
+                fdv[i] = (uint8_t)a;
+                const unsigned long long ba = 1ull << (8 * (a & 7)), bm = 1ull << (8 * (m & 7));
+                if (a < 8) hl0 += ba; else hl1 += ba;
+                if (m < 8) hm0 += bm; else hm1 += bm;
             }
-            Dp = Dp < D ? Dp : D;   // past D every run is one keypoint: nothing changes
         }
-        // ---- 5. the depth-Dp runs (the nodes) in key order ---------------------------------
-        uint32_t* zst = (uint32_t*)(smem + Ly.zst);
-        unsigned long long* lkey = (unsigned long long*)(smem + Ly.lkey);
-        {
-            const int per = (n + NT - 1) / NT;
-            const int b0 = tid * per, e0 = min(n, b0 + per);
-            uint32_t local = 0;
-            for (int i = b0; i < e0; ++i) local += fd(i) <= Dp ? 1u : 0u;
-            const uint32_t inc = wave_incl_scan(local);
-            if (lane == 63) wsum[tid >> 6] = inc;
-            __syncthreads();
-            uint32_t run = inc - local, total = 0;
+        if (tid == 0) fdv[n] = 0;
+        const unsigned long long hh[4] = {hl0, hl1, hm0, hm1};
+        uint32_t tot[16];
 #pragma unroll
-            for (int w = 0; w < NW; ++w) {
-                const uint32_t t = wsum[w];
-                run += w < (tid >> 6) ? t : 0u;
-                total += t;
-            }
-            for (int i = b0; i < e0; ++i)
-                if (fd(i) <= Dp) zst[run++] = (uint32_t)i;
-            L = (int)total;
-            if (tid == 0) zst[L] = (uint32_t)n;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t lo = (uint32_t)hh[k], hi = (uint32_t)(hh[k] >> 32);
+            tot[4 * k + 0] = wave_sum_u32(lo & 0x00FF00FFu);          // values 0, 2 (+8k/2 ...)
+            tot[4 * k + 1] = wave_sum_u32((lo >> 8) & 0x00FF00FFu);   // values 1, 3
+            tot[4 * k + 2] = wave_sum_u32(hi & 0x00FF00FFu);          // values 4, 6
+            tot[4 * k + 3] = wave_sum_u32((hi >> 8) & 0x00FF00FFu);   // values 5, 7
         }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int h0 = (k >> 1) * 16 + (k & 1) * 8;   // L: 0..15, M: 16..31
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int v0 = (e >> 1) * 4 + (e & 1);   // value of the low 16 bits
+                    const uint32_t t = tot[4 * k + e];
+                    if (t & 0xFFFFu) atomicAdd(&hist[h0 + v0], t & 0xFFFFu);
+                    if (t >> 16) atomicAdd(&hist[h0 + v0 + 2], t >> 16);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    QP_STAMP(5);
+    const int N = LG.nfeat;
+    int Dp = D, ph2 = 0;
+    {
+        int cumL = (int)hist[0], cumM = (int)hist[16];
+        for (int d = 1; d <= D + 1; ++d) {   // round 1 always runs
+            const int Ld = cumL + (d <= D ? (int)hist[d] : 0), Md = cumM + (d <= D ? (int)hist[16 + d] : 0);
+            if (Ld >= N || Ld == cumL) {
+                Dp = d;
+                break;
+            }
+            if (Ld + 3 * (Ld - Md) > N) {
+                Dp = d;
+                ph2 = 1;
+                break;
+            }
+            cumL = Ld;
+            cumM = Md;
+        }
+        Dp = Dp < D ? Dp : D;   // past D every run is one keypoint: nothing changes
+    }
+    // ---- 5. the depth-Dp runs (the nodes) in key order ---------------------------------------------
+    uint32_t* zst = (uint32_t*)(smem + Ly.zst);
+    uint32_t* lkey = (uint32_t*)(smem + Ly.lkey);
+    int L = 0;
+    {
+        // thread t's positions [t * KPT, t * KPT + KPT) (n <= NT * KPT): whole dwords of fd bytes when KPT is a
+        // multiple of 4, bytes otherwise
+        constexpr int KW = (KPT + 3) / 4;
+        const int b0 = tid * KPT;
+        uint32_t fw[KW];
+        uint32_t local = 0;
+#pragma unroll
+        for (int w = 0; w < KW; ++w) {
+            if constexpr (KPT % 4 == 0) {
+                fw[w] = b0 + 4 * w < n ? ((const uint32_t*)fdv)[tid * (KPT / 4) + w] : 0xFFFFFFFFu;
+            } else {
+                fw[w] = 0xFFFFFFFFu;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * w + k < KPT && b0 + 4 * w + k < n)
+                        fw[w] = (fw[w] & ~(0xFFu << (8 * k))) | ((uint32_t)fdv[b0 + 4 * w + k] << (8 * k));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                local += (4 * w + k < KPT) & (b0 + 4 * w + k < n) & ((int)((fw[w] >> (8 * k)) & 0xFFu) <= Dp);
+        }
+        const uint32_t inc = wave_incl_scan(local);
+        if (lane == 63) wsum[tid >> 6] = inc;
         __syncthreads();
-        // list keys: group Dp - b (b = the round that created the node), then the first b digits with
-        // reverse(B_b)'s directions (digit j ascending iff b - j is odd, the root like digit 1)
-        for (int id = tid; id < L; id += NT) {
+        uint32_t run = inc - local, total = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t t = wsum[w];
+            run += w < (tid >> 6) ? t : 0u;
+            total += t;
+        }
+#pragma unroll
+        for (int w = 0; w < KW; ++w)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((4 * w + k < KPT) & (b0 + 4 * w + k < n) & ((int)((fw[w] >> (8 * k)) & 0xFFu) <= Dp))
+                    zst[run++] = (uint32_t)(b0 + 4 * w + k);
+        L = (int)total;
+        if (tid == 0) zst[L] = (uint32_t)n;
+    }
+    __syncthreads();
+    QP_STAMP(6);
+    // list keys: group Dp - b (b = the round that created the node) above the first b digits with
+    // reverse(B_b)'s directions (digit j ascending iff b - j is odd, the root like digit 1), left-aligned
+    const int L4 = (L + 3) & ~3;
+    for (int id = tid; id < L4; id += NT) {
+        uint32_t key = 0xFFFFFFFFu;   // padding: above every key
+        if (id < L) {
             const int s = (int)zst[id], c = (int)zst[id + 1] - s;
             int b = Dp;
             if (c == 1) {
-                const int f0 = fd(s), f1 = fd(s + 1);
+                const int f0 = fdv[s], f1 = fdv[s + 1];
                 b = f0 > f1 ? f0 : f1;
             }
-            const uint32_t path = B[s] >> 8;
+            const uint32_t path = K[s] >> 8;
             uint32_t root = path >> (2 * D);
             uint32_t pd = (path & ((1u << (2 * D)) - 1u)) >> (2 * (D - b));
             if (b & 1) root ^= (1u << RB) - 1u;
             pd ^= 0x33333333u & ((1u << (2 * b)) - 1u);
-            const uint32_t tk = ((root << (2 * b)) | pd) << (2 * (D - b));
-            lkey[id] = ((unsigned long long)(Dp - b) << 32) | tk;
+            key = ((uint32_t)(Dp - b) << PB) | (((root << (2 * b)) | pd) << (2 * (D - b)));
         }
-        __syncthreads();
-        uint32_t* nst0 = (uint32_t*)(smem + Ly.nst);
-        uint32_t* ncnt0 = (uint32_t*)(smem + Ly.ncnt);
-        uint8_t* ndep0 = smem + Ly.ndep;
-        uint32_t* scan = (uint32_t*)(smem + Ly.scan);
-        {
-            const int L2 = (L + 1) >> 1;
-            const ulonglong2* k2 = (const ulonglong2*)lkey;
-            for (int id = tid; id < L; id += NT) {
-                const unsigned long long key = lkey[id];
-                int pos = 0;
-                for (int j = 0; j < L2; ++j) {
-                    const ulonglong2 u = k2[j];
-                    pos += (int)(u.x < key) + (int)(2 * j + 1 < L && u.y < key);
-                }
-                const int s = (int)zst[id], c = (int)zst[id + 1] - s;
-                nst0[pos] = (uint32_t)s;
-                ncnt0[pos] = (uint32_t)c;
-                ndep0[pos] = (uint8_t)Dp;
-                scan[pos] = (key >> 32) == 0 && c > 1 ? 1u : 0u;   // phase 2's first vPrev (group 0, expandable)
+        lkey[id] = key;
+    }
+    __syncthreads();
+    uint16_t* nst0 = (uint16_t*)(smem + Ly.nst);
+    uint16_t* ncnt0 = (uint16_t*)(smem + Ly.ncnt);
+    uint8_t* ndep0 = smem + Ly.ndep;
+    uint32_t* scan = (uint32_t*)(smem + Ly.scan);
+    {
+        const uint4* k4 = (const uint4*)lkey;
+        for (int id = tid; id < L; id += NT) {
+            const uint32_t key = lkey[id];
+            int pos = 0;
+            for (int j = 0; j < L4 / 4; ++j) {
+                const uint4 u = k4[j];
+                pos += (int)(u.x < key) + (int)(u.y < key) + (int)(u.z < key) + (int)(u.w < key);
             }
+            const int s = (int)zst[id], c = (int)zst[id + 1] - s;
+            nst0[pos] = (uint16_t)s;
+            ncnt0[pos] = (uint16_t)c;
+            ndep0[pos] = (uint8_t)Dp;
+            scan[pos] = (key >> PB) == 0 && c > 1 ? 1u : 0u;   // phase 2's first vPrev (group 0, expandable)
         }
-        __syncthreads();
-        // ---- 6. phase 2 on nodes (:805-874) ---------------------------------------------------
-        if (ph2) {   // block-uniform
-            uint16_t* vprev = (uint16_t*)(smem + Ly.vprev);
-            uint16_t* vnew = (uint16_t*)(smem + Ly.vnew);
-            uint16_t* srank = (uint16_t*)(smem + Ly.srank);
-            uint16_t* npos = (uint16_t*)(smem + Ly.npos);
-            uint16_t* snode = (uint16_t*)(smem + Ly.snode);
-            uint32_t* ccnt = (uint32_t*)(smem + Ly.ccnt);
-            uint16_t* cpos = (uint16_t*)(smem + Ly.cpos);
-            uint32_t* skey = (uint32_t*)(smem + Ly.skey);
-            uint32_t* scan2 = (uint32_t*)(smem + Ly.scan2);
-            // vPrev in creation order = group 0's expandable nodes in descending list position
-            const uint32_t m0 = block_scan_fn<NT>(scan2, L, wsum, [&](int p) { return scan[p]; });
-            for (int p = tid; p < L; p += NT)
-                if (scan[p]) vprev[m0 - 1 - scan2[p]] = (uint16_t)p;
-            if (tid == 0) {
-                sh[SH_L] = L;
-                sh[SH_M] = (int)m0;
-                sh[SH_DONE] = 0;
-                sh[SH_ERR] = 0;
-            }
-            while (true) {
-                __syncthreads();
-                if (sh[SH_DONE]) break;
-                const int Lc = sh[SH_L];
-                const int m = sh[SH_M];
-                uint32_t* stc = (uint32_t*)(smem + Ly.nst) + (size_t)cur * lcap;
-                uint32_t* stn = (uint32_t*)(smem + Ly.nst) + (size_t)(cur ^ 1) * lcap;
-                uint32_t* cntc = (uint32_t*)(smem + Ly.ncnt) + (size_t)cur * lcap;
-                uint32_t* cntn = (uint32_t*)(smem + Ly.ncnt) + (size_t)(cur ^ 1) * lcap;
-                uint8_t* dpc = smem + Ly.ndep + (size_t)cur * lcap;
-                uint8_t* dpn = smem + Ly.ndep + (size_t)(cur ^ 1) * lcap;
-                const uint16_t* vin = cur ? vnew : vprev;
-                uint16_t* vout = cur ? vprev : vnew;
-                // A: vPrev ranked by (size, creation) descending (unique keys: one barrier); the ranking
-                // thread also finds the candidate's four child runs (digit dp + 1 inside its key range)
-                const int m4 = (m + 3) >> 2;
-                for (int k = tid; k < 4 * m4; k += NT) skey[k] = k < m ? (cntc[vin[k]] << 16) | (uint32_t)k : 0u;
-                for (int p = tid; p < Lc; p += NT) srank[p] = kNone;
-                if (tid == 0) sh[SH_KK] = m;
-                __syncthreads();
-                {
-                    const uint4* k4 = (const uint4*)skey;
-                    for (int k = tid; k < m; k += NT) {
-                        const uint32_t key = skey[k];
-                        int j = 0;
-                        for (int i4 = 0; i4 < m4; ++i4) {
-                            const uint4 u = k4[i4];
-                            j += (int)(u.x > key) + (int)(u.y > key) + (int)(u.z > key) + (int)(u.w > key);
+    }
+    __syncthreads();
+    // the inverse tables (path digits -> cell column << 12 | x, cell row << 12 | y) into LDS over the fd
+    // bytes by LDS-DMA (global_load_lds_dword: lane i of a wave instruction lands at dst + 4 i), so they
+    // arrive under phase 2; retain waits for them
+    const int nxi = LG.nIni << D, nyi = 1 << D;
+    uint32_t* inv = (uint32_t*)fdv;
+    for (int b = (tid >> 6) * 64; b < nxi + nyi; b += NT) {   // wave-uniform
+        const int i = b + lane;
+        if (i < nxi + nyi) {
+            const uint32_t* src = qpt + (i < nxi ? LG.qp_xi + i : LG.qp_yi + (i - nxi));
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(inv + b), 4, 0, 0);
+        }
+    }
+    QP_STAMP(7);
+    // ---- 6. phase 2 on nodes (:805-874) -------------------------------------------------------------
+    // (Measured and not kept: the whole phase by one wave with wave-level ordering instead of block
+    // barriers: level 0 75 against 63 us, the ranking of ~200 candidates serialised on 64 lanes.)
+    int cur = 0;
+    bool ok = true;
+    if (ph2) {   // block-uniform
+        uint16_t* vprev = (uint16_t*)(smem + Ly.vprev);
+        uint16_t* vnew = (uint16_t*)(smem + Ly.vnew);
+        uint16_t* srank = (uint16_t*)(smem + Ly.srank);
+        uint16_t* snode = (uint16_t*)(smem + Ly.snode);
+        uint16_t* ccnt = (uint16_t*)(smem + Ly.ccnt);
+        uint32_t* skey = (uint32_t*)(smem + Ly.skey);
+        uint32_t* scan2 = (uint32_t*)(smem + Ly.scan2);
+        // vPrev in creation order = group 0's expandable nodes in descending list position
+        const uint32_t m0 = block_scan_fn<NT>(scan2, L, wsum, [&](int p) { return scan[p]; });
+        for (int p = tid; p < L; p += NT)
+            if (scan[p]) vprev[m0 - 1 - scan2[p]] = (uint16_t)p;
+        if (tid == 0) {
+            sh[SH_L] = L;
+            sh[SH_M] = (int)m0;
+            sh[SH_DONE] = 0;
+            sh[SH_ERR] = 0;
+        }
+        QP_STAMP(15);
+        while (true) {
+            __syncthreads();
+            if (sh[SH_DONE]) break;
+            const int Lc = sh[SH_L];
+            const int m = sh[SH_M];
+            uint16_t* stc = (uint16_t*)(smem + Ly.nst) + (size_t)cur * lcap;
+            uint16_t* stn = (uint16_t*)(smem + Ly.nst) + (size_t)(cur ^ 1) * lcap;
+            uint16_t* cntc = (uint16_t*)(smem + Ly.ncnt) + (size_t)cur * lcap;
+            uint16_t* cntn = (uint16_t*)(smem + Ly.ncnt) + (size_t)(cur ^ 1) * lcap;
+            uint8_t* dpc = smem + Ly.ndep + (size_t)cur * lcap;
+            uint8_t* dpn = smem + Ly.ndep + (size_t)(cur ^ 1) * lcap;
+            const uint16_t* vin = cur ? vnew : vprev;
+            uint16_t* vout = cur ? vprev : vnew;
+            // A: vPrev ranked by (size, creation) descending (unique keys: one barrier); the ranking thread
+            // also finds the candidate's four child runs (digit dp + 1 inside its key range)
+            const int m4 = (m + 3) >> 2;
+            for (int k = tid; k < 4 * m4; k += NT) skey[k] = k < m ? ((uint32_t)cntc[vin[k]] << 16) | (uint32_t)k : 0u;
+            for (int p = tid; p < Lc; p += NT) srank[p] = kNone;
+            if (tid == 0) sh[SH_KK] = m;
+            __syncthreads();
+            {
+                const uint4* k4 = (const uint4*)skey;
+                for (int k = tid; k < m; k += NT) {
+                    const uint32_t key = skey[k];
+                    int j = 0;
+                    for (int i4 = 0; i4 < m4; ++i4) {
+                        const uint4 u = k4[i4];
+                        j += (int)(u.x > key) + (int)(u.y > key) + (int)(u.z > key) + (int)(u.w > key);
+                    }
+                    const int p = vin[k];
+                    srank[p] = (uint16_t)j;
+                    snode[j] = (uint16_t)p;
+                    const int s0 = (int)stc[p], c = (int)cntc[p];
+                    const int sd = 8 + 2 * (D - (dpc[p] + 1));   // the child digit's bit position
+                    int lo = s0;
+                    for (int q = 0; q < 3; ++q) {   // first key with digit > q
+                        int a = lo, e = s0 + c;
+                        while (a < e) {
+                            const int mid = (a + e) >> 1;
+                            if ((int)((K[mid] >> sd) & 3u) <= q) a = mid + 1; else e = mid;
                         }
-                        const int p = vin[k];
-                        srank[p] = (uint16_t)j;
-                        snode[j] = (uint16_t)p;
-                        const int s = (int)stc[p], c = (int)cntc[p];
-                        const int sd = 8 + 2 * (D - (dpc[p] + 1));   // the child digit's bit position
-                        int lo = s;
-                        for (int q = 0; q < 3; ++q) {   // first key with digit > q
-                            int a = lo, e = s + c;
-                            while (a < e) {
-                                const int mid = (a + e) >> 1;
-                                if ((int)((B[mid] >> sd) & 3u) <= q) a = mid + 1; else e = mid;
-                            }
-                            ccnt[4 * p + q] = (uint32_t)(a - lo);
-                            lo = a;
-                        }
-                        ccnt[4 * p + 3] = (uint32_t)(s + c - lo);
+                        ccnt[4 * p + q] = (uint16_t)(a - lo);
+                        lo = a;
                     }
+                    ccnt[4 * p + 3] = (uint16_t)(s0 + c - lo);
                 }
-                __syncthreads();
-                // C: children (low half) and expandable children (high half) per split rank
-                const int S = m;
-                auto kids = [&](int s) -> uint32_t {
-                    const int p = snode[s];
-                    uint32_t v2 = 0;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t c = ccnt[4 * p + q];
-                        v2 += (c > 0 ? 1u : 0u) + (c > 1 ? 0x10000u : 0u);
-                    }
-                    return v2;
-                };
-                const uint32_t T = block_scan_fn<NT>(scan, S, wsum, kids);
-                // how many candidates are split: the size after splitting j grows with j (a split node
-                // leaves >= 1 child), so the one j that crosses N writes (:843-845)
-                for (int j = tid; j < S; j += NT) {
-                    const int cs = (int)(kids(j) & 0xFFFFu), sj = (int)(scan[j] & 0xFFFFu);
-                    if (Lc + sj + cs - (j + 1) >= N && Lc + sj - j < N) sh[SH_KK] = j + 1;
-                }
-                __syncthreads();
-                const int kk = sh[SH_KK];
-                const uint32_t pre = kk < S ? scan[kk] : T;
-                block_scan_fn<NT>(scan2, Lc, wsum, [&](int p) {
-                    return (srank[p] != kNone && (int)srank[p] < kk) ? 1u : 0u;
-                });
-                const int Ctot = (int)(pre & 0xFFFFu), nexp = (int)(pre >> 16);
-                const int newL = Ctot + (Lc - kk);
-                if (newL > lcap) {
-                    if (tid == 0) {
-                        sh[SH_ERR] |= kStatusListOverflow;
-                        sh[SH_DONE] = 1;
-                    }
-                    continue;
-                }
-                // D: the new list: children of split rank s at Ctot - prefix(s) - children(s) (later splits
-                // in front, n4..n1), the rest after them in order; expandable children in creation order
-                for (int s = tid; s < kk; s += NT) {
-                    const int p = snode[s];
-                    const uint32_t ps = scan[s];
-                    uint32_t c4[4];
-                    int cs = 0;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        c4[q] = ccnt[4 * p + q];
-                        cs += c4[q] > 0;
-                    }
-                    const int pos0 = Ctot - (int)(ps & 0xFFFFu) - cs;
-                    int e = (int)(ps >> 16);
-                    int np = pos0 + cs;   // n1 lands last (it was pushed first)
-                    uint32_t st = stc[p];
-                    const uint8_t dch = (uint8_t)(dpc[p] + 1);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t c = c4[q];
-                        if (c == 0) continue;
-                        --np;
-                        stn[np] = st;
-                        cntn[np] = c;
-                        dpn[np] = dch;
-                        st += c;
-                        if (c > 1) vout[e++] = (uint16_t)np;   // creation order: split rank, then n1..n4
-                    }
-                }
-                for (int p = tid; p < Lc; p += NT) {
-                    const bool split = srank[p] != kNone && (int)srank[p] < kk;
-                    if (!split) {
-                        const int np = Ctot + p - (int)scan2[p];
-                        stn[np] = stc[p];
-                        cntn[np] = cntc[p];
-                        dpn[np] = dpc[p];
-                    }
-                }
-                if (tid == 0) {
-                    sh[SH_L] = newL;
-                    if (newL >= N || newL == Lc) sh[SH_DONE] = 1;
-                    sh[SH_M] = nexp;
-                }
-                __syncthreads();
-                cur ^= 1;
-                (void)npos;
-                (void)cpos;
             }
             __syncthreads();
-            L = sh[SH_L];
-            ok = sh[SH_ERR] == 0;
-        }
-        // ---- 7. retain the best keypoint per node (:882-906) ------------------------------------
-        const uint32_t* stf = (uint32_t*)(smem + Ly.nst) + (size_t)cur * lcap;
-        const uint32_t* cntf = (uint32_t*)(smem + Ly.ncnt) + (size_t)cur * lcap;
-        const int outn = ok ? (L < LG.cap ? L : LG.cap) : 0;
-        const uint32_t* xinv = qpt + LG.qp_xi;
-        const uint32_t* yinv = qpt + LG.qp_yi;
-        const uint32_t dmask = (1u << (2 * D)) - 1u;
-        for (int p = tid; p < outn; p += NT) {
-            const int s = (int)stf[p], c = (int)cntf[p];
-            uint32_t ms = 0;
-            for (int j = s; j < s + c; ++j) ms = max(ms, B[j] & 0xFFu);
-            unsigned long long bo = ~0ull;
-            uint32_t bx = 0, by = 0;
-            for (int j = s; j < s + c; ++j) {
-                const uint32_t k = B[j];
-                if ((k & 0xFFu) != ms) continue;
-                const uint32_t path = k >> 8, dg = path & dmask;
-                const uint32_t x = xinv[((path >> (2 * D)) << D) | compact_even(dg)];
-                const uint32_t y = yinv[compact_even(dg >> 1)];
-                // reference order: cell row, cell column (src/ORBextractor.cc:952-1000), then cv::FAST's
-                // row-major order inside the cell
-                const unsigned long long o = ((unsigned long long)((y - 3) / (uint32_t)LG.qp_hc) << 40) |
-                                             ((unsigned long long)((x - 3) / (uint32_t)LG.qp_wc) << 24) |
-                                             ((unsigned long long)y << 12) | x;
-                if (o < bo) {
-                    bo = o;
-                    bx = x;
-                    by = y;
+            QP_STAMP(12);
+            // C: children (low half) and expandable children (high half) per split rank
+            const int S = m;
+            auto kids = [&](int sr) -> uint32_t {
+                const int p = snode[sr];
+                uint32_t v2 = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t c = ccnt[4 * p + q];
+                    v2 += (c > 0 ? 1u : 0u) + (c > 1 ? 0x10000u : 0u);
+                }
+                return v2;
+            };
+            const uint32_t T = block_scan_fn<NT>(scan, S, wsum, kids);
+            // how many candidates are split: the size after splitting j grows with j (a split node leaves
+            // >= 1 child), so the one j that crosses N writes (:843-845)
+            for (int j = tid; j < S; j += NT) {
+                const int cs = (int)(kids(j) & 0xFFFFu), sj = (int)(scan[j] & 0xFFFFu);
+                if (Lc + sj + cs - (j + 1) >= N && Lc + sj - j < N) sh[SH_KK] = j + 1;
+            }
+            __syncthreads();
+            const int kk = sh[SH_KK];
+            const uint32_t pre = kk < S ? scan[kk] : T;
+            block_scan_fn<NT>(scan2, Lc, wsum, [&](int p) {
+                return (srank[p] != kNone && (int)srank[p] < kk) ? 1u : 0u;
+            });
+            const int Ctot = (int)(pre & 0xFFFFu), nexp = (int)(pre >> 16);
+            const int newL = Ctot + (Lc - kk);
+            QP_STAMP(13);
+            if (newL > lcap) {
+                if (tid == 0) {
+                    sh[SH_ERR] |= kStatusListOverflow;
+                    sh[SH_DONE] = 1;
+                }
+                continue;
+            }
+            // D: the new list: children of split rank s at Ctot - prefix(s) - children(s) (later splits in
+            // front, n4..n1), the rest after them in order; expandable children in creation order
+            for (int sr = tid; sr < kk; sr += NT) {
+                const int p = snode[sr];
+                const uint32_t pss = scan[sr];
+                uint32_t c4[4];
+                int cs = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    c4[q] = ccnt[4 * p + q];
+                    cs += c4[q] > 0;
+                }
+                const int pos0 = Ctot - (int)(pss & 0xFFFFu) - cs;
+                int e = (int)(pss >> 16);
+                int np = pos0 + cs;   // n1 lands last (it was pushed first)
+                uint32_t st = stc[p];
+                const uint8_t dch = (uint8_t)(dpc[p] + 1);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t c = c4[q];
+                    if (c == 0) continue;
+                    --np;
+                    stn[np] = (uint16_t)st;
+                    cntn[np] = (uint16_t)c;
+                    dpn[np] = dch;
+                    st += c;
+                    if (c > 1) vout[e++] = (uint16_t)np;   // creation order: split rank, then n1..n4
                 }
             }
-            out[p] = pack_kp(bx + kMinBorder, by + kMinBorder, ms);
+            for (int p = tid; p < Lc; p += NT) {
+                const bool split = srank[p] != kNone && (int)srank[p] < kk;
+                if (!split) {
+                    const int np = Ctot + p - (int)scan2[p];
+                    stn[np] = stc[p];
+                    cntn[np] = cntc[p];
+                    dpn[np] = dpc[p];
+                }
+            }
+            if (tid == 0) {
+                sh[SH_L] = newL;
+                if (newL >= N || newL == Lc) sh[SH_DONE] = 1;
+                sh[SH_M] = nexp;
+            }
+            __syncthreads();
+            QP_STAMP(14);
+            cur ^= 1;
+#ifdef ORBX_QT_PROF
+            qt_acc[10] += 1;
+#endif
         }
-        if (!ok) L = 0;
-        if (tid == 0) {
-            const int on = outn;
-            qt_cnt[(size_t)f * G->nlevels + l] = on;
-            atomicAdd(&frame_counts[f], on);
-            int err = ok ? 0 : kStatusListOverflow;
-            if (ok && L > LG.cap) err |= kStatusOutOverflow;
-            if (err) atomicOr(status, err);
-        }
-        return;
+        __syncthreads();
+        L = sh[SH_L];
+        ok = sh[SH_ERR] == 0;
     }
-    if (tid == 0) qt_cnt[(size_t)f * G->nlevels + l] = 0;
+    QP_STAMP(9);
+    // ---- 7. retain the best keypoint per node (:882-906) ----------------------------------------------
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the inverse tables' DMA
+    __syncthreads();
+    const uint16_t* stf = (const uint16_t*)(smem + Ly.nst) + (size_t)cur * lcap;
+    const uint16_t* cntf = (const uint16_t*)(smem + Ly.ncnt) + (size_t)cur * lcap;
+    const int outn = ok ? (L < LG.cap ? L : LG.cap) : 0;
+    const uint32_t dmask = (1u << (2 * D)) - 1u;
+    for (int p = tid; p < outn; p += NT) {
+        const int s = (int)stf[p], c = (int)cntf[p];
+        uint32_t ms = 0;
+#pragma unroll 8
+        for (int j = 0; j < c; ++j) ms = max(ms, K[s + j] & 0xFFu);
+        // among the keys at the highest score, the first in reference order: cell row, cell column
+        // (src/ORBextractor.cc:952-1000), then cv::FAST's row-major order inside the cell
+        unsigned long long bo = ~0ull;
+        for (int j0 = 0; j0 < c; j0 += 8) {   // eight loads in flight, then the (rare) ties decoded
+            uint32_t kk[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) kk[k] = K[s + min(j0 + k, c - 1)];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (j0 + k >= c || (kk[k] & 0xFFu) != ms) continue;
+                const uint32_t path = kk[k] >> 8, dg = path & dmask;
+                const uint32_t xv = inv[((path >> (2 * D)) << D) | compact_even(dg)];
+                const uint32_t yv = inv[nxi + compact_even(dg >> 1)];
+                const unsigned long long o = ((unsigned long long)(yv >> 12) << 40) |
+                                             ((unsigned long long)(xv >> 12) << 24) |
+                                             ((unsigned long long)(yv & 0xFFFu) << 12) | (xv & 0xFFFu);
+                bo = o < bo ? o : bo;
+            }
+        }
+        out[p] = pack_kp((uint32_t)(bo & 0xFFFu) + kMinBorder, (uint32_t)((bo >> 12) & 0xFFFu) + kMinBorder, ms);
+    }
+    QP_STAMP(11);
+    if (tid == 0) {
+#ifdef ORBX_QT_PROF
+        qt_acc[8] = 1;
+        for (int q = 0; q < 16; ++q) atomicAdd(&g_qt_prof[l][q], qt_acc[q]);
+#endif
+        qt_cnt[(size_t)f * G->nlevels + l] = outn;
+        atomicAdd(&frame_counts[f], outn);
+        int err = ok ? 0 : kStatusListOverflow;
+        if (ok && L > LG.cap) err |= kStatusOutOverflow;
+        if (err) atomicOr(status, err);
+    }
+#undef QP_STAMP
+#undef QP_STAMP1
 }
 
 template <int NT, int KPT, bool kG>
-static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
-                      hipStream_t s)
+static void qt_launch_nodes(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
+                            hipStream_t s, int only_flagged)
 {
-    size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap, 2, qt_kpn(NT, KPT, 0)).total;
-    if constexpr (!kG) {
-        if (q.nbins > 0 && !getenv("ORBX_QT_NODES")) {   // the path-code kernel (its fallback body needs smem too)
-            smem = std::max(smem, qp_layout(NT * KPT, q.lcap, q.cellcap, q.nbins).total);
-            hipFuncSetAttribute((const void*)k_qt_paths<NT, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)smem);
-            hipLaunchKernelGGL((k_qt_paths<NT, KPT>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
-                               b.slots, b.cell_counts, b.cell_addr, b.qpt, b.spill, b.spill_node, b.qt_out,
-                               b.qt_cnt, frame_counts, b.status, q.lcap, q.cellcap, q.nbins);
-            return;
-        }
-    }
+    const size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap, 2, qt_kpn(NT, KPT, 0)).total;
     hipFuncSetAttribute((const void*)k_quadtree<NT, KPT, kG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_quadtree<NT, KPT, kG>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
                        b.slots, b.cell_counts, b.cell_addr, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt,
-                       frame_counts, b.status, q.lcap, q.cellcap);
+                       frame_counts, b.status, q.lcap, q.cellcap, only_flagged);
+}
+
+// The path-code kernel for a group of the node-list plan (same candidate capacity NT * KPT, its own
+// workgroup shape PNT x PKPT), then, if some level of the group may not fit it, the node-list kernel over the
+// (frame, level)s it flagged.
+template <int NT, int KPT, int PNT, int PKPT>
+static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
+                      hipStream_t s)
+{
+    static_assert(PNT * PKPT >= NT * KPT, "at least the node-list kernel's capacity");
+    if (q.ninv == 0 || getenv("ORBX_QT_NODES")) {
+        qt_launch_nodes<NT, KPT, false>(g, b, frame_counts, q, batch, s, 0);
+        return;
+    }
+    const size_t smem = qp_layout(PNT * PKPT, q.lcap, q.cellcap, q.ninv, q.nbins).total;
+    hipFuncSetAttribute((const void*)k_qt_paths<PNT, PKPT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL((k_qt_paths<PNT, PKPT>), dim3(q.nl, batch), dim3(PNT), smem, s, q.l0, b.geom, b.cells, b.slots,
+                       b.cell_counts, b.cell_addr, b.qpt, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts,
+                       b.status, q.lcap, q.cellcap, q.ninv, q.nbins);
+    bool fb = false;
+    for (int l = q.l0; l < q.l0 + q.nl; ++l) fb |= !g.lv[l].qp_ok || g.lv[l].slot_cap > PNT * PKPT;
+    if (fb) qt_launch_nodes<NT, KPT, false>(g, b, frame_counts, q, batch, s, 1);
 }
 
 // Launch groups.  A group's node capacity is the largest cap + 4 of its levels: a level's list never holds
@@ -2561,11 +2759,15 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
     auto caps = [&](QtGroup& q) {
         q.lcap = 8;
         q.cellcap = 1;
-        q.nbins = 0;   // 0: no level of the group takes the path-code kernel
+        q.ninv = 0;   // 0: no level of the group takes the path-code kernel
+        q.nbins = 0;
         for (int l = q.l0; l < q.l0 + q.nl; ++l) {
             q.lcap = std::max(q.lcap, g.lv[l].cap + 4);
             q.cellcap = std::max(q.cellcap, g.lv[l].ncells);
-            if (g.lv[l].qp_ok) q.nbins = std::max(q.nbins, 1 << g.lv[l].qp_bb);
+            if (g.lv[l].qp_ok) {
+                q.ninv = std::max(q.ninv, (g.lv[l].nIni << g.lv[l].qp_D) + (1 << g.lv[l].qp_D));
+                q.nbins = std::max(q.nbins, 1 << g.lv[l].qp_bb);
+            }
         }
     };
     bool anyg = false;
@@ -2574,7 +2776,7 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
     // the levels run concurrently instead of as dependent launches (latency, not throughput).
     // A level run with more register capacity than qt_regcap(g, l) spills less than its region holds.
     if (batch <= kQtMergedMaxBatch && !anyg) {
-        QtGroup q{0, g.nlevels, 512, g.qt_kpt0, 0, 0, 0, 0};
+        QtGroup q{0, g.nlevels, 512, g.qt_kpt0, 0, 0, 0, 0, 0};
         caps(q);
         if (qt_layout(q.lcap, q.cellcap, 2, qt_kpn(q.nt, q.kpt, 0)).total <= kQtLdsMax) {
             out[0] = q;
@@ -2588,7 +2790,7 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
         const int nt = qt_nt(g, l0), kpt = qt_kpt(g, l0), gl = g.lv[l0].qt_glob;
         int l1 = l0 + 1;
         while (l1 < g.nlevels && qt_nt(g, l1) == nt && qt_kpt(g, l1) == kpt && g.lv[l1].qt_glob == gl) ++l1;
-        QtGroup q{l0, l1 - l0, nt, kpt, gl, 0, 0, 0};
+        QtGroup q{l0, l1 - l0, nt, kpt, gl, 0, 0, 0, 0};
         caps(q);
         out[n++] = q;
         l0 = l1;
@@ -2664,7 +2866,7 @@ void qp_tables(Geometry& g, std::vector<uint32_t>& tab)
         int rb = 1;
         while ((1 << rb) < nIni) ++rb;
         if (L.qt_glob || rb + 2 * D + 8 > 32 || D < 1) continue;
-        int bb = 0;   // sort bins: about four candidates per bin when the workgroup is full
+        int bb = 0;   // sort bins: about a quarter of the candidates a workgroup holds
         while ((8 << bb) <= qt_regcap(g, l)) ++bb;
         L.qp_ok = 1;
         L.qp_D = D;
@@ -2690,8 +2892,11 @@ void qp_tables(Geometry& g, std::vector<uint32_t>& tab)
                 if (bit) x0 = mid; else x1 = mid;
             }
             tab[L.qp_xk + x] = code << 8;
+            // a candidate's FAST cell column: x = j * wCell + 3 + (its column in the cell's detection window),
+            // src/ORBextractor.cc:952-1000
+            const uint32_t col = x >= 3 ? (uint32_t)((x - 3) / L.qp_wc) : 0u;
             uint32_t& inv = tab[L.qp_xi + (((size_t)r << D) | bits)];
-            if (inv == 0xFFFFFFFFu) inv = (uint32_t)x;   // the smallest coordinate of a code is the keypoints'
+            if (inv == 0xFFFFFFFFu) inv = (col << 12) | (uint32_t)x;   // the smallest coordinate of a code is the keypoints'
         }
         for (int y = 0; y < L.h; ++y) {
             int y0 = 0, y1 = L.qh;
@@ -2704,8 +2909,9 @@ void qp_tables(Geometry& g, std::vector<uint32_t>& tab)
                 if (bit) y0 = mid; else y1 = mid;
             }
             tab[L.qp_yk + y] = code << 8;
+            const uint32_t row = y >= 3 ? (uint32_t)((y - 3) / L.qp_hc) : 0u;
             uint32_t& inv = tab[L.qp_yi + bits];
-            if (inv == 0xFFFFFFFFu) inv = (uint32_t)y;
+            if (inv == 0xFFFFFFFFu) inv = (row << 12) | (uint32_t)y;
         }
     }
 }
@@ -2730,11 +2936,11 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
     const int ng = qt_plan(g, batch, grp);
     for (int i = 0; i < ng; ++i) {
         const QtGroup& q = grp[i];
-        if (q.glob) qt_launch<kQtGlobNT, kQtGlobKPT, true>(g, b, frame_counts, q, batch, s);
-        else if (q.nt == 512 && q.kpt == 24) qt_launch<512, 24, false>(g, b, frame_counts, q, batch, s);
-        else if (q.nt == 512 && q.kpt == 16) qt_launch<512, 16, false>(g, b, frame_counts, q, batch, s);
-        else if (q.nt == 512) qt_launch<512, 8, false>(g, b, frame_counts, q, batch, s);
-        else qt_launch<256, 4, false>(g, b, frame_counts, q, batch, s);
+        if (q.glob) qt_launch_nodes<kQtGlobNT, kQtGlobKPT, true>(g, b, frame_counts, q, batch, s, 0);
+        else if (q.nt == 512 && q.kpt == 24) qt_launch<512, 24, 1024, 12>(g, b, frame_counts, q, batch, s);
+        else if (q.nt == 512 && q.kpt == 16) qt_launch<512, 16, 1024, 11>(g, b, frame_counts, q, batch, s);
+        else if (q.nt == 512) qt_launch<512, 8, 1024, 4>(g, b, frame_counts, q, batch, s);
+        else qt_launch<256, 4, 256, 4>(g, b, frame_counts, q, batch, s);
     }
 }
 

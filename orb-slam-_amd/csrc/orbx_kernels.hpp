@@ -59,7 +59,8 @@ enum : int {
 // live in global memory (ExtractBufs::qt_nodes) because lcap nodes need more LDS than a workgroup has.
 struct QtGroup {
     int l0, nl, nt, kpt, glob, lcap, cellcap;
-    int nbins;   // path-code kernel sort bins (the group's largest); 0: node-list kernel only
+    int ninv;    // path-code kernel: the group's largest inverse-table size (entries); 0: node-list kernel only
+    int nbins;   // path-code kernel: the group's largest sort-bin count
 };
 constexpr int kQtMaxGroups = kMaxLevels + 1;
 int qt_plan(const Geometry& g, int batch, QtGroup* out);   // returns the group count
