@@ -362,6 +362,13 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
                 cells.push_back(c);
             }
         }
+        // empty cells up to a whole number of FAST waves (kCellsPerWave): no wave spans two levels
+        while (((int)cells.size() - L.cell_begin) % kCellsPerWave) {
+            Cell c{};
+            c.level = (int16_t)l;
+            c.slot_base = slot;
+            cells.push_back(c);
+        }
         L.ncells = (int)cells.size() - L.cell_begin;
         L.slot_cap = slot - L.slot_begin;
         maxcells = std::max(maxcells, L.ncells);
@@ -449,7 +456,7 @@ orbx_status ensure_batch(orbx_handle* h, int batch)
     if (!dalloc(h, h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h, h->d_slots, (size_t)g.slots_per_frame * B) ||
         !dalloc(h, h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h, h->d_cell_addr, (size_t)g.ncells * B) || !dalloc(h, h->d_spill, (size_t)g.spill_per_frame * B) ||
         !dalloc(h, h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h, h->d_qt_out, (size_t)g.out_per_frame * B) ||
-        !dalloc(h, h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h, h->d_status, 16) ||
+        !dalloc(h, h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h, h->d_status, kFillOff + (size_t)g.nlevels * B) ||
         !dalloc(h, h->d_qt_nodes, (size_t)g.qtg_per_frame * B)) {
         h->batch_cap = 0;
         return ORBX_ENOMEM;
@@ -515,12 +522,9 @@ void enqueue_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoi
 {
     const Geometry& g = h->geom;
     ExtractBufs b = bufs(h);
-    if (counts == h->d_status + 1 && batch == 1) {   // the host path: status and count in one memset
-        hipMemsetAsync(h->d_status, 0, 2 * sizeof(int), s);
-    } else {
-        hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
-        hipMemsetAsync(h->d_status, 0, sizeof(int), s);
-    }
+    // the status block: error bits, (host path) the count, FAST's fill counters
+    if (!(counts == h->d_status + 1 && batch == 1)) hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
+    hipMemsetAsync(h->d_status, 0, sizeof(int) * (kFillOff + (size_t)g.nlevels * batch), s);
     if (ev) hipEventRecord(ev[0], s);
     launch_pyramid(g, b, P, batch, s);
     if (ev) hipEventRecord(ev[1], s);
@@ -897,7 +901,7 @@ orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* 
     switch (stage) {
     case 0:
         hipMemsetAsync(d_counts, 0, sizeof(int) * batch, s);
-        hipMemsetAsync(h->d_status, 0, sizeof(int), s);
+        hipMemsetAsync(h->d_status, 0, sizeof(int) * (kFillOff + (size_t)g.nlevels * batch), s);
         launch_pyramid(g, b, P, batch, s);
         break;
     case 1:

@@ -692,10 +692,7 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* m, int t)
 // its neighbour), and the realigning second dword of a lane is the next lane's, read by DPP at the
 // commit, so a pass costs one register.  LD passes are prefetched (the launch's largest ROI: 8 for
 // 38 x 39, 10 for 38 x 46 ROIs); bigger ROIs load their remainder synchronously.
-#ifndef ORBX_FAST_CPW
-#define ORBX_FAST_CPW 3
-#endif
-constexpr int kCellsPerWave = ORBX_FAST_CPW;   // cells per wave: the next cell's ROI loads fly under this one's passes
+// kCellsPerWave (orbx_kernels.hpp) cells per wave: the next cell's ROI loads fly under this one's passes
 
 template <int LD>
 struct FastPrefetch {
@@ -793,6 +790,9 @@ __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builti
 #ifndef ORBX_FAST_SPT
 #define ORBX_FAST_SPT 1   // strength entries per lane per trip
 #endif
+#ifndef ORBX_FAST_BUMP
+#define ORBX_FAST_BUMP 1   // 1: a wave's run taken from the level's fill counter after its last cell; 0: see below
+#endif
 #ifndef ORBX_FAST_P1
 #define ORBX_FAST_P1 2    // pass 1: 2 = compile-time column width, unchecked full trips; 1 = round 3's loop
 #endif
@@ -800,7 +800,7 @@ template <int TP, int LD>
 __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                    const Cell* __restrict__ cells, uint32_t* __restrict__ slots,
                                                    int* __restrict__ cell_counts, uint32_t* __restrict__ cell_addr,
-                                                   int cb, int ce, int rw, int rh, int cpw)
+                                                   int* __restrict__ fill, int cb, int ce, int rw, int rh, int cpw)
 {
     // cells [cb, ce); LDS sized from the group's largest cell ROI (rw x rh)
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
@@ -817,14 +817,19 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     const int lcap = fast_list_cap(rw, rh);
     uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
     // lane i: the wave's cell c0 + i -- its candidate count, obuf offset (buffered cells) and the slot its
-    // candidates start at.  The wave's first cells are buffered in obuf and go to HBM together after its
-    // last cell, packed from the first cell's slot base (consecutive slot regions, each holding its cell's
-    // count), so a wave's candidates form one run of whole lines for the quadtree's gather (cell_addr says
-    // where each cell's start).  A cell that does not fit writes straight to its own slot region, and so do
-    // the wave's later cells: the packed run then ends before that region.
+    // candidates start at.  The wave's cells (one level: the cell lists are padded to whole waves) are
+    // buffered in obuf and go to HBM together after its last cell, as one run taken from the level's slot
+    // region by a bump counter (fill), so a level's candidates end up dense, in whole lines, for the
+    // quadtree's gather (cell_addr says where each cell's start).  A cell that does not fit obuf, and the
+    // wave's cells after it, take runs of their own.
+    const int lev = cells[c0].level;
+    int* lfill = fill + (size_t)f * G->nlevels + lev;
+    const int lslot = G->lv[lev].slot_begin;
     int cnt_all = 0, c_off = -1, c_addr = 0;   // c_off >= 0: the lane's cell is buffered
     int obn = 0;
     bool direct = false;   // wave-uniform
+    int early = 0;             // lane 0: the run's offset, when taken before the last cell's output
+    bool have_early = false;   // wave-uniform
     // kept-pixel bitmask, one u64 per window row: aliases the tile, which is dead once every strength
     // of the cell is known
     unsigned long long* kept = (unsigned long long*)tile;
@@ -875,7 +880,6 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     for (int c = c0; c < c1; ++c) {
         const int dw = C.roi_w - 6, dh = C.roi_h - 6;
         const Cell Cc = C;
-        if (lane == c - c0) c_addr = Cc.slot_base;
         FP_STAMP(7);
         fast_commit(F, S, M, 0, tile);
         for (int u0 = LD; u0 * FastLaneMap<TP>::kRPP < S.rh; u0 += LD) {   // ROIs beyond LD passes
@@ -1045,6 +1049,12 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             kept_n = nms(nf2, nbk, t_min, keepm);
         }
         FP_STAMP(4);
+        // the wave's last cell: its run is known now, so the bump allocation's round trip overlaps the output
+        // (ORBX_FAST_BUMP=2: 87 VGPRs against 79)
+        if (ORBX_FAST_BUMP == 2 && c == c1 - 1 && !direct && obn + kept_n > 0 && obn + kept_n <= kFastObCap) {
+            if (lane == 0) early = atomicAdd(lfill, obn + kept_n);
+            have_early = true;
+        }
 
         // ---- output: kept pixels into the per-row bitmask (the tile is dead now), then row-major into
         // the wave's output buffer (or, for a cell with more than the buffer holds, straight to HBM)
@@ -1090,7 +1100,15 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 obn += kept_n;
             } else {   // rare: more than obuf holds
                 direct = true;
-                uint32_t* dst = fslots + Cc.slot_base;
+#if ORBX_FAST_BUMP
+                int a = 0;
+                if (lane == 0) a = atomicAdd(lfill, kept_n);
+                a = lslot + __builtin_amdgcn_readfirstlane(a);
+#else
+                const int a = Cc.slot_base;
+#endif
+                if (lane == ci) c_addr = a;
+                uint32_t* dst = fslots + a;
                 while (bits) {
                     const int jj = __builtin_ctzll(bits);
                     bits &= bits - 1;
@@ -1106,8 +1124,14 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         fp_acc[6] += 1;
 #endif
     }
-    if (obn > 0) {   // the buffered cells, packed from the wave's first cell's slot base
+    if (obn > 0) {   // the buffered cells: one run from the level's region
+#if ORBX_FAST_BUMP
+        int a = early;
+        if (!have_early && lane == 0) a = atomicAdd(lfill, obn);
+        const int base = lslot + __builtin_amdgcn_readfirstlane(a);
+#else   // round 4's first form: the wave's run from its first cell's slot region (gaps between waves)
         const int base = cells[c0].slot_base;
+#endif
         uint32_t* out = fslots + base;
         if (lane < obn) out[lane] = obuf[lane];
         if (lane + 64 < obn) out[lane + 64] = obuf[lane + 64];
@@ -1191,7 +1215,7 @@ static void fast_launch(const ExtractBufs& b, const FramePtrs& p, int cb, int ce
     const size_t smem = fast_wave_bytes(rw, rh);
     hipFuncSetAttribute((const void*)k_fast_cells<TP, LD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_fast_cells<TP, LD>), grid, dim3(64), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
-                       b.cell_addr, cb, ce, rw, rh, cpw);
+                       b.cell_addr, b.status + kFillOff, cb, ce, rw, rh, cpw);
 }
 
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
@@ -1410,7 +1434,7 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 }
 
 #ifndef ORBX_QT0_WPE
-#define ORBX_QT0_WPE 3   // round 4: the path-code kernel's fallback; 3 keeps it free of scratch (168 VGPRs)
+#define ORBX_QT0_WPE 4
 #endif
 #ifndef ORBX_QT1_WPE
 #define ORBX_QT1_WPE 4
@@ -2736,7 +2760,10 @@ static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts
                       hipStream_t s)
 {
     static_assert(PNT * PKPT >= NT * KPT, "at least the node-list kernel's capacity");
-    if (q.ninv == 0 || getenv("ORBX_QT_NODES")) {
+    // Round 4: measured slower than the node-list kernel once FAST writes each wave's candidates as one run
+    // (DESIGN.md §6), so it runs only when ORBX_QT_PATHS=1 asks for it.
+    static const bool paths = getenv("ORBX_QT_PATHS") && atoi(getenv("ORBX_QT_PATHS")) != 0;
+    if (q.ninv == 0 || !paths) {
         qt_launch_nodes<NT, KPT, false>(g, b, frame_counts, q, batch, s, 0);
         return;
     }

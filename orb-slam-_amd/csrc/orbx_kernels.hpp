@@ -34,7 +34,7 @@ struct ExtractBufs {
     const uint32_t* qpt;        // K3 path tables (LevelGeom::qp_*)
     uint32_t* qt_out;           // [B][out_per_frame] retained keypoints (level coords)
     int* qt_cnt;                // [B][nlevels]
-    int* status;                // device error word (bit flags)
+    int* status;                // device error word (bit flags), then the FAST fill counters (kFillOff)
 };
 
 // XCD-aware workgroup order.  The dispatcher hands flat workgroup id b to XCD b % 8;
@@ -77,6 +77,15 @@ void qp_tables(Geometry& g, std::vector<uint32_t>& tab);
 constexpr long long kQtBigArea = 1000000;
 constexpr int kQtMergedMaxBatch = 8;   // batches up to this size run all levels in one launch
 constexpr int kLatencyMaxBatch = 8;    // batches up to this size: FAST one cell per wave, describe one keypoint per wave
+// FAST cells per wave above kLatencyMaxBatch.  Every level's cell list is padded with empty cells to a
+// multiple of it, so a wave's cells share one level and its candidates land in that level's slot region.
+#ifndef ORBX_FAST_CPW
+#define ORBX_FAST_CPW 3
+#endif
+constexpr int kCellsPerWave = ORBX_FAST_CPW;
+// The status block (ExtractBufs::status, zeroed before every extraction): [0] error bits, [1] the host
+// path's keypoint count, [kFillOff + f * nlevels + l] the slots FAST has handed out in (frame f, level l).
+constexpr int kFillOff = 16;
 // Workgroup size and keypoints per thread of level l's quadtree: level 0 holds most candidates
 // (KITTI ~6,800), level 1 ~2,700, levels >= 2 a few hundred.  Measured per launch (KITTI, 192 frames):
 // fewer waves per workgroup on the small levels does not shorten them (one wave for levels 3-7:
