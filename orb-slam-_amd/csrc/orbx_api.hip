@@ -356,6 +356,9 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
                 L.roi_mw = std::max(L.roi_mw, (int)c.roi_w);
                 L.roi_mh = std::max(L.roi_mh, (int)c.roi_h);
                 const int dw = c.roi_w - 6, dh = c.roi_h - 6;
+                // a FAST wave's cells (kCellsPerWave consecutive cells of the level) write one run from the
+                // first one's slot base: it starts on a 128-byte line, so the quadtree's gather reads whole lines
+                if (((int)cells.size() - L.cell_begin) % kCellsPerWave == 0) slot = (slot + 31) & ~31;
                 c.slot_base = slot;
                 c.slot_cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
                 slot += c.slot_cap;
@@ -391,7 +394,7 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     std::vector<int4> pyrbt;
     if (!pyr_plan(g, yt.data(), pyrbt)) return ORBX_EINVAL;
     fast_groups(g);
-    g.slots_per_frame = slot;
+    g.slots_per_frame = (slot + 31) & ~31;   // frames' slot blocks start on 128-byte lines
     g.out_per_frame = out;
     g.max_cells_level = maxcells;
     g.lcap = lcap;

@@ -790,8 +790,14 @@ __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builti
 #ifndef ORBX_FAST_SPT
 #define ORBX_FAST_SPT 1   // strength entries per lane per trip
 #endif
+// A wave's candidates go to HBM as one run from its first cell's slot region, which starts on a 128-byte line
+// (the slot regions of a wave's cells are consecutive, so the run fits).  ORBX_FAST_BUMP=1: the run taken
+// instead from a per-(frame, level) fill counter by one atomic after the wave's last cell, so each level's
+// candidates are dense: quadtree fetch 1.05x algorithmic, but FAST waits on the atomic's round trip
+// (+13-19 us per 384 frames, -0.8% frames/s).  Taking each cell's run by its own lane as soon as it is known,
+// so the return lands under the next cells: 783 against 669 us.
 #ifndef ORBX_FAST_BUMP
-#define ORBX_FAST_BUMP 1   // 1: a wave's run taken from the level's fill counter after its last cell; 0: see below
+#define ORBX_FAST_BUMP 0
 #endif
 #ifndef ORBX_FAST_P1
 #define ORBX_FAST_P1 2    // pass 1: 2 = compile-time column width, unchecked full trips; 1 = round 3's loop
@@ -818,18 +824,16 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
     // lane i: the wave's cell c0 + i -- its candidate count, obuf offset (buffered cells) and the slot its
     // candidates start at.  The wave's cells (one level: the cell lists are padded to whole waves) are
-    // buffered in obuf and go to HBM together after its last cell, as one run taken from the level's slot
-    // region by a bump counter (fill), so a level's candidates end up dense, in whole lines, for the
-    // quadtree's gather (cell_addr says where each cell's start).  A cell that does not fit obuf, and the
-    // wave's cells after it, take runs of their own.
+    // buffered in obuf and go to HBM together after its last cell, as one run from a 128-byte line
+    // (ORBX_FAST_BUMP above), so the quadtree's gather reads few partial lines (cell_addr says where each
+    // cell's candidates start).  A cell that does not fit obuf, and the wave's cells after it, write to their
+    // own slot regions.
     const int lev = cells[c0].level;
     int* lfill = fill + (size_t)f * G->nlevels + lev;
     const int lslot = G->lv[lev].slot_begin;
     int cnt_all = 0, c_off = -1, c_addr = 0;   // c_off >= 0: the lane's cell is buffered
     int obn = 0;
     bool direct = false;   // wave-uniform
-    int early = 0;             // lane 0: the run's offset, when taken before the last cell's output
-    bool have_early = false;   // wave-uniform
     // kept-pixel bitmask, one u64 per window row: aliases the tile, which is dead once every strength
     // of the cell is known
     unsigned long long* kept = (unsigned long long*)tile;
@@ -1049,12 +1053,6 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             kept_n = nms(nf2, nbk, t_min, keepm);
         }
         FP_STAMP(4);
-        // the wave's last cell: its run is known now, so the bump allocation's round trip overlaps the output
-        // (ORBX_FAST_BUMP=2: 87 VGPRs against 79)
-        if (ORBX_FAST_BUMP == 2 && c == c1 - 1 && !direct && obn + kept_n > 0 && obn + kept_n <= kFastObCap) {
-            if (lane == 0) early = atomicAdd(lfill, obn + kept_n);
-            have_early = true;
-        }
 
         // ---- output: kept pixels into the per-row bitmask (the tile is dead now), then row-major into
         // the wave's output buffer (or, for a cell with more than the buffer holds, straight to HBM)
@@ -1124,13 +1122,13 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         fp_acc[6] += 1;
 #endif
     }
-    if (obn > 0) {   // the buffered cells: one run from the level's region
+    if (obn > 0) {   // the buffered cells: one run
 #if ORBX_FAST_BUMP
-        int a = early;
-        if (!have_early && lane == 0) a = atomicAdd(lfill, obn);
+        int a = 0;
+        if (lane == 0) a = atomicAdd(lfill, obn);
         const int base = lslot + __builtin_amdgcn_readfirstlane(a);
-#else   // round 4's first form: the wave's run from its first cell's slot region (gaps between waves)
-        const int base = cells[c0].slot_base;
+#else
+        const int base = cells[c0].slot_base;   // 128-byte aligned (ensure_geometry)
 #endif
         uint32_t* out = fslots + base;
         if (lane < obn) out[lane] = obuf[lane];
