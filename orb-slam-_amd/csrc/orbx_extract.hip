@@ -707,9 +707,16 @@ struct FastCellSrc {
 // The lane map of the tile pitch's widest row (TP / 4 dwords + the extra one): rows per pass and the
 // lane's (row in pass, dword) are compile-time / per-kernel constants, so every pass's offsets are
 // immediates; a narrower cell leaves its lanes past its own dwords idle.
+// ORBX_FAST_UNAL=1: each lane loads its dword at the exact (unaligned) ROI byte, which gfx950 serves
+// exactly (tools/probes/glb_unaligned.hip), so the commit is a plain store: no realigning alignbyte, no DPP
+// for the neighbour dword, no extra dword per row (TP / 4 lanes per row instead of TP / 4 + 1).
+#ifndef ORBX_FAST_UNAL
+#define ORBX_FAST_UNAL 1
+#endif
+__host__ __device__ constexpr int fast_lanes_per_row(int tp) { return ORBX_FAST_UNAL ? tp / 4 : tp / 4 + 1; }
 template <int TP>
 struct FastLaneMap {
-    static constexpr int kND1 = TP / 4 + 1, kRPP = 64 / kND1;
+    static constexpr int kND1 = fast_lanes_per_row(TP), kRPP = 64 / kND1;
     int rl, kl;
     __device__ explicit FastLaneMap(int lane) : rl(lane / kND1), kl(lane - (lane / kND1) * kND1) {}
 };
@@ -717,6 +724,17 @@ struct FastLaneMap {
 template <int TP, int LD>
 __device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneMap<TP>& M, int u0, FastPrefetch<LD>& F)
 {
+#if ORBX_FAST_UNAL
+    const __attribute__((address_space(1))) uint8_t* base = (const __attribute__((address_space(1))) uint8_t*)S.src;
+    const bool lane_ok = M.rl < FastLaneMap<TP>::kRPP && M.kl < S.nd;
+    const uint32_t o0 = (uint32_t)__mul24(u0 * FastLaneMap<TP>::kRPP + M.rl, S.pitch) + 4u * (uint32_t)M.kl;
+    const uint32_t dsh = (uint32_t)__mul24(FastLaneMap<TP>::kRPP, S.pitch);
+#pragma unroll
+    for (int u = 0; u < LD; ++u) {
+        const int row = (u0 + u) * FastLaneMap<TP>::kRPP + M.rl;
+        if (lane_ok && row < S.rh) F.w[u] = *(const __attribute__((address_space(1))) uint32_t*)(base + o0 + (uint32_t)u * dsh);
+    }
+#else
     // 32-bit byte offsets from the wave-uniform aligned ROI origin: scalar base + vector offset
     // addressing, no 64-bit address arithmetic per load
     const __attribute__((address_space(1))) uint8_t* base =
@@ -731,6 +749,7 @@ __device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneM
             F.w[u] = *(const __attribute__((address_space(1))) uint32_t*)(base + o);
         }
     }
+#endif
 }
 
 // 4 pixels of ROI row r from column 4 kl: the lane's dword and its neighbour's realigned by the row's
@@ -741,6 +760,16 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const Fas
                                             const FastLaneMap<TP>& M, int u0, uint8_t* tile)
 {
     constexpr int kRPP = FastLaneMap<TP>::kRPP;
+#if ORBX_FAST_UNAL
+    {
+        const bool lane_ok = M.rl < kRPP && M.kl < S.nd;
+        const int row0 = u0 * kRPP + M.rl;
+        uint8_t* dst = tile + row0 * TP + 4 * M.kl;
+#pragma unroll
+        for (int u = 0; u < LD; ++u)
+            if (lane_ok && row0 + u * kRPP < S.rh) *(uint32_t*)(dst + u * kRPP * TP) = F.w[u];
+    }
+#else
     const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
     const bool lane_ok = M.rl < kRPP && M.kl < S.nd;
     const int row0 = u0 * kRPP + M.rl;
@@ -753,6 +782,7 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const Fas
         if (lane_ok && row0 + u * kRPP < S.rh)
             *(uint32_t*)(dst + u * kRPP * TP) = __builtin_amdgcn_alignbyte(hi, F.w[u], sh0 + (uint32_t)u * dsh);
     }
+#endif
 }
 
 #ifdef ORBX_FAST_PROF
@@ -1225,7 +1255,7 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
     static const int one = getenv("ORBX_FAST_ONE") ? atoi(getenv("ORBX_FAST_ONE")) : 1;
     if (one && batch <= kLatencyMaxBatch && g.fast_groups > 1) {
         const int rw = std::max(g.fast_rw[0], g.fast_rw[1]), rh = std::max(g.fast_rh[0], g.fast_rh[1]);
-        const int rpp = 64 / (fast_tile_pitch(rw) / 4 + 1), ld = (rh + rpp - 1) / rpp;
+        const int rpp = 64 / fast_lanes_per_row(fast_tile_pitch(rw)), ld = (rh + rpp - 1) / rpp;
         if (fast_tile_pitch(rw) == 40) {
             if (ld <= 8) fast_launch<40, 8>(b, p, 0, g.ncells, rw, rh, cpw, batch, s);
             else fast_launch<40, 10>(b, p, 0, g.ncells, rw, rh, cpw, batch, s);
@@ -1239,7 +1269,7 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
         if (ce <= cb) continue;
         const int rw = g.fast_rw[i], rh = g.fast_rh[i];
         // register prefetch passes: the group's largest ROI in passes of whole rows (FastLaneMap)
-        const int rpp = 64 / (fast_tile_pitch(rw) / 4 + 1), ld = (rh + rpp - 1) / rpp;
+        const int rpp = 64 / fast_lanes_per_row(fast_tile_pitch(rw)), ld = (rh + rpp - 1) / rpp;
         if (fast_tile_pitch(rw) == 40) {
             if (ld <= 8) fast_launch<40, 8>(b, p, cb, ce, rw, rh, cpw, batch, s);
             else fast_launch<40, 10>(b, p, cb, ce, rw, rh, cpw, batch, s);
