@@ -673,10 +673,25 @@ __device__ __forceinline__ _Float16 fast_compass_q(const uint8_t* c)
     return __builtin_fmaxf16(q.x, q.y);   // one v_max_f16 (SDWA high-half operand)
 }
 
-// strict 3x3 non-maximum suppression on the strength map at threshold t (m[0]: the pixel)
+// strict 3x3 non-maximum suppression on the strength map at threshold t (m[0]: the pixel).  cv::FAST keeps
+// a corner whose score s - 1 beats every neighbour's score, a neighbour that is no corner at t scoring 0:
+//   s > t and, for each neighbour n, (n > t ? s > n : s > 1),
+// and since s > t already beats every n <= t, that is s > max(t, 1, n_0 .. n_7): four max3, one compare.
+// (t1 = max(t, 1), wave-uniform)
+__device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c); }
+#ifndef ORBX_FAST_NMSMAX
+#define ORBX_FAST_NMSMAX 1
+#endif
 template <int TP>
-__device__ __forceinline__ bool nms_keep(const uint8_t* m, int t)
+__device__ __forceinline__ bool nms_keep(const uint8_t* m, uint32_t t1)
 {
+#if ORBX_FAST_NMSMAX
+    const uint32_t a = umax3(m[-TP - 1], m[-TP], m[-TP + 1]);
+    const uint32_t b = umax3(m[-1], m[1], m[TP - 1]);
+    const uint32_t c = umax3(m[TP], m[TP + 1], t1);
+    return (uint32_t)m[0] > umax3(a, b, c);
+#else   // round 3: the per-neighbour form
+    const int t = (int)t1 == 1 ? 0 : (int)t1;   // (t >= 1 in every configuration the tests run)
     const int s = m[0];
     if (s <= t) return false;
     const int sc = s - 1;
@@ -685,6 +700,7 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* m, int t)
 #pragma unroll
     for (int k = 0; k < 8; ++k) keep &= sc > (nb[k] > t ? nb[k] - 1 : 0);
     return keep;
+#endif
 }
 
 // ROI bytes of one cell staged in registers, in passes of rpp whole rows: lane = rl * (nd + 1) + kl loads
@@ -829,6 +845,15 @@ __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builti
 #ifndef ORBX_FAST_BUMP
 #define ORBX_FAST_BUMP 0
 #endif
+// Row-validity masks of pass 1: 0 = a ballot of one compare per row step; 1 = scalar arithmetic per trip
+// (697.6 against 641.5 us: FAST is sensitive to its scalar instruction count), 2 = the last trip's masks
+// hoisted out of the loop, a select per trip (657.7 us)
+#ifndef ORBX_FAST_ROWMASK
+#define ORBX_FAST_ROWMASK 0
+#endif
+#ifndef ORBX_FAST_CWT
+#define ORBX_FAST_CWT 0
+#endif
 #ifndef ORBX_FAST_P1
 #define ORBX_FAST_P1 2    // pass 1: 2 = compile-time column width, unchecked full trips; 1 = round 3's loop
 #endif
@@ -948,30 +973,62 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         // (survivors are emitted through the row bitmask), so a trip's back entries take
         // [lcap - nb - count, lcap - nb) in lane order.  (Tried: a compile-time column width with immediate
         // second-row offsets and unchecked full trips: 85-95 VGPRs instead of 80, 6 -> 5 waves per SIMD.)
-        const int cw_shift = dw <= 32 ? 5 : 6;
-        const int col = lane & ((1 << cw_shift) - 1);
-        const int rstep = 64 >> cw_shift;
-        const int rlane = lane >> cw_shift;
-        const unsigned long long colmask = ballot64(col < dw);
-        int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
-        for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {
-            const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
-            const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
-            const unsigned long long va = colmask & ballot64(rlane < dh - r0);
-            const unsigned long long vb = colmask & ballot64(rlane < dh - r0 - rstep);
-            const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
-            const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
-            const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
-            if (__builtin_amdgcn_inverse_ballot_w64(mfa)) list[nf + lanes_below(mfa)] = (uint16_t)t;
-            nf += __popcll(mfa);
-            if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
-            nf += __popcll(mfb);
-            nb += __popcll(mba);
-            if (__builtin_amdgcn_inverse_ballot_w64(mba)) list[lcap - nb + lanes_below(mba)] = (uint16_t)t;
-            nb += __popcll(mbb);
-            if (__builtin_amdgcn_inverse_ballot_w64(mbb)) list[lcap - nb + lanes_below(mbb)] = (uint16_t)(t + rstep * TP);
-            t += 2 * rstep * TP;
-        }
+        // ORBX_FAST_CWT=1: the loop compiled once per column width (cw = 32 or 64), so the second row
+        // step's offset is an immediate
+        auto pass1 = [&](auto cw_tag) {
+            constexpr int kCwShift = decltype(cw_tag)::value;
+            const int cw_shift = kCwShift > 0 ? kCwShift : (dw <= 32 ? 5 : 6);
+            const int col = lane & ((1 << cw_shift) - 1);
+            const int rstep = 64 >> cw_shift;
+            const int rlane = lane >> cw_shift;
+            const unsigned long long colmask = ballot64(col < dw);
+            // lanes of the first k rows of a row step (whole rows of cw lanes): scalar arithmetic, no compare
+            // (branch-free: a branch here splits the loop body, and the byte loads above it get re-masked)
+            auto rows_below = [&](int k) -> unsigned long long {
+#if ORBX_FAST_ROWMASK
+                const int n = min(max(k, 0), rstep) << cw_shift;
+                return n >= 64 ? ~0ull : (1ull << n) - 1ull;
+#else
+                return ballot64(rlane < k);
+#endif
+            };
+            int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
+#if ORBX_FAST_ROWMASK == 2
+            // every trip but the last covers whole row steps: its masks are colmask; the last trip's, once
+            const int r_last = (dh - 1) / (2 * rstep) * (2 * rstep);
+            const unsigned long long va_last = colmask & rows_below(dh - r_last);
+            const unsigned long long vb_last = colmask & rows_below(dh - r_last - rstep);
+#endif
+            for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {
+                const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
+                const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
+#if ORBX_FAST_ROWMASK == 2
+                const unsigned long long va = r0 == r_last ? va_last : colmask;
+                const unsigned long long vb = r0 == r_last ? vb_last : colmask;
+#else
+                const unsigned long long va = colmask & rows_below(dh - r0);
+                const unsigned long long vb = colmask & rows_below(dh - r0 - rstep);
+#endif
+                const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
+                const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
+                const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
+                if (__builtin_amdgcn_inverse_ballot_w64(mfa)) list[nf + lanes_below(mfa)] = (uint16_t)t;
+                nf += __popcll(mfa);
+                if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
+                nf += __popcll(mfb);
+                nb += __popcll(mba);
+                if (__builtin_amdgcn_inverse_ballot_w64(mba)) list[lcap - nb + lanes_below(mba)] = (uint16_t)t;
+                nb += __popcll(mbb);
+                if (__builtin_amdgcn_inverse_ballot_w64(mbb)) list[lcap - nb + lanes_below(mbb)] = (uint16_t)(t + rstep * TP);
+                t += 2 * rstep * TP;
+            }
+        };
+#if ORBX_FAST_CWT
+        if (dw <= 32) pass1(std::integral_constant<int, 5>{});
+        else pass1(std::integral_constant<int, 6>{});
+#else
+        pass1(std::integral_constant<int, 0>{});
+#endif
 #else
         const int cw_shift = dw <= 32 ? 5 : 6;
         const int col = lane & ((1 << cw_shift) - 1);
@@ -1068,7 +1125,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 bool keep = false;
                 if (j < nfr + nbk) {
                     const int k = list[j < nfr ? j : lcap - 1 - (j - nfr)];
-                    keep = nms_keep<TP>(map + k + (TP + 1), th);
+                    keep = nms_keep<TP>(map + k + (TP + 1), (uint32_t)max(th, 1));
                 }
                 keepm[r >> 6] |= (unsigned long long)keep << (r & 63);
                 kept_n += __popcll(ballot64(keep));
@@ -1190,9 +1247,13 @@ namespace orbx {
 #endif
 
 // LDS per CU on gfx950: the occupancy a FAST launch's per-wave tiles allow, up to what the kernel's
-// registers allow (80 VGPRs: 6 waves per SIMD, 24 one-wave workgroups per CU)
+// registers allow (<40, 8>: 71 VGPRs, 7 waves per SIMD, 28 one-wave workgroups per CU; round 3's
+// realigning staging: 80 VGPRs, 24)
+#ifndef ORBX_FAST_OCC
+#define ORBX_FAST_OCC 28
+#endif
 constexpr size_t kLdsPerCu = 160 * 1024;
-constexpr int kFastVgprWavesPerCu = 24;
+constexpr int kFastVgprWavesPerCu = ORBX_FAST_OCC;
 static int fast_blocks_per_cu(int w, int h)
 {
     return std::min((int)(kLdsPerCu / fast_wave_bytes(w, h)), kFastVgprWavesPerCu);
@@ -1470,6 +1531,9 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 #ifndef ORBX_QT2_WPE
 #define ORBX_QT2_WPE 5
 #endif
+#ifndef ORBX_QT3_WPE
+#define ORBX_QT3_WPE 5   // <128, 8> (ORBX_QT2_SHAPE=1)
+#endif
 // Minimum waves per SIMD (HIP's second __launch_bounds__ argument), i.e. a VGPR budget per template:
 //   <512,16> (level 0) 4: 128 VGPRs (7 dwords spilled) instead of the compiler's 172, so two workgroups
 //            share a CU and a 384-frame launch runs every frame at once: 106 -> 68 us;
@@ -1482,7 +1546,7 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 #define ORBX_QT_WPE(NT, KPT, G) ((G) ? 1                                          \
                                  : ((NT) == 512 && (KPT) == 16) ? ORBX_QT0_WPE  \
                                  : ((NT) == 512 && (KPT) == 8) ? ORBX_QT1_WPE   \
-                                 : ((NT) == 256) ? ORBX_QT2_WPE : 1)
+                                 : ((NT) == 256) ? ORBX_QT2_WPE : ((NT) == 128) ? ORBX_QT3_WPE : 1)
 //
 // The node-list form of DistributeOctTree, one workgroup per (frame l's level l), used for the levels the
 // path-code kernel (k_qt_paths) does not take: node lists in global memory (kG), keys too wide for its
@@ -2995,7 +3059,11 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
         else if (q.nt == 512 && q.kpt == 24) qt_launch<512, 24, 1024, 12>(g, b, frame_counts, q, batch, s);
         else if (q.nt == 512 && q.kpt == 16) qt_launch<512, 16, 1024, 11>(g, b, frame_counts, q, batch, s);
         else if (q.nt == 512) qt_launch<512, 8, 1024, 4>(g, b, frame_counts, q, batch, s);
+#if ORBX_QT2_SHAPE
+        else qt_launch<128, 8, 256, 4>(g, b, frame_counts, q, batch, s);
+#else
         else qt_launch<256, 4, 256, 4>(g, b, frame_counts, q, batch, s);
+#endif
     }
 }
 
@@ -3021,7 +3089,13 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 constexpr int kRawP = 48;                             // LDS row pitch (bytes): the 43 columns + shift slack
 constexpr int kRawRows = 44;                          // 43 rows used (row 43 repeats row 42)
 constexpr int kRawSlots = kRawRows * kRawP / 4;
-constexpr int kTCols = 40, kTP = 22;                  // row-blurred, transposed: [col][row pairs], 22 dwords/col
+#ifndef ORBX_DESC_ROW1
+#define ORBX_DESC_ROW1 0
+#endif
+// row-blurred, transposed: [col][row pairs], 22 dwords per column; ORBX_DESC_ROW1=1: one dword per row y
+// holding rows (y, y + 1), at dword y + 1 of its column (dword 0 a pad), so a sample's seven taps are dwords
+// y + 1, y + 3, y + 5, y + 7 with fixed weights whatever y's parity
+constexpr int kTCols = 40, kTP = ORBX_DESC_ROW1 ? 44 : 22;
 #ifndef ORBX_DESC_KPW
 #define ORBX_DESC_KPW 4
 #endif
@@ -3129,6 +3203,22 @@ constexpr uint32_t kRoundBits = 0x4B400000u;
 // The LDS byte address in three VALU: bfe of by's bits 1..23 (0x200000 + (yy >> 1)), shifted and added to
 // mad24(bx, 4 kTP, C) with C = rowT + 4 (9 - 0x200000 + (18 - 0x400000) kTP) (mod 2^32); the compiler's
 // form of (by >> 1) + bx * kTP + rowT took five.
+#if ORBX_DESC_ROW1
+// dword (18 + xx) * kTP + (18 + yy) + 1: by << 2 is 4 * (0x4B400000 + yy) (mod 2^32)
+constexpr uint32_t kBlurByte0 = 4u * (19u + (18u - 0x400000u) * (uint32_t)kTP) - 4u * 0x4B400000u;
+__device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t bx)
+{
+    const uint32_t t = __umul24(bx, 4u * (uint32_t)kTP) + C;
+    uint32_t a;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"(by), "v"(t));
+    const __attribute__((address_space(3))) uint32_t* col = (const __attribute__((address_space(3))) uint32_t*)(uintptr_t)a;
+    const uint32_t d0 = col[0], d1 = col[2], d2 = col[4], d3 = col[6];
+    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), ushort2_t{18, 34}, 1u << 15, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d1), ushort2_t{49, 55}, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d2), ushort2_t{49, 34}, acc, false);
+    return __builtin_amdgcn_udot2(as_us2(d3), ushort2_t{18, 0}, acc, false);
+}
+#else
 constexpr uint32_t kBlurByte0 = 4u * (9u - 0x200000u + (18u - 0x400000u) * (uint32_t)kTP);
 __device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t bx)
 {
@@ -3149,6 +3239,7 @@ __device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t b
     acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
     return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
 }
+#endif
 
 #ifndef ORBX_DESC_WPE
 #define ORBX_DESC_WPE 1
@@ -3163,7 +3254,8 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                                                int cap, int* __restrict__ status, int kpw)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_raw[kDescWaves][kRawSlots];
-    __shared__ __attribute__((aligned(16))) uint32_t s_rowT[kDescWaves][kTCols * kTP];
+    // (ORBX_DESC_ROW1: + 4, the last column's item 21 writes one dword past its column)
+    __shared__ __attribute__((aligned(16))) uint32_t s_rowT[kDescWaves][kTCols * kTP + (ORBX_DESC_ROW1 ? 4 : 0)];
     __shared__ uint32_t s_out[kDescWaves][15 * kDescPerWave];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
@@ -3289,10 +3381,15 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     // once per wave with lane j on keypoint j, instead of once per keypoint on every lane (the angle was
     // 17% of the launch).  Loads of every keypoint first, then the sums.
     float kp_ang = 0.f, kp_cos = 1.f, kp_sin = 0.f;
-    if (nkp > 0) {
-        uint32_t q[kDescPerWave][5], qs[kDescPerWave];
+    int ic_m10 = 0, ic_m01 = 0;   // lane j: keypoint j's moments
+    // (keypoints in groups of 4: one group's 20 row dwords in registers at a time)
+    constexpr int kIcGroup = kDescPerWave < 4 ? kDescPerWave : 4;
+#pragma unroll 1
+    for (int j0 = 0; j0 < kDescPerWave && j0 < nkp; j0 += kIcGroup) {
+        uint32_t q[kIcGroup][5], qs[kIcGroup];
 #pragma unroll
-        for (int jj = 0; jj < kDescPerWave; ++jj) {
+        for (int ji = 0; ji < kIcGroup; ++ji) {
+            const int jj = j0 + ji;
             const int jc = jj < nkp ? jj : nkp - 1;   // wave-uniform
             const int l = __builtin_amdgcn_readlane(my_l, jc);
             const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)my_pk, jc);
@@ -3301,28 +3398,29 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             const uint8_t* img = level_base(P, G, f, l, pitch);
             const uintptr_t a = (uintptr_t)(img + (size_t)(cy + vrow) * pitch + (cx - 15 + 16 * ich));
             const uint32_t* src = (const uint32_t*)(a & ~(uintptr_t)3);
-            qs[jj] = (uint32_t)(a & 3);
+            qs[ji] = (uint32_t)(a & 3);
 #pragma unroll
-            for (int k = 0; k < 5; ++k) q[jj][k] = src[k];
+            for (int k = 0; k < 5; ++k) q[ji][k] = src[k];
         }
-        int m10 = 0, m01 = 0;
 #pragma unroll
-        for (int jj = 0; jj < kDescPerWave; ++jj) {
+        for (int ji = 0; ji < kIcGroup; ++ji) {
             uint32_t s1 = 0u, s0 = 0u;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const uint32_t w = __builtin_amdgcn_alignbyte(q[jj][k + 1], q[jj][k], qs[jj]);
+                const uint32_t w = __builtin_amdgcn_alignbyte(q[ji][k + 1], q[ji][k], qs[ji]);
                 s1 = __builtin_amdgcn_udot4(w, W1[k], s1, false);
                 s0 = __builtin_amdgcn_udot4(w, W0[k], s0, false);
             }
             const int x10 = wave_sum((int)s1 - 16 * (int)s0);
             const int x01 = wave_sum(vrow * (int)s0);
-            if (lane == jj) {
-                m10 = x10;
-                m01 = x01;
+            if (lane == j0 + ji) {
+                ic_m10 = x10;
+                ic_m01 = x01;
             }
         }
-        kp_ang = fast_atan2_deg((float)m01, (float)m10);
+    }
+    if (nkp > 0) {
+        kp_ang = fast_atan2_deg((float)ic_m01, (float)ic_m10);
         glibc_sincosf_pair(kp_ang * kFactorPI, &kp_sin, &kp_cos);   // (src/ORBextractor.cc:148)
     }
 #endif
@@ -3413,7 +3511,19 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                     }
                 }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
+                for (int j = 0; j < 4; ++j) {
+#if ORBX_DESC_ROW1
+                    // rows (2rp, 2rp + 1) at dword 2rp + 1, row 2rp + 1 also in the low half of dword 2rp + 2 and
+                    // row 2rp in the high half of dword 2rp (one address, three immediate offsets)
+                    const uint32_t pr = o[0][j] | (o[1][j] << 16);
+                    uint8_t* b = (uint8_t*)(rowT + (4 * cg + j) * kTP + 2 * rp) + 2;
+                    *(uint16_t*)b = (uint16_t)pr;
+                    *(uint32_t*)(b + 2) = pr;
+                    *(uint16_t*)(b + 6) = (uint16_t)(pr >> 16);
+#else
+                    rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
+#endif
+                }
             }
         };
         if (csp != 0) hpass(std::integral_constant<int, -1>{});

@@ -93,13 +93,17 @@ constexpr int kFillOff = 16;
 // a split round is a chain of dependent LDS steps whatever the workgroup size.
 // Levels whose node list runs from global memory (LevelGeom::qt_glob) take one configuration.
 constexpr int kQtGlobNT = 512, kQtGlobKPT = 8;
+// ORBX_QT2_SHAPE=1: levels >= 2 in 128-thread workgroups of 8 keypoints per thread (same capacity)
+#ifndef ORBX_QT2_SHAPE
+#define ORBX_QT2_SHAPE 0
+#endif
 __host__ __device__ inline int qt_nt(const Geometry& g, int l)
 {
-    return g.lv[l].qt_glob ? kQtGlobNT : (l >= 2 ? 256 : 512);
+    return g.lv[l].qt_glob ? kQtGlobNT : (l >= 2 ? (ORBX_QT2_SHAPE ? 128 : 256) : 512);
 }
 __host__ __device__ inline int qt_kpt(const Geometry& g, int l)
 {
-    return g.lv[l].qt_glob ? kQtGlobKPT : (l == 0 ? g.qt_kpt0 : (l == 1 ? 8 : 4));
+    return g.lv[l].qt_glob ? kQtGlobKPT : (l == 0 ? g.qt_kpt0 : (l == 1 ? 8 : (ORBX_QT2_SHAPE ? 8 : 4)));
 }
 __host__ __device__ inline int qt_regcap(const Geometry& g, int l) { return qt_nt(g, l) * qt_kpt(g, l); }
 
