@@ -616,11 +616,15 @@ __host__ __device__ inline int fast_list_cap(int rw, int rh) { return (rh - 6) *
 // store inside the cell loop would make the next cell's wait for its prefetched ROI (vmcnt counts loads
 // and stores, completed in issue order) wait for the store's round trip as well.
 constexpr int kFastObCap = 128;
+#ifndef ORBX_FAST_BACKW
+#define ORBX_FAST_BACKW 1
+#endif
+constexpr int kFastScratch = ORBX_FAST_BACKW ? 256 : 0;   // a dword per lane after obuf (pass 1's masked-off writes)
 __host__ __device__ inline size_t fast_list_bytes(int rw, int rh) { return (2 * (size_t)fast_list_cap(rw, rh) + 3) & ~(size_t)3; }
 __host__ __device__ inline size_t fast_wave_bytes(int rw, int rh)
 {
     const size_t tile = (size_t)rh * fast_tile_pitch(rw);
-    return (tile + fast_map_bytes(rw, rh) + fast_list_bytes(rw, rh) + 4 * kFastObCap + 15) & ~(size_t)15;
+    return (tile + fast_map_bytes(rw, rh) + fast_list_bytes(rw, rh) + 4 * kFastObCap + kFastScratch + 15) & ~(size_t)15;
 }
 
 // max(v - minMax, maxMin - v) over the 16 cyclic 9-arcs of the Bresenham ring of the
@@ -815,6 +819,16 @@ __device__ unsigned long long g_fast_prof[8];
 #endif
 
 __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// per lane: a if the lane's bit of the scalar mask m is set, else b -- one v_cndmask on the mask, with every
+// lane active (the compiler's form of the select is an exec-masked region)
+__device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* a, uint16_t* b)
+{
+    const uint32_t ua = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)a;
+    const uint32_t ub = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)b;
+    uint32_t r;
+    asm volatile("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(ub), "v"(ua), "s"(m));
+    return (uint16_t*)(__attribute__((address_space(3))) uint16_t*)(uintptr_t)r;
+}
 
 // K2: one wave per workgroup (LDS is granted per wave), cpw consecutive cells per wave.  Per cell
 // (src/ORBextractor.cc:952-1000, cv::FAST on the cell ROI with nonmax suppression, retried at
@@ -876,6 +890,9 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     uint16_t* list = (uint16_t*)(map + fast_map_bytes(rw, rh));
     uint32_t* obuf = (uint32_t*)((uint8_t*)list + fast_list_bytes(rw, rh));
     const int lcap = fast_list_cap(rw, rh);
+#if ORBX_FAST_BACKW
+    uint16_t* const bscratch = (uint16_t*)(obuf + kFastObCap + lane);
+#endif
     uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
     // lane i: the wave's cell c0 + i -- its candidate count, obuf offset (buffered cells) and the slot its
     // candidates start at.  The wave's cells (one level: the cell lists are padded to whole waves) are
@@ -1016,10 +1033,20 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 nf += __popcll(mfa);
                 if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
                 nf += __popcll(mfb);
+#if ORBX_FAST_BACKW
+                // back entries (a quarter of the pixels: the mask is rarely empty) written by every lane, the
+                // lanes outside the mask into their own scratch dword: an address select instead of the exec
+                // save / branch / restore (FAST's time follows its scalar instruction count)
+                nb += __popcll(mba);
+                *lds_select(mba, &list[lcap - nb + lanes_below(mba)], bscratch) = (uint16_t)t;
+                nb += __popcll(mbb);
+                *lds_select(mbb, &list[lcap - nb + lanes_below(mbb)], bscratch) = (uint16_t)(t + rstep * TP);
+#else
                 nb += __popcll(mba);
                 if (__builtin_amdgcn_inverse_ballot_w64(mba)) list[lcap - nb + lanes_below(mba)] = (uint16_t)t;
                 nb += __popcll(mbb);
                 if (__builtin_amdgcn_inverse_ballot_w64(mbb)) list[lcap - nb + lanes_below(mbb)] = (uint16_t)(t + rstep * TP);
+#endif
                 t += 2 * rstep * TP;
             }
         };
