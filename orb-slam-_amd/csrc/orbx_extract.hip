@@ -617,7 +617,7 @@ __host__ __device__ inline int fast_list_cap(int rw, int rh) { return (rh - 6) *
 // and stores, completed in issue order) wait for the store's round trip as well.
 constexpr int kFastObCap = 128;
 #ifndef ORBX_FAST_BACKW
-#define ORBX_FAST_BACKW 1
+#define ORBX_FAST_BACKW 2   // 1: list indices; 2: running byte address, one scalar loop counter
 #endif
 constexpr int kFastScratch = ORBX_FAST_BACKW ? 256 : 0;   // a dword per lane after obuf (pass 1's masked-off writes)
 __host__ __device__ inline size_t fast_list_bytes(int rw, int rh) { return (2 * (size_t)fast_list_cap(rw, rh) + 3) & ~(size_t)3; }
@@ -819,6 +819,7 @@ __device__ unsigned long long g_fast_prof[8];
 #endif
 
 __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint16_t* lds_u16(uint32_t a) { return (uint16_t*)(__attribute__((address_space(3))) uint16_t*)(uintptr_t)a; }
 // per lane: a if the lane's bit of the scalar mask m is set, else b -- one v_cndmask on the mask, with every
 // lane active (the compiler's form of the select is an exec-masked region)
 __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* a, uint16_t* b)
@@ -1016,12 +1017,29 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const unsigned long long va_last = colmask & rows_below(dh - r_last);
             const unsigned long long vb_last = colmask & rows_below(dh - r_last - rstep);
 #endif
+#if ORBX_FAST_BACKW == 2
+            // LDS byte address of list[lcap - nb]: a back write is one v_lshl_add from it, and its update one
+            // scalar subtract of twice the count
+            const uint32_t bend = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)(list + lcap);
+            uint32_t bptr = bend;
+            const int rlane_b = rlane + rstep;
+#endif
+#if ORBX_FAST_BACKW == 2
+            // rem = rows left: one scalar counter for the loop and the row masks
+            for (int rem = dh; rem > 0; rem -= 2 * rstep) {
+                const int r0 = dh - rem;
+                (void)r0;
+#else
             for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {
+#endif
                 const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
                 const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
 #if ORBX_FAST_ROWMASK == 2
                 const unsigned long long va = r0 == r_last ? va_last : colmask;
                 const unsigned long long vb = r0 == r_last ? vb_last : colmask;
+#elif ORBX_FAST_BACKW == 2
+                const unsigned long long va = colmask & ballot64(rlane < rem);
+                const unsigned long long vb = colmask & ballot64(rlane_b < rem);
 #else
                 const unsigned long long va = colmask & rows_below(dh - r0);
                 const unsigned long long vb = colmask & rows_below(dh - r0 - rstep);
@@ -1033,7 +1051,15 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 nf += __popcll(mfa);
                 if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
                 nf += __popcll(mfb);
-#if ORBX_FAST_BACKW
+#if ORBX_FAST_BACKW == 2
+                // back entries (a quarter of the pixels: the mask is rarely empty) written by every lane, the
+                // lanes outside the mask into their own scratch dword: an address select instead of the exec
+                // save / branch / restore (FAST's time follows its scalar instruction count)
+                bptr -= 2u * (uint32_t)__popcll(mba);
+                *lds_select(mba, lds_u16(bptr + 2u * (uint32_t)lanes_below(mba)), bscratch) = (uint16_t)t;
+                bptr -= 2u * (uint32_t)__popcll(mbb);
+                *lds_select(mbb, lds_u16(bptr + 2u * (uint32_t)lanes_below(mbb)), bscratch) = (uint16_t)(t + rstep * TP);
+#elif ORBX_FAST_BACKW
                 // back entries (a quarter of the pixels: the mask is rarely empty) written by every lane, the
                 // lanes outside the mask into their own scratch dword: an address select instead of the exec
                 // save / branch / restore (FAST's time follows its scalar instruction count)
@@ -1049,6 +1075,9 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
 #endif
                 t += 2 * rstep * TP;
             }
+#if ORBX_FAST_BACKW == 2
+            nb = (int)(bend - bptr) >> 1;
+#endif
         };
 #if ORBX_FAST_CWT
         if (dw <= 32) pass1(std::integral_constant<int, 5>{});
