@@ -733,6 +733,9 @@ struct FastCellSrc {
 #ifndef ORBX_FAST_UNAL
 #define ORBX_FAST_UNAL 1
 #endif
+#ifndef ORBX_FAST_CLAMP
+#define ORBX_FAST_CLAMP 1
+#endif
 __host__ __device__ constexpr int fast_lanes_per_row(int tp) { return ORBX_FAST_UNAL ? tp / 4 : tp / 4 + 1; }
 template <int TP>
 struct FastLaneMap {
@@ -744,7 +747,20 @@ struct FastLaneMap {
 template <int TP, int LD>
 __device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneMap<TP>& M, int u0, FastPrefetch<LD>& F)
 {
-#if ORBX_FAST_UNAL
+#if ORBX_FAST_UNAL && ORBX_FAST_CLAMP
+    // branch-free: every lane loads, its row clamped to the ROI's last and its dword to the row's last (the
+    // lanes past a row's dwords and past a pass's rows repeat a neighbour's load, which the commit stores to
+    // the same place): no exec save / branch / restore per pass
+    // (an empty cell -- the level padding's -- loads nothing: its clamps would go negative)
+    if (S.rh <= 0 || S.nd <= 0) return;   // wave-uniform
+    const __attribute__((address_space(1))) uint8_t* base = (const __attribute__((address_space(1))) uint8_t*)S.src;
+    const uint32_t kb = 4u * (uint32_t)min(M.kl, S.nd - 1);
+#pragma unroll
+    for (int u = 0; u < LD; ++u) {
+        const uint32_t row = (uint32_t)min((u0 + u) * FastLaneMap<TP>::kRPP + M.rl, S.rh - 1);
+        F.w[u] = *(const __attribute__((address_space(1))) uint32_t*)(base + (__umul24(row, (uint32_t)S.pitch) + kb));
+    }
+#elif ORBX_FAST_UNAL
     const __attribute__((address_space(1))) uint8_t* base = (const __attribute__((address_space(1))) uint8_t*)S.src;
     const bool lane_ok = M.rl < FastLaneMap<TP>::kRPP && M.kl < S.nd;
     const uint32_t o0 = (uint32_t)__mul24(u0 * FastLaneMap<TP>::kRPP + M.rl, S.pitch) + 4u * (uint32_t)M.kl;
@@ -780,7 +796,18 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const Fas
                                             const FastLaneMap<TP>& M, int u0, uint8_t* tile)
 {
     constexpr int kRPP = FastLaneMap<TP>::kRPP;
-#if ORBX_FAST_UNAL
+#if ORBX_FAST_UNAL && ORBX_FAST_CLAMP
+    if (S.rh > 0 && S.nd > 0) {   // wave-uniform (empty cells store nothing)
+        // 32-bit LDS byte addresses (a pointer offset compiles to a 64-bit multiply-add)
+        const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)tile +
+                             4u * (uint32_t)min(M.kl, S.nd - 1);
+#pragma unroll
+        for (int u = 0; u < LD; ++u) {
+            const uint32_t row = (uint32_t)min(u0 * kRPP + u * kRPP + M.rl, S.rh - 1);
+            *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(__umul24(row, (uint32_t)TP) + dst) = F.w[u];
+        }
+    }
+#elif ORBX_FAST_UNAL
     {
         const bool lane_ok = M.rl < kRPP && M.kl < S.nd;
         const int row0 = u0 * kRPP + M.rl;
