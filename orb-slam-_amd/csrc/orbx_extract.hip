@@ -893,6 +893,9 @@ __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* 
 #ifndef ORBX_FAST_ROWMASK
 #define ORBX_FAST_ROWMASK 0
 #endif
+#ifndef ORBX_FAST_BF2
+#define ORBX_FAST_BF2 1   // strength-pass stores and NMS rounds branch-free
+#endif
 #ifndef ORBX_FAST_CWT
 #define ORBX_FAST_CWT 0
 #endif
@@ -1184,10 +1187,17 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 const int sa = fast_strength<TP>(tile + ka + (3 * TP + 3));
                 // mask before any branch (an i1 live across a divergent branch is materialised in a VGPR)
                 const unsigned long long ma = ballot64(ja < n) & ballot64(sa > t_lo);
+#if ORBX_FAST_BF2
+                // both stores by every lane through address selects (the masked-off lanes into scratch)
+                *(uint8_t*)lds_select(ma, (uint16_t*)(map + ka + (TP + 1)), bscratch) = (uint8_t)sa;
+                wave_lds_sync();   // the entries are read before the compaction overwrites the list
+                *lds_select(ma, &list[back ? lcap - 1 - (n2 + lanes_below(ma)) : n2 + lanes_below(ma)], bscratch) = (uint16_t)ka;
+#else
                 const bool ina = (ja < n) & (sa > t_lo);
                 if (ina) map[ka + (TP + 1)] = (uint8_t)sa;
                 wave_lds_sync();   // the entries are read before the compaction overwrites the list
                 if (ina) list[back ? lcap - 1 - (n2 + lanes_below(ma)) : n2 + lanes_below(ma)] = (uint16_t)ka;
+#endif
                 n2 += __popcll(ma);
             }
 #endif
@@ -1205,11 +1215,18 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             keepm[0] = keepm[1] = 0;
             for (int r = 0; r < rounds; ++r) {
                 const int j = lane + (r << 6);
+#if ORBX_FAST_BF2
+                // branch-free: lanes past the entries re-test the last one, masked out of the ballot
+                const int jc = min(j, nfr + nbk - 1);
+                const int k = list[jc < nfr ? jc : lcap - 1 - (jc - nfr)];
+                const bool keep = (j < nfr + nbk) & nms_keep<TP>(map + k + (TP + 1), (uint32_t)max(th, 1));
+#else
                 bool keep = false;
                 if (j < nfr + nbk) {
                     const int k = list[j < nfr ? j : lcap - 1 - (j - nfr)];
                     keep = nms_keep<TP>(map + k + (TP + 1), (uint32_t)max(th, 1));
                 }
+#endif
                 keepm[r >> 6] |= (unsigned long long)keep << (r & 63);
                 kept_n += __popcll(ballot64(keep));
             }
