@@ -28,6 +28,8 @@ ap.add_argument("--P", type=int, default=3)
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--lstreams", type=int, default=1, help="split: 1 = quadtree, match and pyramid on one stream; "
                 "2 = match on a stream of its own")
+ap.add_argument("--lprio", type=int, default=0, help="split: priority of the latency-bound streams L, L2 "
+                "(-1 = high: the dispatcher places their workgroups first as CU space frees)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 B, P, nb = args.batch, args.P, 4
@@ -44,8 +46,12 @@ pb = torch.arange(1, B, dtype=torch.int32, device=dev)
 matcher = orbx.ORBmatcher(0.9, True)
 streams = [torch.cuda.Stream(device=dev) for _ in range(P)]
 V = streams[0]
-L = streams[1]
-L2 = streams[2] if args.lstreams > 1 and P > 2 else L
+if args.lprio:
+    L = torch.cuda.Stream(device=dev, priority=args.lprio)
+    L2 = torch.cuda.Stream(device=dev, priority=args.lprio) if args.lstreams > 1 else L
+else:
+    L = streams[1]
+    L2 = streams[2] if args.lstreams > 1 and P > 2 else L
 
 
 def imgs(i):
