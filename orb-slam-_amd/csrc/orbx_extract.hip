@@ -893,6 +893,10 @@ __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* 
 #ifndef ORBX_FAST_ROWMASK
 #define ORBX_FAST_ROWMASK 0
 #endif
+#ifndef ORBX_FAST_FRONTW
+#define ORBX_FAST_FRONTW 0   // 1: pass 1's front list by address selects as well (586 -> 606 us: every lane
+                             // stores where a few would)
+#endif
 #ifndef ORBX_FAST_BF2
 #define ORBX_FAST_BF2 1   // strength-pass stores and NMS rounds branch-free
 #endif
@@ -1053,6 +1057,8 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const uint32_t bend = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)(list + lcap);
             uint32_t bptr = bend;
             const int rlane_b = rlane + rstep;
+            const uint32_t fbeg = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)list;
+            uint32_t fptr = fbeg;
 #endif
 #if ORBX_FAST_BACKW == 2
             // rem = rows left: one scalar counter for the loop and the row masks
@@ -1077,10 +1083,19 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
                 const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
                 const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
+#if ORBX_FAST_BACKW == 2 && ORBX_FAST_FRONTW
+                // front entries (2% of the pixels, but some in most row steps) the same way, by a running
+                // byte address fptr = &list[nf]
+                *lds_select(mfa, lds_u16(fptr + 2u * (uint32_t)lanes_below(mfa)), bscratch) = (uint16_t)t;
+                fptr += 2u * (uint32_t)__popcll(mfa);
+                *lds_select(mfb, lds_u16(fptr + 2u * (uint32_t)lanes_below(mfb)), bscratch) = (uint16_t)(t + rstep * TP);
+                fptr += 2u * (uint32_t)__popcll(mfb);
+#else
                 if (__builtin_amdgcn_inverse_ballot_w64(mfa)) list[nf + lanes_below(mfa)] = (uint16_t)t;
                 nf += __popcll(mfa);
                 if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
                 nf += __popcll(mfb);
+#endif
 #if ORBX_FAST_BACKW == 2
                 // back entries (a quarter of the pixels: the mask is rarely empty) written by every lane, the
                 // lanes outside the mask into their own scratch dword: an address select instead of the exec
@@ -1107,6 +1122,9 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             }
 #if ORBX_FAST_BACKW == 2
             nb = (int)(bend - bptr) >> 1;
+#if ORBX_FAST_FRONTW
+            nf = (int)(fptr - fbeg) >> 1;
+#endif
 #endif
         };
 #if ORBX_FAST_CWT
