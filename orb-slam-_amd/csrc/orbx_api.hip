@@ -144,7 +144,6 @@ struct orbx_handle {
     uint8_t* d_pyr = nullptr;
     uint32_t* d_slots = nullptr;
     int* d_cell_counts = nullptr;
-    uint32_t* d_cell_addr = nullptr;
     uint32_t* d_spill = nullptr;
     uint32_t* d_spill_node = nullptr;
     uint8_t* d_qt_nodes = nullptr;
@@ -457,9 +456,9 @@ orbx_status ensure_batch(orbx_handle* h, int batch)
     const Geometry& g = h->geom;
     const size_t B = (size_t)batch;
     if (!dalloc(h, h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h, h->d_slots, (size_t)g.slots_per_frame * B) ||
-        !dalloc(h, h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h, h->d_cell_addr, (size_t)g.ncells * B) || !dalloc(h, h->d_spill, (size_t)g.spill_per_frame * B) ||
+        !dalloc(h, h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h, h->d_spill, (size_t)g.spill_per_frame * B) ||
         !dalloc(h, h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h, h->d_qt_out, (size_t)g.out_per_frame * B) ||
-        !dalloc(h, h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h, h->d_status, kFillOff + (size_t)g.nlevels * B) ||
+        !dalloc(h, h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h, h->d_status, 16) ||
         !dalloc(h, h->d_qt_nodes, (size_t)g.qtg_per_frame * B)) {
         h->batch_cap = 0;
         return ORBX_ENOMEM;
@@ -479,7 +478,6 @@ ExtractBufs bufs(orbx_handle* h)
     b.qpt = h->d_qpt;
     b.slots = h->d_slots;
     b.cell_counts = h->d_cell_counts;
-    b.cell_addr = h->d_cell_addr;
     b.spill = h->d_spill;
     b.spill_node = h->d_spill_node;
     b.qt_nodes = h->d_qt_nodes;
@@ -525,9 +523,12 @@ void enqueue_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoi
 {
     const Geometry& g = h->geom;
     ExtractBufs b = bufs(h);
-    // the status block: error bits, (host path) the count, FAST's fill counters
-    if (!(counts == h->d_status + 1 && batch == 1)) hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
-    hipMemsetAsync(h->d_status, 0, sizeof(int) * (kFillOff + (size_t)g.nlevels * batch), s);
+    if (counts == h->d_status + 1 && batch == 1) {   // the host path: status and count in one memset
+        hipMemsetAsync(h->d_status, 0, 2 * sizeof(int), s);
+    } else {
+        hipMemsetAsync(counts, 0, sizeof(int) * batch, s);
+        hipMemsetAsync(h->d_status, 0, sizeof(int), s);
+    }
     if (ev) hipEventRecord(ev[0], s);
     launch_pyramid(g, b, P, batch, s);
     if (ev) hipEventRecord(ev[1], s);
@@ -617,7 +618,6 @@ void orbx_destroy(orbx_handle* h)
     dfree(h->d_pyr);
     dfree(h->d_slots);
     dfree(h->d_cell_counts);
-    dfree(h->d_cell_addr);
     dfree(h->d_spill);
     dfree(h->d_spill_node);
     dfree(h->d_qt_nodes);
@@ -774,7 +774,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     };
     // Replayed as a hipGraph: one submission instead of ~17 (launch overhead is most of a 640x480 frame's
     // latency).  The graph is re-captured when any buffer or size it holds changes.
-    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_cell_addr, h->d_spill,
+    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
                                           h->d_spill_node, h->d_qt_nodes, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
                                           h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, h->d_qpt, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
@@ -904,7 +904,7 @@ orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* 
     switch (stage) {
     case 0:
         hipMemsetAsync(d_counts, 0, sizeof(int) * batch, s);
-        hipMemsetAsync(h->d_status, 0, sizeof(int) * (kFillOff + (size_t)g.nlevels * batch), s);
+        hipMemsetAsync(h->d_status, 0, sizeof(int), s);
         launch_pyramid(g, b, P, batch, s);
         break;
     case 1:
@@ -997,20 +997,26 @@ orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys
     order_after_last(h, own_stream(h));
     const Geometry& g = h->geom;
     std::vector<int> cnt(g.ncells);
-    std::vector<uint32_t> addr(g.ncells);
     std::vector<uint32_t> sl(g.slots_per_frame);
     hipMemcpyAsync(cnt.data(), h->d_cell_counts + (size_t)frame * g.ncells, sizeof(int) * g.ncells,
-                   hipMemcpyDeviceToHost, own_stream(h));
-    hipMemcpyAsync(addr.data(), h->d_cell_addr + (size_t)frame * g.ncells, sizeof(uint32_t) * g.ncells,
                    hipMemcpyDeviceToHost, own_stream(h));
     hipMemcpyAsync(sl.data(), h->d_slots + (size_t)frame * g.slots_per_frame, sizeof(uint32_t) * g.slots_per_frame,
                    hipMemcpyDeviceToHost, own_stream(h));
     if (hipStreamSynchronize(own_stream(h)) != hipSuccess) return ORBX_EDEVICE;
     const LevelGeom& L = g.lv[level];
+    // a cell's first slot: its own slot base if FAST wrote it directly (kCellDirect), else its wave's run
+    // (the wave's first cell's slot base plus the wave's earlier cells' counts; orbx_kernels.hpp)
+    const int cpw = fast_cells_per_wave(h->last_batch);
     int k = 0;
+    uint32_t run = 0;
     for (int c = L.cell_begin; c < L.cell_begin + L.ncells; ++c) {
-        for (int i = 0; i < cnt[c]; ++i) {
-            const uint32_t v = sl[addr[c] + i];
+        const uint32_t raw = (uint32_t)cnt[c];
+        const int n = (int)(raw & ~kCellDirect);
+        if ((c - L.cell_begin) % cpw == 0) run = (uint32_t)h->cells[c].slot_base;
+        const uint32_t a = (raw & kCellDirect) ? (uint32_t)h->cells[c].slot_base : run;
+        run += (raw & kCellDirect) ? 0u : (uint32_t)n;
+        for (int i = 0; i < n; ++i) {
+            const uint32_t v = sl[a + i];
             if (k < cap && xys) {
                 xys[3 * k] = (int)(v & 0xFFF);
                 xys[3 * k + 1] = (int)((v >> 12) & 0xFFF);

@@ -879,14 +879,10 @@ __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* 
 #define ORBX_FAST_SPT 1   // strength entries per lane per trip
 #endif
 // A wave's candidates go to HBM as one run from its first cell's slot region, which starts on a 128-byte line
-// (the slot regions of a wave's cells are consecutive, so the run fits).  ORBX_FAST_BUMP=1: the run taken
-// instead from a per-(frame, level) fill counter by one atomic after the wave's last cell, so each level's
-// candidates are dense: quadtree fetch 1.05x algorithmic, but FAST waits on the atomic's round trip
-// (+13-19 us per 384 frames, -0.8% frames/s).  Taking each cell's run by its own lane as soon as it is known,
-// so the return lands under the next cells: 783 against 669 us.
-#ifndef ORBX_FAST_BUMP
-#define ORBX_FAST_BUMP 0
-#endif
+// (the slot regions of a wave's cells are consecutive, so the run fits).  (Measured and removed in round 4:
+// the run taken from a per-(frame, level) fill counter by one atomic after the wave's last cell, which makes
+// each level's candidates dense -- quadtree fetch 1.05x algorithmic -- but makes every wave wait on the
+// atomic's round trip: FAST +13-19 us per 384 frames, -0.8% frames/s)
 // Row-validity masks of pass 1: 0 = a ballot of one compare per row step; 1 = scalar arithmetic per trip
 // (697.6 against 641.5 us: FAST is sensitive to its scalar instruction count), 2 = the last trip's masks
 // hoisted out of the loop, a select per trip (657.7 us)
@@ -909,8 +905,8 @@ __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* 
 template <int TP, int LD>
 __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                    const Cell* __restrict__ cells, uint32_t* __restrict__ slots,
-                                                   int* __restrict__ cell_counts, uint32_t* __restrict__ cell_addr,
-                                                   int* __restrict__ fill, int cb, int ce, int rw, int rh, int cpw)
+                                                   int* __restrict__ cell_counts, int cb, int ce, int rw, int rh,
+                                                   int cpw)
 {
     // cells [cb, ce); LDS sized from the group's largest cell ROI (rw x rh)
     extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
@@ -931,14 +927,10 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
     // lane i: the wave's cell c0 + i -- its candidate count, obuf offset (buffered cells) and the slot its
     // candidates start at.  The wave's cells (one level: the cell lists are padded to whole waves) are
-    // buffered in obuf and go to HBM together after its last cell, as one run from a 128-byte line
-    // (ORBX_FAST_BUMP above), so the quadtree's gather reads few partial lines (cell_addr says where each
-    // cell's candidates start).  A cell that does not fit obuf, and the wave's cells after it, write to their
-    // own slot regions.
-    const int lev = cells[c0].level;
-    int* lfill = fill + (size_t)f * G->nlevels + lev;
-    const int lslot = G->lv[lev].slot_begin;
-    int cnt_all = 0, c_off = -1, c_addr = 0;   // c_off >= 0: the lane's cell is buffered
+    // buffered in obuf and go to HBM together after its last cell, as one run from a 128-byte line, so the
+    // quadtree's gather reads few partial lines.  A cell that does not fit obuf, and the wave's cells after
+    // it, write to their own slot regions (flagged kCellDirect in cell_counts).
+    int cnt_all = 0, c_off = -1;   // c_off >= 0: the lane's cell is buffered
     int obn = 0;
     bool direct = false;   // wave-uniform
     // kept-pixel bitmask, one u64 per window row: aliases the tile, which is dead once every strength
@@ -1303,15 +1295,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 obn += kept_n;
             } else {   // rare: more than obuf holds
                 direct = true;
-#if ORBX_FAST_BUMP
-                int a = 0;
-                if (lane == 0) a = atomicAdd(lfill, kept_n);
-                a = lslot + __builtin_amdgcn_readfirstlane(a);
-#else
-                const int a = Cc.slot_base;
-#endif
-                if (lane == ci) c_addr = a;
-                uint32_t* dst = fslots + a;
+                uint32_t* dst = fslots + Cc.slot_base;
                 while (bits) {
                     const int jj = __builtin_ctzll(bits);
                     bits &= bits - 1;
@@ -1327,24 +1311,15 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         fp_acc[6] += 1;
 #endif
     }
-    if (obn > 0) {   // the buffered cells: one run
-#if ORBX_FAST_BUMP
-        int a = 0;
-        if (lane == 0) a = atomicAdd(lfill, obn);
-        const int base = lslot + __builtin_amdgcn_readfirstlane(a);
-#else
-        const int base = cells[c0].slot_base;   // 128-byte aligned (ensure_geometry)
-#endif
-        uint32_t* out = fslots + base;
+    if (obn > 0) {   // the buffered cells: one run from the wave's first cell's slot base (128-byte aligned)
+        uint32_t* out = fslots + cells[c0].slot_base;
         if (lane < obn) out[lane] = obuf[lane];
         if (lane + 64 < obn) out[lane + 64] = obuf[lane + 64];
         static_assert(kFastObCap <= 128, "two stores per lane");
-        if (c_off >= 0) c_addr = base + c_off;
     }
-    if (lane < c1 - c0) {
-        cell_counts[(size_t)f * G->ncells + c0 + lane] = cnt_all;
-        cell_addr[(size_t)f * G->ncells + c0 + lane] = (uint32_t)c_addr;
-    }
+    // a cell written straight to its own slots is flagged; the buffered ones' slots follow from the counts
+    if (lane < c1 - c0)
+        cell_counts[(size_t)f * G->ncells + c0 + lane] = (int)((uint32_t)cnt_all | (c_off < 0 && cnt_all > 0 ? kCellDirect : 0u));
 #ifdef ORBX_FAST_PROF
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(&g_fast_prof[k], (unsigned long long)fp_acc[k]);
@@ -1422,13 +1397,13 @@ static void fast_launch(const ExtractBufs& b, const FramePtrs& p, int cb, int ce
     const size_t smem = fast_wave_bytes(rw, rh);
     hipFuncSetAttribute((const void*)k_fast_cells<TP, LD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_fast_cells<TP, LD>), grid, dim3(64), smem, s, b.geom, p, b.cells, b.slots, b.cell_counts,
-                       b.cell_addr, b.status + kFillOff, cb, ce, rw, rh, cpw);
+                       cb, ce, rw, rh, cpw);
 }
 
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
     // small batches (the per-frame host path) are latency-bound: one cell per wave, 3x the waves
-    const int cpw = batch <= kLatencyMaxBatch ? 1 : kCellsPerWave;
+    const int cpw = fast_cells_per_wave(batch);
     // small batches: every cell in one launch sized for the largest ROI (one launch latency fewer; the
     // occupancy split only pays when the chip is full).  ORBX_FAST_ONE=0: the groups as for large batches.
     static const int one = getenv("ORBX_FAST_ONE") ? atoi(getenv("ORBX_FAST_ONE")) : 1;
@@ -1571,6 +1546,23 @@ __device__ __forceinline__ int next_pow2(int v)
     return p;
 }
 
+// The slot of cell c's first candidate, in two steps around the level's exclusive count scan: before it, the
+// word cell_slot_word (the cell's own slot base | kCellDirect for a directly written cell, else its wave's first
+// cell's slot base), after it cell_slot_fix (the run offset: the counts of the wave's cells before c).  cpw:
+// FAST's cells per wave for this batch (fast_cells_per_wave); level cell lists start at multiples of it.
+__device__ __forceinline__ uint32_t cell_slot_base(const Cell* cells, int c)
+{
+    return ((const uint32_t*)(cells + c))[4];   // Cell::slot_base (a whole-dword scalar-friendly load)
+}
+__device__ __forceinline__ uint32_t cell_slot_word(const Cell* cells, int cb, int c, uint32_t raw, int cpw)
+{
+    return (raw & kCellDirect) ? (cell_slot_base(cells, cb + c) | kCellDirect) : cell_slot_base(cells, cb + c - c % cpw);
+}
+__device__ __forceinline__ uint32_t cell_slot_fix(uint32_t w, const uint32_t* scan, int c, int cpw)
+{
+    return (w & kCellDirect) ? (w & ~kCellDirect) : w + scan[c] - scan[c - c % cpw];
+}
+
 struct QtLayout {
     size_t scan, rect, cnt, srank, npos, snode, sinfo, ccnt, cpos, vprev, vnew, skey, best, wsum, sh, kpa, total;
 };
@@ -1676,7 +1668,7 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 template <int QT_NT, int QT_KPT, bool kG>
 __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometry* __restrict__ G,
                                          const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
-                                         const int* __restrict__ cell_counts, const uint32_t* __restrict__ cell_addr,
+                                         const int* __restrict__ cell_counts,
                                          uint32_t* __restrict__ spill,
                                          uint32_t* __restrict__ spill_node, uint8_t* __restrict__ gnodes,
                                          uint32_t* __restrict__ qt_out, int* __restrict__ qt_cnt,
@@ -1729,12 +1721,19 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     uint16_t* owner = (uint16_t*)(gbase + ncl);
     const size_t gregion = kG ? 0 : Ly.wsum - Ly.rect;
     const bool gb_ok = !kG && ncl <= 65536 && (size_t)4 * ncl <= gregion;   // block-uniform
+    const int cpw = fast_cells_per_wave(gridDim.y);   // gridDim.y = the batch FAST ran on
     for (int c = tid; c < ncl; c += QT_NT) {
-        scan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
-        if (gb_ok) gbase[c] = cell_addr[(size_t)f * G->ncells + cb + c];
+        const uint32_t raw = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
+        scan[c] = raw & ~kCellDirect;
+        if (gb_ok) gbase[c] = cell_slot_word(cells, cb, c, raw, cpw);
     }
     __syncthreads();
     const int n = (int)block_scan_excl<QT_NT>(scan, ncl, wsum);
+    // the slot of cell c's first candidate without the per-cell table (the search and staged forms)
+    auto caddr = [&](int c) -> uint32_t {
+        const uint32_t raw = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
+        return cell_slot_fix(cell_slot_word(cells, cb, c, raw, cpw), scan, c, cpw);
+    };
 #ifdef ORBX_QT_PROF
     long long qt_g = qt_t0;
     QT_STAMP(4, qt_g);
@@ -1743,6 +1742,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     if (omap) {
         for (int c = tid; c < ncl; c += QT_NT) {
             const int base = (int)scan[c], cnt = (c + 1 < ncl ? (int)scan[c + 1] : n) - base;
+            gbase[c] = cell_slot_fix(gbase[c], scan, c, cpw);
             for (int j = 0; j < cnt; ++j) owner[base + j] = (uint16_t)c;
         }
         __syncthreads();
@@ -1772,7 +1772,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
             const int mid = (lo + hi + 1) >> 1;
             if ((int)scan[mid] <= i) lo = mid; else hi = mid - 1;
         }
-        return fslots[cell_addr[(size_t)f * G->ncells + cb + lo] + (i - (int)scan[lo])];
+        return fslots[caddr(lo) + (i - (int)scan[lo])];
     };
     uint32_t kp[kKpL ? 1 : QT_KPT], nd[QT_KPT];
     // register slot r's keypoint (candidate tid + r * QT_NT)
@@ -1788,7 +1788,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     if (staged) {
         for (int c = tid; c < ncl; c += QT_NT) {
             const int base = (int)scan[c], cnt = (c + 1 < ncl ? (int)scan[c + 1] : n) - base;
-            const uint32_t* src = fslots + cell_addr[(size_t)f * G->ncells + cb + c];
+            const uint32_t* src = fslots + caddr(c);
             // 8 loads in flight per batch instead of one dependent HBM round trip per candidate
             for (int j0 = 0; j0 < cnt; j0 += 8) {
                 uint32_t v[8];
@@ -2253,14 +2253,14 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
 template <int QT_NT, int QT_KPT, bool kG>
 __global__ __launch_bounds__(QT_NT, ORBX_QT_WPE(QT_NT, QT_KPT, kG)) void k_quadtree(
     int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
-    const int* __restrict__ cell_counts, const uint32_t* __restrict__ cell_addr, uint32_t* __restrict__ spill,
+    const int* __restrict__ cell_counts, uint32_t* __restrict__ spill,
     uint32_t* __restrict__ spill_node, uint8_t* __restrict__ gnodes, uint32_t* __restrict__ qt_out,
     int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap,
     int only_flagged)
 {
     // only_flagged: the path-code kernel's fallback launch, for the (frame, level)s it left (count -1)
     if (only_flagged && qt_cnt[(size_t)blockIdx.y * G->nlevels + level0 + blockIdx.x] != -1) return;
-    qt_nodes<QT_NT, QT_KPT, kG>(level0 + blockIdx.x, blockIdx.y, G, cells, slots, cell_counts, cell_addr, spill,
+    qt_nodes<QT_NT, QT_KPT, kG>(level0 + blockIdx.x, blockIdx.y, G, cells, slots, cell_counts, spill,
                                 spill_node, gnodes, qt_out, qt_cnt, frame_counts, status, lcap, cellcap);
 }
 
@@ -2400,7 +2400,7 @@ __device__ __forceinline__ uint32_t compact_even(uint32_t x)   // bits 0, 2, 4, 
 template <int NT, int KPT>
 __global__ __launch_bounds__(NT, ORBX_QP_WPE(NT)) void k_qt_paths(
     int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
-    const int* __restrict__ cell_counts, const uint32_t* __restrict__ cell_addr, const uint32_t* __restrict__ qpt,
+    const int* __restrict__ cell_counts, const uint32_t* __restrict__ qpt,
     uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_node, uint32_t* __restrict__ qt_out,
     int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap,
     int ninv, int nbins)
@@ -2452,8 +2452,9 @@ __global__ __launch_bounds__(NT, ORBX_QP_WPE(NT)) void k_qt_paths(
 
     // ---- 1. candidate counts and run starts of the level's cells; the key tables into LDS ----------
     for (int c = tid; c < ncl; c += NT) {
-        cscan[c] = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
-        cbase[c] = cell_addr[(size_t)f * G->ncells + cb + c];
+        const uint32_t raw = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
+        cscan[c] = raw & ~kCellDirect;
+        cbase[c] = cell_slot_word(cells, cb, c, raw, fast_cells_per_wave(gridDim.y));
     }
     // xkey[w], ykey[h] staged in K's high half (free until the scatter; the owner map takes the low half)
     // when they fit: the keys then cost an LDS lookup instead of an L2 round trip behind the candidate loads
@@ -2484,6 +2485,7 @@ __global__ __launch_bounds__(NT, ORBX_QP_WPE(NT)) void k_qt_paths(
     uint16_t* owner = (uint16_t*)K;   // candidate -> cell (K's low half)
     for (int c = tid; c < ncl; c += NT) {
         const int base = (int)cscan[c], cnt = (c + 1 < ncl ? (int)cscan[c + 1] : n) - base;
+        cbase[c] = cell_slot_fix(cbase[c], cscan, c, fast_cells_per_wave(gridDim.y));
         for (int j = 0; j < cnt; ++j) owner[base + j] = (uint16_t)c;
     }
     __syncthreads();
@@ -2958,7 +2960,7 @@ static void qt_launch_nodes(const Geometry& g, const ExtractBufs& b, int* frame_
     const size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap, 2, qt_kpn(NT, KPT, 0)).total;
     hipFuncSetAttribute((const void*)k_quadtree<NT, KPT, kG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_quadtree<NT, KPT, kG>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
-                       b.slots, b.cell_counts, b.cell_addr, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt,
+                       b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt,
                        frame_counts, b.status, q.lcap, q.cellcap, only_flagged);
 }
 
@@ -2980,7 +2982,7 @@ static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts
     const size_t smem = qp_layout(PNT * PKPT, q.lcap, q.cellcap, q.ninv, q.nbins).total;
     hipFuncSetAttribute((const void*)k_qt_paths<PNT, PKPT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_qt_paths<PNT, PKPT>), dim3(q.nl, batch), dim3(PNT), smem, s, q.l0, b.geom, b.cells, b.slots,
-                       b.cell_counts, b.cell_addr, b.qpt, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts,
+                       b.cell_counts, b.qpt, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts,
                        b.status, q.lcap, q.cellcap, q.ninv, q.nbins);
     bool fb = false;
     for (int l = q.l0; l < q.l0 + q.nl; ++l) fb |= !g.lv[l].qp_ok || g.lv[l].slot_cap > PNT * PKPT;

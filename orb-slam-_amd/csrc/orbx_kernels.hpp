@@ -27,14 +27,13 @@ struct ExtractBufs {
     const int4* pyr_bands;      // K1 small-batch band tables (Geometry::pg)
     uint32_t* slots;            // [B][slots_per_frame] FAST candidates
     int* cell_counts;           // [B][ncells]
-    uint32_t* cell_addr;        // [B][ncells] first slot of the cell's candidates (FAST packs a wave's cells)
     uint32_t* spill;            // [B][spill_per_frame] quadtree overflow (packed kp)
     uint32_t* spill_node;       // [B][spill_per_frame]
     uint8_t* qt_nodes;          // [B][qtg_per_frame] K3 node arrays of the levels whose list outgrows LDS
     const uint32_t* qpt;        // K3 path tables (LevelGeom::qp_*)
     uint32_t* qt_out;           // [B][out_per_frame] retained keypoints (level coords)
     int* qt_cnt;                // [B][nlevels]
-    int* status;                // device error word (bit flags), then the FAST fill counters (kFillOff)
+    int* status;                // device error word (bit flags)
 };
 
 // XCD-aware workgroup order.  The dispatcher hands flat workgroup id b to XCD b % 8;
@@ -83,9 +82,12 @@ constexpr int kLatencyMaxBatch = 8;    // batches up to this size: FAST one cell
 #define ORBX_FAST_CPW 3
 #endif
 constexpr int kCellsPerWave = ORBX_FAST_CPW;
-// The status block (ExtractBufs::status, zeroed before every extraction): [0] error bits, [1] the host
-// path's keypoint count, [kFillOff + f * nlevels + l] the slots FAST has handed out in (frame f, level l).
-constexpr int kFillOff = 16;
+// cell_counts flag: the cell's candidates start at its own slot base (it did not fit its wave's output buffer).
+// Otherwise they follow the wave's earlier cells' in one run from the slot base of the wave's first cell
+// (kCellsPerWave consecutive cells of the level above kLatencyMaxBatch frames, one cell below), so a cell's
+// first slot is that base plus the counts of the wave's cells before it (orbx_extract.hip cell_slot_word).
+constexpr uint32_t kCellDirect = 0x80000000u;
+__host__ __device__ inline int fast_cells_per_wave(int batch) { return batch <= kLatencyMaxBatch ? 1 : kCellsPerWave; }
 // Workgroup size and keypoints per thread of level l's quadtree: level 0 holds most candidates
 // (KITTI ~6,800), level 1 ~2,700, levels >= 2 a few hundred.  Measured per launch (KITTI, 192 frames):
 // fewer waves per workgroup on the small levels does not shorten them (one wave for levels 3-7:
