@@ -3359,6 +3359,43 @@ __device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t b
     acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
     return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
 }
+// The vertical taps of a sample from its four dwords (even or odd row parity)
+__device__ __forceinline__ uint32_t blur_taps(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t by)
+{
+    const bool odd = by & 1u;
+    const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
+    const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
+    const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
+    const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
+    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), w0, 1u << 15, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d1), w1, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
+    return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
+}
+// A test's two samples with their LDS reads in inline asm (ORBX_DESC_ASMRD=1).  The compiler treats the next
+// keypoint's patch DMA (in flight under BRIEF, into the raw rows) as a store that may alias any LDS read and
+// waits for it (vmcnt(0)) before the first BRIEF read it can see; reads it cannot see keep the DMA in flight.
+// The asm waits for its own reads (lgkmcnt) and orders after the transpose's stores ("memory").
+__device__ __forceinline__ void blur_pair(uint32_t C, uint32_t by0, uint32_t bx0, uint32_t by1, uint32_t bx1,
+                                          uint32_t& r0, uint32_t& r1)
+{
+    const uint32_t t0 = __umul24(bx0, 4u * (uint32_t)kTP) + C, f0 = __builtin_amdgcn_ubfe(by0, 1, 23);
+    const uint32_t t1 = __umul24(bx1, 4u * (uint32_t)kTP) + C, f1 = __builtin_amdgcn_ubfe(by1, 1, 23);
+    uint32_t a0, a1;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a0) : "v"(f0), "v"(t0));
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(f1), "v"(t1));
+    unsigned long long p0, p1, q0, q1;
+    asm volatile("ds_read2_b32 %0, %4 offset1:1\n\t"
+                 "ds_read2_b32 %1, %4 offset0:2 offset1:3\n\t"
+                 "ds_read2_b32 %2, %5 offset1:1\n\t"
+                 "ds_read2_b32 %3, %5 offset0:2 offset1:3\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(p0), "=&v"(p1), "=&v"(q0), "=&v"(q1)
+                 : "v"(a0), "v"(a1)
+                 : "memory");
+    r0 = blur_taps((uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32), by0);
+    r1 = blur_taps((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32), by1);
+}
 #endif
 
 #ifndef ORBX_DESC_WPE
@@ -3366,6 +3403,13 @@ __device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t b
 #endif
 #ifndef ORBX_DESC_DEFER
 #define ORBX_DESC_DEFER 0
+#endif
+#ifndef ORBX_DESC_STW
+#define ORBX_DESC_STW 1
+#endif
+#ifndef ORBX_DESC_ASMRD
+#define ORBX_DESC_ASMRD 0   // 1: BRIEF's LDS reads in inline asm (597.7 against 593.0 us; the compiler's vmcnt(0)
+                            // at BRIEF's start stays: it is not the LDS-alias wait this aimed at)
 #endif
 __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
                                                const uint32_t* __restrict__ qt_out,
@@ -3557,7 +3601,15 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         const int csb = sb, csp = sp;
         const LevelGeom& LG = G->lv[l];
         const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF), score = (int)(pk >> 24);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this keypoint's DMA has landed
+        // this keypoint's DMA has landed.  vmcnt counts loads and stores and retires them in issue order, and
+        // the previous keypoint's three output stores (desc dwordx2, cv::KeyPoint dwordx4 + dwordx3) were issued
+        // after this DMA: waiting down to 3 leaves their round trip in flight (ORBX_DESC_STW=0: wait for all)
+#if ORBX_DESC_STW && !ORBX_DESC_DEFER
+        if (jj > 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         wave_lds_sync();
 
 #if !ORBX_DESC_ICG
@@ -3683,8 +3735,15 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             const f2v BY = __builtin_elementwise_fma(PX, vb, PY * va) + mg;
             const f2v BX = __builtin_elementwise_fma(PX, va, -(PY * vb)) + mg;
             uint32_t t2[2];
+#if ORBX_DESC_ASMRD && !ORBX_DESC_ROW1
+            blur_pair(cblur, __float_as_uint(BY[0]), __float_as_uint(BX[0]), __float_as_uint(BY[1]), __float_as_uint(BX[1]),
+                      t2[0], t2[1]);
+            t2[0] >>= 16;
+            t2[1] >>= 16;
+#else
 #pragma unroll
             for (int e = 0; e < 2; ++e) t2[e] = blur_acc(cblur, __float_as_uint(BY[e]), __float_as_uint(BX[e])) >> 16;
+#endif
             words[wd] = __ballot(t2[0] < (t2[1] < 255u ? t2[1] : 255u));
         }
 #if ORBX_DESC_DEFER == 0
