@@ -3407,6 +3407,9 @@ __device__ __forceinline__ void blur_pair(uint32_t C, uint32_t by0, uint32_t bx0
 #ifndef ORBX_DESC_STW
 #define ORBX_DESC_STW 1
 #endif
+#ifndef ORBX_DESC_KEEPVA
+#define ORBX_DESC_KEEPVA 1
+#endif
 #ifndef ORBX_DESC_ASMRD
 #define ORBX_DESC_ASMRD 0   // 1: BRIEF's LDS reads in inline asm (597.7 against 593.0 us; the compiler's vmcnt(0)
                             // at BRIEF's start stays: it is not the LDS-alias wait this aimed at)
@@ -3485,6 +3488,11 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     };
     // raw patch rows cy-21..cy+21 from column cx-21 (48 bytes used per row); sets the
     // wave-uniform row-shift state: row r starts at byte (sb + r*sp) & 3 of its LDS row
+#if ORBX_DESC_KEEPVA
+    // the DMA's address registers kept live until the loop-top wait for it, so no later write to them makes
+    // the compiler wait for the DMA (a write-after-read on a VMEM source register) before BRIEF
+    uint32_t dma_va[3] = {0u, 0u, 0u};
+#endif
     auto fill = [&](int l, uint32_t pk, int& sb, int& sp) {
         const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF);
         const int w = G->lv[l].w, h = G->lv[l].h;
@@ -3513,6 +3521,9 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                     const uint32_t o = (uint32_t)((sb + min(row, 42) * pitch) & ~3) + 16u * (uint32_t)k;
                     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ub + o),
                                                      (__attribute__((address_space(3))) void*)(raw32 + 256 * t), 16, 0, 0);
+#if ORBX_DESC_KEEPVA
+                    dma_va[t] = o;
+#endif
                 }
             }
         } else {
@@ -3609,6 +3620,9 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#if ORBX_DESC_KEEPVA
+        asm volatile("" ::"v"(dma_va[0]), "v"(dma_va[1]), "v"(dma_va[2]));
 #endif
         wave_lds_sync();
 
