@@ -3411,8 +3411,9 @@ __device__ __forceinline__ void blur_pair(uint32_t C, uint32_t by0, uint32_t bx0
 #define ORBX_DESC_KEEPVA 1
 #endif
 #ifndef ORBX_DESC_ASMRD
-#define ORBX_DESC_ASMRD 0   // 1: BRIEF's LDS reads in inline asm (597.7 against 593.0 us; the compiler's vmcnt(0)
-                            // at BRIEF's start stays: it is not the LDS-alias wait this aimed at)
+#define ORBX_DESC_ASMRD 0   // 1: BRIEF's LDS reads and the transpose's stores in inline asm (blur_pair), so the
+                            // compiler cannot wait for the next patch's DMA before them: 585.0 -> 580.9 us
+                            // alone, no gain in the pipelined step (263.6k against 264.9k frames/s)
 #endif
 __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
                                                const uint32_t* __restrict__ qt_out,
@@ -3542,6 +3543,9 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                     for (int u = 0; u < 11; ++u) raw[(s0 + u) * kRawP + lane] = v[u];
                 }
             }
+            // (no-op at run time: every byte load above is consumed; it tells the compiler's wait-count pass so,
+            // which otherwise waits for the DMA path's loads before BRIEF reuses these registers)
+            __builtin_amdgcn_s_waitcnt(0x0F70);
         }
     };
 
@@ -3615,11 +3619,14 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         // this keypoint's DMA has landed.  vmcnt counts loads and stores and retires them in issue order, and
         // the previous keypoint's three output stores (desc dwordx2, cv::KeyPoint dwordx4 + dwordx3) were issued
         // after this DMA: waiting down to 3 leaves their round trip in flight (ORBX_DESC_STW=0: wait for all)
+        // (the builtin, not inline asm: the compiler's wait-count pass sees it, and does not wait again for
+        // loads it already covers -- an inline-asm wait is opaque to it; gfx9 simm16: vmcnt[3:0], expcnt[6:4]
+        // = 7, lgkmcnt[11:8] = 15, vmcnt[5:4] at [15:14])
 #if ORBX_DESC_STW && !ORBX_DESC_DEFER
-        if (jj > 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // (also right for jj = 0: the IC_Angle loads issued after the first keypoint's DMA were waited for)
+        __builtin_amdgcn_s_waitcnt(0x0F73);   // vmcnt(3)
 #else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0x0F70);
 #endif
 #if ORBX_DESC_KEEPVA
         asm volatile("" ::"v"(dma_va[0]), "v"(dma_va[1]), "v"(dma_va[2]));
@@ -3706,10 +3713,27 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                     *(uint16_t*)b = (uint16_t)pr;
                     *(uint32_t*)(b + 2) = pr;
                     *(uint16_t*)(b + 6) = (uint16_t)(pr >> 16);
+#elif ORBX_DESC_ASMRD
+                    (void)0;
 #else
                     rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
 #endif
                 }
+#if ORBX_DESC_ASMRD && !ORBX_DESC_ROW1
+                {   // the transpose's stores in inline asm as well: the compiler's wait-count pass would wait
+                    // for the next patch's DMA (a store to LDS it cannot tell apart) before them
+                    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(rowT + 4 * cg * kTP + rp);
+                    asm volatile("ds_write_b32 %0, %1\n\t"
+                                 "ds_write_b32 %0, %2 offset:%5\n\t"
+                                 "ds_write_b32 %0, %3 offset:%6\n\t"
+                                 "ds_write_b32 %0, %4 offset:%7"
+                                 :
+                                 : "v"(a), "v"(o[0][0] | (o[1][0] << 16)), "v"(o[0][1] | (o[1][1] << 16)),
+                                   "v"(o[0][2] | (o[1][2] << 16)), "v"(o[0][3] | (o[1][3] << 16)), "i"(4 * kTP),
+                                   "i"(8 * kTP), "i"(12 * kTP)
+                                 : "memory");
+                }
+#endif
             }
         };
         if (csp != 0) hpass(std::integral_constant<int, -1>{});
@@ -3717,6 +3741,9 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         else if (csb == 1) hpass(std::integral_constant<int, 1>{});
         else if (csb == 2) hpass(std::integral_constant<int, 2>{});
         else hpass(std::integral_constant<int, 3>{});
+#endif
+#if ORBX_DESC_ASMRD && !ORBX_DESC_ROW1
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the asm stores above are not tracked by the compiler
 #endif
         wave_lds_sync();   // raw is free: start the next keypoint's patch, it lands under BRIEF
         nvalid = lookup(jj + 1, nl, npk);
