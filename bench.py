@@ -33,6 +33,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+DEFAULT_BATCH = 768   # frames per GPU per step (tools/collect_pmc.sh and tools/sq_summary.py record the same)
+
 import orbx  # noqa: E402
 
 sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -187,9 +189,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=384, help="frames per GPU per step (measured: 128 -> 149.9k, 192 -> "
-                    "152.6k, 256 -> 154.6k, 384 -> 156.4k frames/s; fixed per-launch costs amortise)")
-    ap.add_argument("--pool", type=int, default=4, help="distinct batches resident per GPU (4 x 384 frames = 717 MB > the 256 MB Infinity Cache)")
+    ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="frames per GPU per step (round 4, K = 20: 384 -> "
+                    "249k, 512 -> 257k, 768 -> 260k frames/s: the pipeline's fill and drain weigh less; round 2, K = 100: "
+                    "128 -> 149.9k, 192 -> 152.6k, 256 -> 154.6k, 384 -> 156.4k)")
+    ap.add_argument("--pool", type=int, default=4, help="distinct batches resident per GPU (4 x 768 frames = 1.4 GB > the 256 MB Infinity Cache)")
     ap.add_argument("--streams", type=int, default=3, help="pipeline depth (batches in flight per GPU); "
                     "GPU_MAX_HW_QUEUES=4 leaves 3 besides the default stream")
     ap.add_argument("--iso-steps", type=int, default=3, help="untimed one-stream steps for roofline_isolated")

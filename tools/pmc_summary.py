@@ -36,7 +36,7 @@ def load(counter_dir, counter):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--batch", type=int, default=384)
+    ap.add_argument("--batch", type=int, default=768)
     ap.add_argument("--profiles", default=None)
     a = ap.parse_args()
     fetch = load(os.path.join(a.dir, "FETCH_SIZE"), "FETCH_SIZE")
