@@ -33,7 +33,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-DEFAULT_BATCH = 768   # frames per GPU per step (tools/collect_pmc.sh and tools/sq_summary.py record the same)
+DEFAULT_BATCH = 1024   # frames per GPU per step (tools/pmc_summary.py and tools/sq_summary.py read it from here)
 
 import orbx  # noqa: E402
 
@@ -190,9 +190,10 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="frames per GPU per step (round 4, K = 20: 384 -> "
-                    "249k, 512 -> 257k, 768 -> 260k frames/s: the pipeline's fill and drain weigh less; round 2, K = 100: "
+                    "249k, 512 -> 257k, 768 -> 261-263k, 1024 -> 263-266k, 1280 -> 265-267k frames/s: the pipeline's fill and drain "
+                    "weigh less; round 2, K = 100: "
                     "128 -> 149.9k, 192 -> 152.6k, 256 -> 154.6k, 384 -> 156.4k)")
-    ap.add_argument("--pool", type=int, default=4, help="distinct batches resident per GPU (4 x 768 frames = 1.4 GB > the 256 MB Infinity Cache)")
+    ap.add_argument("--pool", type=int, default=4, help="distinct batches resident per GPU (4 x 1024 frames = 1.9 GB > the 256 MB Infinity Cache)")
     ap.add_argument("--streams", type=int, default=3, help="pipeline depth (batches in flight per GPU); "
                     "GPU_MAX_HW_QUEUES=4 leaves 3 besides the default stream")
     ap.add_argument("--iso-steps", type=int, default=3, help="untimed one-stream steps for roofline_isolated")

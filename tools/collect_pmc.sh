@@ -11,4 +11,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
     python3 $R/bench.py --steps 5 --warmup 1 --no-cpu --host-steps 0 > $R/gpurun_out/pmc_$TAG/bench_$C.json 2> $R/gpurun_out/pmc_$TAG/bench_$C.err \
     || { echo PMC_FAIL $C; tail -20 $R/gpurun_out/pmc_$TAG/bench_$C.err; exit 1; }
 done
-python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_$TAG --batch 768 --profiles $R/gpurun_out/pmc_$TAG/pmc_traffic.json
+python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc_$TAG --profiles $R/gpurun_out/pmc_$TAG/pmc_traffic.json

@@ -36,9 +36,12 @@ def load(counter_dir, counter):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--batch", type=int, default=768)
+    ap.add_argument("--batch", type=int, default=None, help="frames per step (default: bench.py's DEFAULT_BATCH)")
     ap.add_argument("--profiles", default=None)
     a = ap.parse_args()
+    if a.batch is None:
+        from srchash import bench_default_batch
+        a.batch = bench_default_batch()
     fetch = load(os.path.join(a.dir, "FETCH_SIZE"), "FETCH_SIZE")
     write = load(os.path.join(a.dir, "WRITE_SIZE"), "WRITE_SIZE")
     out = {}

@@ -11,3 +11,6 @@ cp $S/sq.txt $D/sq_$V.txt
 cp $S/pmc_traffic.json $D/pmc_traffic_$V.json
 cp $S/pytest_gpu.log $D/pytest_gpu_$V.log
 cp $S/smoke.log $D/smoke_$V.log
+# the counter files bench.py reads (it reports their figures only for its own batch and kernel sources)
+cp $S/pmc_traffic.json profiles/pmc_traffic.json
+cp $S/sq_counters.json profiles/sq_counters.json

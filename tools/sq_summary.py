@@ -31,13 +31,13 @@ if save:
     import json
     import os
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from srchash import kernel_sources_sha256
+    from srchash import bench_default_batch, kernel_sources_sha256
     out = {}
     for k, c in vals.items():
         if k.startswith("k_"):
             out[k] = {n: sum(v) / len(v) for n, v in c.items()}
             out[k]["dispatches"] = len(next(iter(c.values())))
-    json.dump({"batch": 768, "source": "rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU "
+    json.dump({"batch": bench_default_batch(), "source": "rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU "
                "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -- python3 bench.py --steps 3 "
                "--warmup 1 --no-cpu --streams 1 --iso-steps 0 (tools/gpu_sq.sh)",
                "kernel_sources_sha256": kernel_sources_sha256(), "per_dispatch_averages": out},

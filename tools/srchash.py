@@ -6,6 +6,7 @@ timing (the GPU box has no .git, so a content hash stands in for the commit)."""
 import glob
 import hashlib
 import os
+import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -18,6 +19,13 @@ def kernel_sources_sha256(root=ROOT):
             h.update(os.path.relpath(fn, root).encode())
             h.update(open(fn, "rb").read())
     return h.hexdigest()
+
+
+def bench_default_batch(root=ROOT):
+    """bench.py's DEFAULT_BATCH (frames per GPU per step), read from its source so the counter tools
+    record the same step as the bench without importing torch."""
+    m = re.search(r"^DEFAULT_BATCH = (\d+)", open(os.path.join(root, "bench.py")).read(), re.M)
+    return int(m.group(1))
 
 
 if __name__ == "__main__":
