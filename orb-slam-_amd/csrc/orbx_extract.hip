@@ -900,6 +900,12 @@ __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* 
 #ifndef ORBX_FAST_CWT
 #define ORBX_FAST_CWT 0
 #endif
+#ifndef ORBX_FAST_PEEL
+#define ORBX_FAST_PEEL 1   // pass 1's last, partial trip peeled: no row-mask compares in the full trips
+#endif
+#if ORBX_FAST_PEEL && ORBX_FAST_BACKW != 2
+#error "ORBX_FAST_PEEL needs ORBX_FAST_BACKW=2"
+#endif
 #ifndef ORBX_FAST_P1
 #define ORBX_FAST_P1 2    // pass 1: 2 = compile-time column width, unchecked full trips; 1 = round 3's loop
 #endif
@@ -1053,7 +1059,12 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const uint32_t fbeg = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)list;
             uint32_t fptr = fbeg;
 #endif
-#if ORBX_FAST_BACKW == 2
+#if ORBX_FAST_PEEL
+            // full trips (both row steps inside the window) take the column mask alone; the last, partial
+            // trip its row masks, once (the loop body is a lambda of the two masks, inlined twice)
+            int rem = dh;
+            auto trip = [&](const unsigned long long va, const unsigned long long vb) {
+#elif ORBX_FAST_BACKW == 2
             // rem = rows left: one scalar counter for the loop and the row masks
             for (int rem = dh; rem > 0; rem -= 2 * rstep) {
                 const int r0 = dh - rem;
@@ -1063,7 +1074,8 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
 #endif
                 const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
                 const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
-#if ORBX_FAST_ROWMASK == 2
+#if ORBX_FAST_PEEL
+#elif ORBX_FAST_ROWMASK == 2
                 const unsigned long long va = r0 == r_last ? va_last : colmask;
                 const unsigned long long vb = r0 == r_last ? vb_last : colmask;
 #elif ORBX_FAST_BACKW == 2
@@ -1112,7 +1124,13 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 if (__builtin_amdgcn_inverse_ballot_w64(mbb)) list[lcap - nb + lanes_below(mbb)] = (uint16_t)(t + rstep * TP);
 #endif
                 t += 2 * rstep * TP;
+#if ORBX_FAST_PEEL
+            };
+            for (; rem >= 2 * rstep; rem -= 2 * rstep) trip(colmask, colmask);
+            if (rem > 0) trip(colmask & ballot64(rlane < rem), colmask & ballot64(rlane_b < rem));
+#else
             }
+#endif
 #if ORBX_FAST_BACKW == 2
             nb = (int)(bend - bptr) >> 1;
 #if ORBX_FAST_FRONTW
