@@ -903,6 +903,9 @@ __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* 
 #ifndef ORBX_FAST_PEEL
 #define ORBX_FAST_PEEL 1   // pass 1's last, partial trip peeled: no row-mask compares in the full trips
 #endif
+#ifndef ORBX_FAST_PEEL2
+#define ORBX_FAST_PEEL2 1   // the strength pass's last, partial trip peeled as well
+#endif
 #if ORBX_FAST_PEEL && ORBX_FAST_BACKW != 2
 #error "ORBX_FAST_PEEL needs ORBX_FAST_BACKW=2"
 #endif
@@ -1208,6 +1211,27 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
 #else
             // one entry per lane per trip: the strength's 16 ring values and their arc maxima are the
             // kernel's register peak, and only ~15% of the window gets here
+#if ORBX_FAST_PEEL2 && ORBX_FAST_BF2
+            // full trips (64 entries) without the tail clamp and its mask; the last, partial trip peeled (the
+            // 8-register prefetch only: 67 VGPRs; the 10-register ones would drop to 6 waves per SIMD)
+            if constexpr (LD < 10) {
+            auto trip = [&](const int j0, auto full_tag) {
+                constexpr bool kFull = decltype(full_tag)::value;
+                const int ja = j0 + lane;
+                const int jc = kFull ? ja : min(ja, n - 1);   // lanes past the list re-test its last entry
+                const int ka = list[back ? lcap - 1 - jc : jc];
+                const int sa = fast_strength<TP>(tile + ka + (3 * TP + 3));
+                const unsigned long long ma = kFull ? ballot64(sa > t_lo) : ballot64(ja < n) & ballot64(sa > t_lo);
+                *(uint8_t*)lds_select(ma, (uint16_t*)(map + ka + (TP + 1)), bscratch) = (uint8_t)sa;
+                wave_lds_sync();   // the entries are read before the compaction overwrites the list
+                *lds_select(ma, &list[back ? lcap - 1 - (n2 + lanes_below(ma)) : n2 + lanes_below(ma)], bscratch) = (uint16_t)ka;
+                n2 += __popcll(ma);
+            };
+            int j0 = 0;
+            for (; j0 + 64 <= n; j0 += 64) trip(j0, std::true_type{});
+            if (j0 < n) trip(j0, std::false_type{});
+            } else
+#endif
             for (int j0 = 0; j0 < n; j0 += 64) {
                 const int ja = j0 + lane;
                 // lanes past the list re-test its last entry, masked out below
