@@ -14,7 +14,13 @@ KITTI replay (already resident in HBM):
 
 Prints ONE JSON line on rank 0.  Launch:
   python bench.py [--steps K --warmup W]                       (1 GPU)
+  python bench.py --gpus N [...]                               (N GPUs: starts the ranks itself)
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Without a launcher (WORLD_SIZE unset), `--gpus N` > 1 starts
+`python -m torch.distributed.run --nproc-per-node N bench.py <same args>` as a
+child process before anything touches the GPU, relays rank 0's JSON line and
+exits with the child's status (`--dry-run` prints that command instead).  Under
+a launcher, `--gpus` must equal WORLD_SIZE.
 """
 from __future__ import annotations
 
@@ -22,6 +28,7 @@ import argparse
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
@@ -29,11 +36,81 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "orb-slam-_amd"))
 
+DEFAULT_BATCH = 1024   # frames per GPU per step (tools/pmc_summary.py and tools/sq_summary.py read it from here)
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(argv, env):
+    """Decide how this invocation runs, before any GPU call.
+
+    Returns ("run", world) to run in this process, ("error", message) for a --gpus / WORLD_SIZE mismatch,
+    or ("spawn", cmd) with the torch.distributed.run command that starts `--gpus` ranks of this script
+    with the same arguments (rendezvous on 127.0.0.1)."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=None)
+    ap.add_argument("--dry-run", action="store_true")
+    a, _ = ap.parse_known_args(argv)
+    if "WORLD_SIZE" in env:   # under torchrun (the driver's N > 1 form, or our own child)
+        world = int(env["WORLD_SIZE"])
+        if a.gpus is not None and a.gpus != world:
+            return "error", "bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world)
+        return "run", world
+    n = 1 if a.gpus is None else a.gpus
+    if n < 1:
+        return "error", "bench.py: --gpus must be >= 1"
+    if n == 1:
+        return "run", 1
+    child_args = [x for x in argv if x != "--dry-run"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + child_args
+    return "spawn", cmd
+
+
+def spawn_ranks(cmd) -> int:
+    """Run the torchrun child, relay rank 0's JSON line to stdout (everything else to stderr, line by line,
+    so a long run keeps showing progress) and return the child's exit status.  A child process, never an
+    exec: this process has not touched the GPU and never will."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL over dmabuf IPC (the host driver's only mode)
+    env["PYTHONUNBUFFERED"] = "1"
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, text=True, env=env)
+    for line in p.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            print(s, flush=True)
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    return p.wait()
+
+
+if __name__ == "__main__":
+    _mode, _what = launch_plan(sys.argv[1:], os.environ)
+    if _mode == "error":
+        print(_what, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if _mode == "spawn":
+        if "--dry-run" in sys.argv[1:]:
+            print(json.dumps({"launch": _what}), flush=True)
+            sys.exit(0)
+        import torch  # noqa: E402  (device_count does not initialise the GPU on this image)
+        _n = next(int(x.split("=")[1]) for x in _what if x.startswith("--nproc-per-node="))
+        if torch.cuda.device_count() < _n:
+            print("bench.py: --gpus %d but %d GPU(s) visible" % (_n, torch.cuda.device_count()), file=sys.stderr)
+            sys.exit(2)
+        sys.exit(spawn_ranks(_what))
+    if "--dry-run" in sys.argv[1:]:
+        print(json.dumps({"launch": None, "world_size": _what}), flush=True)
+        sys.exit(0)
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
-
-DEFAULT_BATCH = 1024   # frames per GPU per step (tools/pmc_summary.py and tools/sq_summary.py read it from here)
 
 import orbx  # noqa: E402
 
@@ -186,7 +263,9 @@ def cpu_baseline_all_cores(frames: np.ndarray, budget_s: float, threads: int = 1
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")),
+                    help="ranks (one per GPU); without a launcher, N > 1 starts them through torch.distributed.run")
+    ap.add_argument("--dry-run", action="store_true", help="print the launch plan and exit")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="frames per GPU per step (round 4, K = 20: 384 -> "
@@ -213,9 +292,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:   # launch_plan already refused this; kept for imports of main()
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     torch.cuda.set_device(local)   # before the process group, so RCCL binds this rank's GPU
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
     dev = torch.device("cuda", local)
     B = args.batch
     nb = max(1, args.pool)
@@ -521,6 +603,7 @@ def main():
         "value": round(value, 2),
         "unit": "frames/s",
         "n_gpus": world,
+        "world_size": world,
         "steps": K,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / K * 1e3, 4),
@@ -533,7 +616,9 @@ def main():
                    "frames_per_gpu_per_step": B, "batches_in_flight": P, "parallelism": "frames sharded, gather to rank 0" if world > 1
                    else "single GPU", "pairs_per_gpu_per_step": B - 1, "window": WINDOW,
                    "input": "device-resident (frames in HBM before the timed region; host-fed figure in "
-                            "value_host_fed)"},
+                            "value_host_fed)",
+                   "handback_bytes_per_rank_per_step": hands[0].payloads[0].nbytes,
+                   "handback_bytes_to_rank0_per_step": hands[0].payloads[0].nbytes * (world - 1)},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stages.items()},
         "stage_timing": "per-stage HIP events in the timed region" if elapsed_inst is None else
                         "per-stage HIP events in a second pass of the same steps (%.1f frames/s with the events)"
