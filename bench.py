@@ -535,7 +535,7 @@ def main():
         launches = {"pyramid": n_launch["pyramid"], "fast": n_launch["fast"]}.get(dom, 1)
         t_launch = st[dom] / launches * 1e-3
         achieved = alg[dom] / launches / t_launch / 1e9
-        qk = "k_qt_paths" if os.environ.get("ORBX_QT_PATHS", "0") not in ("", "0") else "k_quadtree"
+        qk = "k_quadtree"
         kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": qk + "<512,16|512,8|256,4>",
                  "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
         # stages made of several kernels: their per-launch counters add up

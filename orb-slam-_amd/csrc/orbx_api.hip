@@ -122,7 +122,6 @@ struct orbx_handle {
     int2* d_xtab = nullptr;
     int2* d_ytab = nullptr;
     int4* d_pyrbt = nullptr;   // K1 small-batch band tables
-    uint32_t* d_qpt = nullptr; // K3 path tables
     // Every size seen keeps its own immutable device tables: a size switch selects another block
     // instead of rewriting the tables that kernels of an earlier call (still queued on the caller's
     // stream) are reading.  Bounded by the number of distinct image sizes.
@@ -135,7 +134,6 @@ struct orbx_handle {
         int2* d_xtab;
         int2* d_ytab;
         int4* d_pyrbt;
-        uint32_t* d_qpt;
     };
     std::vector<GeomBlock> geom_blocks;
 
@@ -250,7 +248,6 @@ void select_geometry(orbx_handle* h, const orbx_handle::GeomBlock& b)
     h->d_xtab = b.d_xtab;
     h->d_ytab = b.d_ytab;
     h->d_pyrbt = b.d_pyrbt;
-    h->d_qpt = b.d_qpt;
     h->grows = b.rows;
     h->gcols = b.cols;
     h->geom_ok = true;
@@ -329,8 +326,6 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         const int nCols = (int)(width / 30.f), nRows = (int)(height / 30.f);
         if (nCols <= 0 || nRows <= 0) return ORBX_EINVAL;
         const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
-        L.qp_wc = wCell;
-        L.qp_hc = hCell;
         L.cell_begin = (int)cells.size();
         L.slot_begin = slot;
         for (int i = 0; i < nRows; i++) {
@@ -404,22 +399,18 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     if (!qt_prepare(g)) return ORBX_EINVAL;
     for (int l = 0; l < t.nlevels; ++l) spill += std::max(0, g.lv[l].slot_cap - qt_regcap(g, l));
     g.spill_per_frame = std::max(spill, 1);
-    std::vector<uint32_t> qpt;
-    qp_tables(g, qpt);
 
     // once per image size, into fresh buffers that nothing queued can be reading
-    orbx_handle::GeomBlock b{rows, cols, g, std::move(cells), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    orbx_handle::GeomBlock b{rows, cols, g, std::move(cells), nullptr, nullptr, nullptr, nullptr, nullptr};
     auto release = [&b] {
         dfree(b.d_geom);
         dfree(b.d_cells);
         dfree(b.d_xtab);
         dfree(b.d_ytab);
         dfree(b.d_pyrbt);
-        dfree(b.d_qpt);
     };
     if (!dalloc_exact(b.d_geom, 1) || !dalloc_exact(b.d_cells, b.cells.size()) || !dalloc_exact(b.d_xtab, xt.size()) ||
-        !dalloc_exact(b.d_ytab, yt.size()) || !dalloc_exact(b.d_pyrbt, pyrbt.size()) ||
-        !dalloc_exact(b.d_qpt, qpt.size())) {
+        !dalloc_exact(b.d_ytab, yt.size()) || !dalloc_exact(b.d_pyrbt, pyrbt.size())) {
         release();
         return ORBX_ENOMEM;
     }
@@ -439,7 +430,6 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         if (!yt.empty()) hipMemcpyAsync(b.d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice, s);
         if (!pyrbt.empty())
             hipMemcpyAsync(b.d_pyrbt, pyrbt.data(), sizeof(int4) * pyrbt.size(), hipMemcpyHostToDevice, s);
-        if (!qpt.empty()) hipMemcpyAsync(b.d_qpt, qpt.data(), sizeof(uint32_t) * qpt.size(), hipMemcpyHostToDevice, s);
         if (hipStreamSynchronize(s) != hipSuccess) {
             release();
             return ORBX_EDEVICE;
@@ -475,7 +465,6 @@ ExtractBufs bufs(orbx_handle* h)
     b.xtab = h->d_xtab;
     b.ytab = h->d_ytab;
     b.pyr_bands = h->d_pyrbt;
-    b.qpt = h->d_qpt;
     b.slots = h->d_slots;
     b.cell_counts = h->d_cell_counts;
     b.spill = h->d_spill;
@@ -613,7 +602,6 @@ void orbx_destroy(orbx_handle* h)
         dfree(b.d_xtab);
         dfree(b.d_ytab);
         dfree(b.d_pyrbt);
-        dfree(b.d_qpt);
     }
     dfree(h->d_pyr);
     dfree(h->d_slots);
@@ -750,8 +738,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     // the pinned block's device address (the same pointer under unified addressing)
     void* dpin = nullptr;
     if (hipHostGetDevicePointer(&dpin, h->h_pin, 0) != hipSuccess) dpin = nullptr;
-    static const int copyk = getenv("ORBX_HOST_COPYK") ? atoi(getenv("ORBX_HOST_COPYK")) : 1;   // 0: SDMA copies
-    const bool kcopy = copyk && dpin;
+    const bool kcopy = dpin != nullptr;   // else SDMA copies
     uint8_t* dp = (uint8_t*)dpin;
     const size_t out_b = kp_b + (size_t)ocap * 32;   // multiple of 32
     auto enqueue = [&]() {
@@ -776,7 +763,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     // latency).  The graph is re-captured when any buffer or size it holds changes.
     const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
                                           h->d_spill_node, h->d_qt_nodes, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
-                                          h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, h->d_qpt, (const void*)(uintptr_t)rows,
+                                          h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
     bool launched = false;
     if (!ev && !h->graph_failed && !getenv("ORBX_NO_GRAPH")) {
@@ -898,9 +885,11 @@ orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* 
         }
         h->sev_stage[h->sev_used] = stage;
         tev = &h->sev[(size_t)(h->sev_used++) * 2];
-        hipEventRecord(tev[0], s);
     }
-    if (stage == 0) order_after_last(h, s);   // the previous batch's describe (the caller orders the rest)
+    // the previous batch's describe and any stereo search still reading its pyramids (the caller orders
+    // the rest); before the start event, so the wait is not counted as pyramid time
+    if (stage == 0) order_after_last(h, s);
+    if (tev) hipEventRecord(tev[0], s);
     switch (stage) {
     case 0:
         hipMemsetAsync(d_counts, 0, sizeof(int) * batch, s);
@@ -1090,6 +1079,9 @@ orbx_status orbx_compute_stereo_matches(orbx_handle* left, orbx_handle* right, c
     std::memcpy(hd, desc_l, (size_t)32 * n_l);
     if (n_r > 0) std::memcpy(hd + (size_t)32 * cap, desc_r, (size_t)32 * n_r);
     if ((st = c.upload()) != ORBX_OK) return st;
+    // the two images' pyramids: written by each handle's last extraction, on whatever stream it ran
+    order_after_last(left, c.stream());
+    if (right != left) order_after_last(right, c.stream());
     // single images: frame strides 0, so frame indices 0 / 1 both address the handle's image
     FramePtrs PL = left->last, PR = right->last;
     PL.in_fstride = PL.pyr_fstride = 0;
@@ -1132,6 +1124,9 @@ orbx_status orbx_stereo_batch_device(orbx_handle* h, const orbx_keypoint* d_kps,
     launch_stereo(h->geom, h->d_geom, h->last, h->last, d_kps, d_desc, d_counts, cap, d_left, d_right, npairs, bf,
                   maxD, rband, d_u_right, d_depth, dsad, d_n_good, s);
     hipFreeAsync(dsad, s);
+    // the stereo kernels read the handle's pyramid workspace: the next extraction, which rewrites it, waits
+    // for them (s already waited for the extraction, so this event covers both)
+    mark_last(h, s);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
 

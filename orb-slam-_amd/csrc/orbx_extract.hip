@@ -16,7 +16,6 @@
 
 namespace orbx {
 
-
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -437,29 +436,15 @@ bool pyr_plan(Geometry& g, const int2* yt, std::vector<int4>& bands)
     bands.clear();
     g.pyr_ngroups = 0;
     if (g.nlevels < 2) return true;
-    if (const char* v = getenv("ORBX_PYR_FUSED"))   // A/B knob: 0 = per-level launches for every batch
+    // ORBX_PYR_FUSED=0: per-level launches for every batch (tested against the oracle,
+    // tests/test_gpu_parity.py test_pyramid_per_level_launches_small_batch)
+    if (const char* v = getenv("ORBX_PYR_FUSED"))
         if (atoi(v) == 0) return true;
-    // group starts (first computed level of each launch): ORBX_PYR_SPLIT="1,4" (A/B knob), default 1,4;
-    // band height (rows of a group's last level per block): ORBX_PYR_BAND, default 4
-    std::vector<int> st;
-    const char* env = getenv("ORBX_PYR_SPLIT");
-    if (env && *env) {
-        for (const char* p = env; *p;) {
-            char* e = nullptr;
-            const long v = strtol(p, &e, 10);
-            if (e == p) break;
-            if (v >= 1 && v < g.nlevels) st.push_back((int)v);
-            p = *e ? e + 1 : e;
-        }
-    } else {
-        st = {1, 4};   // two launches (640x480 host path: 0.147 against 0.150-0.156 ms for 1 or 3 launches)
-    }
-    st.push_back(1);
-    std::sort(st.begin(), st.end());
-    st.erase(std::unique(st.begin(), st.end()), st.end());
-    while (!st.empty() && st.back() >= g.nlevels) st.pop_back();
-    const char* benv = getenv("ORBX_PYR_BAND");
-    const int R = std::max(1, benv && *benv ? atoi(benv) : 4);
+    // group starts (first computed level of each launch): levels 1-3 from level 0, 4-7 from level 3 (640x480
+    // host path: 0.147 against 0.150-0.156 ms for 1 or 3 launches); bands of 4 rows of a group's last level
+    std::vector<int> st = {1};
+    if (4 < g.nlevels) st.push_back(4);
+    const int R = 4;
     auto lo = [&](int j, int y) { return yt[g.lv[j].ytab_off + y].x & 0xFFFF; };
     auto hi = [&](int j, int y) { return (int)((uint32_t)yt[g.lv[j].ytab_off + y].x >> 16); };
     auto lds_pitch = [&](int j, bool staged) { return staged ? ((g.lv[j].w + 30) >> 4) << 4 : ((g.lv[j].w + 15) >> 4) << 4; };
@@ -484,11 +469,7 @@ bool pyr_plan(Geometry& g, const int2* yt, std::vector<int4>& bands)
         int qmax = 0;
         for (int j = s + 1; j <= b; ++j) qmax = std::max(qmax, (g.lv[j].w + 3) >> 2);
         P.nt = qmax > 256 ? std::min(kPyrMaxNT, (qmax + 63) & ~63) : 256;
-        // A/B knobs: ORBX_PYR_NT (threads per block), ORBX_PYR_SPLITROWS=0 (no extra row chunks on
-        // narrow levels)
-        if (const char* v = getenv("ORBX_PYR_NT")) P.nt = std::min(kPyrMaxNT, std::max(64, (atoi(v) + 63) & ~63));
         P.split = 1;
-        if (const char* v = getenv("ORBX_PYR_SPLITROWS")) P.split = atoi(v) != 0;
         std::vector<int4> e(n + 1);
         for (int k = 0; k < K; ++k) {
             e[n] = make_int4(start[n][k], start[n][k + 1] - 1, start[n][k], start[n][k + 1] - 1);
@@ -548,11 +529,9 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         const int lp = ((g.lv[l - 1].w + 15 + 15) >> 4) << 4;
         const size_t smem = (size_t)srows * lp + 16;
         dim3 grid(1, (h + kPyrRows - 1) / kPyrRows, batch);
-        // a thread per 4-column group: narrow levels take fewer waves per block (ORBX_PYR_NARROW=0: always
-        // kPyrNT, A/B knob)
-        static const int narrow = getenv("ORBX_PYR_NARROW") ? atoi(getenv("ORBX_PYR_NARROW")) : 1;
+        // a thread per 4-column group: narrow levels take fewer waves per block
         const int q = (g.lv[l].w + 3) >> 2;
-        const int nt = narrow ? std::min(kPyrNT, (q + 63) & ~63) : kPyrNT;
+        const int nt = std::min(kPyrNT, (q + 63) & ~63);
         const bool al = l >= 2 || (((uintptr_t)p.in | (uintptr_t)p.in_pitch | (uintptr_t)p.in_fstride) & 3) == 0;
         if (g.lv[l].pyr_win && al)
             hipLaunchKernelGGL((k_pyramid_level<true, true>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
@@ -617,10 +596,7 @@ __host__ __device__ inline int fast_list_cap(int rw, int rh) { return (rh - 6) *
 // store inside the cell loop would make the next cell's wait for its prefetched ROI (vmcnt counts loads
 // and stores, completed in issue order) wait for the store's round trip as well.
 constexpr int kFastObCap = 128;
-#ifndef ORBX_FAST_BACKW
-#define ORBX_FAST_BACKW 2   // 1: list indices; 2: running byte address, one scalar loop counter
-#endif
-constexpr int kFastScratch = ORBX_FAST_BACKW ? 256 : 0;   // a dword per lane after obuf (pass 1's masked-off writes)
+constexpr int kFastScratch = 256;   // a dword per lane after obuf (pass 1's masked-off writes)
 __host__ __device__ inline size_t fast_list_bytes(int rw, int rh) { return (2 * (size_t)fast_list_cap(rw, rh) + 3) & ~(size_t)3; }
 __host__ __device__ inline size_t fast_wave_bytes(int rw, int rh)
 {
@@ -684,34 +660,18 @@ __device__ __forceinline__ _Float16 fast_compass_q(const uint8_t* c)
 // and since s > t already beats every n <= t, that is s > max(t, 1, n_0 .. n_7): four max3, one compare.
 // (t1 = max(t, 1), wave-uniform)
 __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c); }
-#ifndef ORBX_FAST_NMSMAX
-#define ORBX_FAST_NMSMAX 1
-#endif
 template <int TP>
 __device__ __forceinline__ bool nms_keep(const uint8_t* m, uint32_t t1)
 {
-#if ORBX_FAST_NMSMAX
     const uint32_t a = umax3(m[-TP - 1], m[-TP], m[-TP + 1]);
     const uint32_t b = umax3(m[-1], m[1], m[TP - 1]);
     const uint32_t c = umax3(m[TP], m[TP + 1], t1);
     return (uint32_t)m[0] > umax3(a, b, c);
-#else   // round 3: the per-neighbour form
-    const int t = (int)t1 == 1 ? 0 : (int)t1;   // (t >= 1 in every configuration the tests run)
-    const int s = m[0];
-    if (s <= t) return false;
-    const int sc = s - 1;
-    const int nb[8] = {m[-TP - 1], m[-TP], m[-TP + 1], m[-1], m[1], m[TP - 1], m[TP], m[TP + 1]};
-    bool keep = true;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) keep &= sc > (nb[k] > t ? nb[k] - 1 : 0);
-    return keep;
-#endif
 }
 
-// ROI bytes of one cell staged in registers, in passes of rpp whole rows: lane = rl * (nd + 1) + kl loads
-// aligned dword kl of row u * rpp + rl (nd = dwords per ROI row; the row's extra dword kl = nd only feeds
-// its neighbour), and the realigning second dword of a lane is the next lane's, read by DPP at the
-// commit, so a pass costs one register.  LD passes are prefetched (the launch's largest ROI: 8 for
+// ROI bytes of one cell staged in registers, in passes of rpp whole rows: lane = rl * nd + kl loads
+// dword kl of row u * rpp + rl (nd = dwords per ROI row) at its exact byte, so a pass costs one register.
+// LD passes are prefetched (the launch's largest ROI: 8 for
 // 38 x 39, 10 for 38 x 46 ROIs); bigger ROIs load their remainder synchronously.
 // kCellsPerWave (orbx_kernels.hpp) cells per wave: the next cell's ROI loads fly under this one's passes
 
@@ -728,16 +688,9 @@ struct FastCellSrc {
 // The lane map of the tile pitch's widest row (TP / 4 dwords + the extra one): rows per pass and the
 // lane's (row in pass, dword) are compile-time / per-kernel constants, so every pass's offsets are
 // immediates; a narrower cell leaves its lanes past its own dwords idle.
-// ORBX_FAST_UNAL=1: each lane loads its dword at the exact (unaligned) ROI byte, which gfx950 serves
-// exactly (tools/probes/glb_unaligned.hip), so the commit is a plain store: no realigning alignbyte, no DPP
-// for the neighbour dword, no extra dword per row (TP / 4 lanes per row instead of TP / 4 + 1).
-#ifndef ORBX_FAST_UNAL
-#define ORBX_FAST_UNAL 1
-#endif
-#ifndef ORBX_FAST_CLAMP
-#define ORBX_FAST_CLAMP 1
-#endif
-__host__ __device__ constexpr int fast_lanes_per_row(int tp) { return ORBX_FAST_UNAL ? tp / 4 : tp / 4 + 1; }
+// Each lane loads its dword at the exact (unaligned) ROI byte, which gfx950 serves exactly
+// (tools/probes/glb_unaligned.hip), so the commit is a plain store: TP / 4 lanes per row.
+__host__ __device__ constexpr int fast_lanes_per_row(int tp) { return tp / 4; }
 template <int TP>
 struct FastLaneMap {
     static constexpr int kND1 = fast_lanes_per_row(TP), kRPP = 64 / kND1;
@@ -748,7 +701,6 @@ struct FastLaneMap {
 template <int TP, int LD>
 __device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneMap<TP>& M, int u0, FastPrefetch<LD>& F)
 {
-#if ORBX_FAST_UNAL && ORBX_FAST_CLAMP
     // branch-free: every lane loads, its row clamped to the ROI's last and its dword to the row's last (the
     // lanes past a row's dwords and past a pass's rows repeat a neighbour's load, which the commit stores to
     // the same place): no exec save / branch / restore per pass
@@ -761,32 +713,6 @@ __device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneM
         const uint32_t row = (uint32_t)min((u0 + u) * FastLaneMap<TP>::kRPP + M.rl, S.rh - 1);
         F.w[u] = *(const __attribute__((address_space(1))) uint32_t*)(base + (__umul24(row, (uint32_t)S.pitch) + kb));
     }
-#elif ORBX_FAST_UNAL
-    const __attribute__((address_space(1))) uint8_t* base = (const __attribute__((address_space(1))) uint8_t*)S.src;
-    const bool lane_ok = M.rl < FastLaneMap<TP>::kRPP && M.kl < S.nd;
-    const uint32_t o0 = (uint32_t)__mul24(u0 * FastLaneMap<TP>::kRPP + M.rl, S.pitch) + 4u * (uint32_t)M.kl;
-    const uint32_t dsh = (uint32_t)__mul24(FastLaneMap<TP>::kRPP, S.pitch);
-#pragma unroll
-    for (int u = 0; u < LD; ++u) {
-        const int row = (u0 + u) * FastLaneMap<TP>::kRPP + M.rl;
-        if (lane_ok && row < S.rh) F.w[u] = *(const __attribute__((address_space(1))) uint32_t*)(base + o0 + (uint32_t)u * dsh);
-    }
-#else
-    // 32-bit byte offsets from the wave-uniform aligned ROI origin: scalar base + vector offset
-    // addressing, no 64-bit address arithmetic per load
-    const __attribute__((address_space(1))) uint8_t* base =
-        (const __attribute__((address_space(1))) uint8_t*)((uintptr_t)S.src & ~(uintptr_t)3);
-    const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
-    const bool lane_ok = M.rl < FastLaneMap<TP>::kRPP && M.kl <= S.nd;
-#pragma unroll
-    for (int u = 0; u < LD; ++u) {
-        const int row = (u0 + u) * FastLaneMap<TP>::kRPP + M.rl;
-        if (lane_ok && row < S.rh) {
-            const uint32_t o = ((s0 + (uint32_t)__mul24(row, S.pitch)) & ~3u) + 4u * (uint32_t)M.kl;
-            F.w[u] = *(const __attribute__((address_space(1))) uint32_t*)(base + o);
-        }
-    }
-#endif
 }
 
 // 4 pixels of ROI row r from column 4 kl: the lane's dword and its neighbour's realigned by the row's
@@ -797,7 +723,6 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const Fas
                                             const FastLaneMap<TP>& M, int u0, uint8_t* tile)
 {
     constexpr int kRPP = FastLaneMap<TP>::kRPP;
-#if ORBX_FAST_UNAL && ORBX_FAST_CLAMP
     if (S.rh > 0 && S.nd > 0) {   // wave-uniform (empty cells store nothing)
         // 32-bit LDS byte addresses (a pointer offset compiles to a 64-bit multiply-add)
         const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)tile +
@@ -808,29 +733,6 @@ __device__ __forceinline__ void fast_commit(const FastPrefetch<LD>& F, const Fas
             *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(__umul24(row, (uint32_t)TP) + dst) = F.w[u];
         }
     }
-#elif ORBX_FAST_UNAL
-    {
-        const bool lane_ok = M.rl < kRPP && M.kl < S.nd;
-        const int row0 = u0 * kRPP + M.rl;
-        uint8_t* dst = tile + row0 * TP + 4 * M.kl;
-#pragma unroll
-        for (int u = 0; u < LD; ++u)
-            if (lane_ok && row0 + u * kRPP < S.rh) *(uint32_t*)(dst + u * kRPP * TP) = F.w[u];
-    }
-#else
-    const uint32_t s0 = (uint32_t)((uintptr_t)S.src & 3);
-    const bool lane_ok = M.rl < kRPP && M.kl < S.nd;
-    const int row0 = u0 * kRPP + M.rl;
-    const uint32_t sh0 = s0 + (uint32_t)__mul24(row0, S.pitch);
-    const uint32_t dsh = (uint32_t)__mul24(kRPP, S.pitch);
-    uint8_t* dst = tile + row0 * TP + 4 * M.kl;
-#pragma unroll
-    for (int u = 0; u < LD; ++u) {
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)F.w[u], 0x130, 0xF, 0xF, false);   // wave_shl:1
-        if (lane_ok && row0 + u * kRPP < S.rh)
-            *(uint32_t*)(dst + u * kRPP * TP) = __builtin_amdgcn_alignbyte(hi, F.w[u], sh0 + (uint32_t)u * dsh);
-    }
-#endif
 }
 
 #ifdef ORBX_FAST_PROF
@@ -876,9 +778,6 @@ __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* 
 #ifndef ORBX_FAST_WPE10
 #define ORBX_FAST_WPE10 1   // 6 (80 VGPRs, 6 dwords spilled) measured 200.9 against 183.3 us
 #endif
-#ifndef ORBX_FAST_SPT
-#define ORBX_FAST_SPT 1   // strength entries per lane per trip
-#endif
 // A wave's candidates go to HBM as one run from its first cell's slot region, which starts on a 128-byte line
 // (the slot regions of a wave's cells are consecutive, so the run fits).  (Measured and removed in round 4:
 // the run taken from a per-(frame, level) fill counter by one atomic after the wave's last cell, which makes
@@ -887,31 +786,6 @@ __device__ __forceinline__ uint16_t* lds_select(unsigned long long m, uint16_t* 
 // Row-validity masks of pass 1: 0 = a ballot of one compare per row step; 1 = scalar arithmetic per trip
 // (697.6 against 641.5 us: FAST is sensitive to its scalar instruction count), 2 = the last trip's masks
 // hoisted out of the loop, a select per trip (657.7 us)
-#ifndef ORBX_FAST_ROWMASK
-#define ORBX_FAST_ROWMASK 0
-#endif
-#ifndef ORBX_FAST_FRONTW
-#define ORBX_FAST_FRONTW 0   // 1: pass 1's front list by address selects as well (586 -> 606 us: every lane
-                             // stores where a few would)
-#endif
-#ifndef ORBX_FAST_BF2
-#define ORBX_FAST_BF2 1   // strength-pass stores and NMS rounds branch-free
-#endif
-#ifndef ORBX_FAST_CWT
-#define ORBX_FAST_CWT 1   // pass 1 compiled per column width (immediate second-row offset): with the peeled trips 741.6 -> 734.0 us
-#endif
-#ifndef ORBX_FAST_PEEL
-#define ORBX_FAST_PEEL 1   // pass 1's last, partial trip peeled: no row-mask compares in the full trips
-#endif
-#ifndef ORBX_FAST_PEEL2
-#define ORBX_FAST_PEEL2 1   // the strength pass's last, partial trip peeled as well
-#endif
-#if ORBX_FAST_PEEL && ORBX_FAST_BACKW != 2
-#error "ORBX_FAST_PEEL needs ORBX_FAST_BACKW=2"
-#endif
-#ifndef ORBX_FAST_P1
-#define ORBX_FAST_P1 2    // pass 1: 2 = compile-time column width, unchecked full trips; 1 = round 3's loop
-#endif
 template <int TP, int LD>
 __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) void k_fast_cells(const Geometry* __restrict__ G, FramePtrs P,
                                                    const Cell* __restrict__ cells, uint32_t* __restrict__ slots,
@@ -931,9 +805,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     uint16_t* list = (uint16_t*)(map + fast_map_bytes(rw, rh));
     uint32_t* obuf = (uint32_t*)((uint8_t*)list + fast_list_bytes(rw, rh));
     const int lcap = fast_list_cap(rw, rh);
-#if ORBX_FAST_BACKW
     uint16_t* const bscratch = (uint16_t*)(obuf + kFastObCap + lane);
-#endif
     uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
     // lane i: the wave's cell c0 + i -- its candidate count, obuf offset (buffered cells) and the slot its
     // candidates start at.  The wave's cells (one level: the cell lists are padded to whole waves) are
@@ -1021,14 +893,11 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         // value is tile[m + 3 * TP + 3] and its map byte map[m + TP + 1], so every ring, compass and
         // neighbour access is (tile or map) + m plus a non-negative immediate offset.
         int nf = 0, nb = 0;   // front / back entries
-#if ORBX_FAST_P1 == 2
         // Exec for the list writes comes straight from the scalar masks (inverse ballot: no per-lane flag
         // in a VGPR, no VALU compare to rebuild it).  The order of entries inside a list does not matter
         // (survivors are emitted through the row bitmask), so a trip's back entries take
-        // [lcap - nb - count, lcap - nb) in lane order.  (Tried: a compile-time column width with immediate
-        // second-row offsets and unchecked full trips: 85-95 VGPRs instead of 80, 6 -> 5 waves per SIMD.)
-        // ORBX_FAST_CWT=1: the loop compiled once per column width (cw = 32 or 64), so the second row
-        // step's offset is an immediate
+        // [lcap - nb - count, lcap - nb) in lane order.  The loop is compiled once per column width
+        // (cw = 32 or 64), so the second row step's offset is an immediate.
         auto pass1 = [&](auto cw_tag) {
             constexpr int kCwShift = decltype(cw_tag)::value;
             const int cw_shift = kCwShift > 0 ? kCwShift : (dw <= 32 ? 5 : 6);
@@ -1039,21 +908,9 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             // lanes of the first k rows of a row step (whole rows of cw lanes): scalar arithmetic, no compare
             // (branch-free: a branch here splits the loop body, and the byte loads above it get re-masked)
             auto rows_below = [&](int k) -> unsigned long long {
-#if ORBX_FAST_ROWMASK
-                const int n = min(max(k, 0), rstep) << cw_shift;
-                return n >= 64 ? ~0ull : (1ull << n) - 1ull;
-#else
                 return ballot64(rlane < k);
-#endif
             };
             int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
-#if ORBX_FAST_ROWMASK == 2
-            // every trip but the last covers whole row steps: its masks are colmask; the last trip's, once
-            const int r_last = (dh - 1) / (2 * rstep) * (2 * rstep);
-            const unsigned long long va_last = colmask & rows_below(dh - r_last);
-            const unsigned long long vb_last = colmask & rows_below(dh - r_last - rstep);
-#endif
-#if ORBX_FAST_BACKW == 2
             // LDS byte address of list[lcap - nb]: a back write is one v_lshl_add from it, and its update one
             // scalar subtract of twice the count
             const uint32_t bend = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)(list + lcap);
@@ -1061,50 +918,19 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const int rlane_b = rlane + rstep;
             const uint32_t fbeg = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)list;
             uint32_t fptr = fbeg;
-#endif
-#if ORBX_FAST_PEEL
             // full trips (both row steps inside the window) take the column mask alone; the last, partial
             // trip its row masks, once (the loop body is a lambda of the two masks, inlined twice)
             int rem = dh;
             auto trip = [&](const unsigned long long va, const unsigned long long vb) {
-#elif ORBX_FAST_BACKW == 2
-            // rem = rows left: one scalar counter for the loop and the row masks
-            for (int rem = dh; rem > 0; rem -= 2 * rstep) {
-                const int r0 = dh - rem;
-                (void)r0;
-#else
-            for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {
-#endif
                 const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
                 const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
-#if ORBX_FAST_PEEL
-#elif ORBX_FAST_ROWMASK == 2
-                const unsigned long long va = r0 == r_last ? va_last : colmask;
-                const unsigned long long vb = r0 == r_last ? vb_last : colmask;
-#elif ORBX_FAST_BACKW == 2
-                const unsigned long long va = colmask & ballot64(rlane < rem);
-                const unsigned long long vb = colmask & ballot64(rlane_b < rem);
-#else
-                const unsigned long long va = colmask & rows_below(dh - r0);
-                const unsigned long long vb = colmask & rows_below(dh - r0 - rstep);
-#endif
                 const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
                 const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
                 const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
-#if ORBX_FAST_BACKW == 2 && ORBX_FAST_FRONTW
-                // front entries (2% of the pixels, but some in most row steps) the same way, by a running
-                // byte address fptr = &list[nf]
-                *lds_select(mfa, lds_u16(fptr + 2u * (uint32_t)lanes_below(mfa)), bscratch) = (uint16_t)t;
-                fptr += 2u * (uint32_t)__popcll(mfa);
-                *lds_select(mfb, lds_u16(fptr + 2u * (uint32_t)lanes_below(mfb)), bscratch) = (uint16_t)(t + rstep * TP);
-                fptr += 2u * (uint32_t)__popcll(mfb);
-#else
                 if (__builtin_amdgcn_inverse_ballot_w64(mfa)) list[nf + lanes_below(mfa)] = (uint16_t)t;
                 nf += __popcll(mfa);
                 if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
                 nf += __popcll(mfb);
-#endif
-#if ORBX_FAST_BACKW == 2
                 // back entries (a quarter of the pixels: the mask is rarely empty) written by every lane, the
                 // lanes outside the mask into their own scratch dword: an address select instead of the exec
                 // save / branch / restore (FAST's time follows its scalar instruction count)
@@ -1112,73 +938,18 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 *lds_select(mba, lds_u16(bptr + 2u * (uint32_t)lanes_below(mba)), bscratch) = (uint16_t)t;
                 bptr -= 2u * (uint32_t)__popcll(mbb);
                 *lds_select(mbb, lds_u16(bptr + 2u * (uint32_t)lanes_below(mbb)), bscratch) = (uint16_t)(t + rstep * TP);
-#elif ORBX_FAST_BACKW
-                // back entries (a quarter of the pixels: the mask is rarely empty) written by every lane, the
-                // lanes outside the mask into their own scratch dword: an address select instead of the exec
-                // save / branch / restore (FAST's time follows its scalar instruction count)
-                nb += __popcll(mba);
-                *lds_select(mba, &list[lcap - nb + lanes_below(mba)], bscratch) = (uint16_t)t;
-                nb += __popcll(mbb);
-                *lds_select(mbb, &list[lcap - nb + lanes_below(mbb)], bscratch) = (uint16_t)(t + rstep * TP);
-#else
-                nb += __popcll(mba);
-                if (__builtin_amdgcn_inverse_ballot_w64(mba)) list[lcap - nb + lanes_below(mba)] = (uint16_t)t;
-                nb += __popcll(mbb);
-                if (__builtin_amdgcn_inverse_ballot_w64(mbb)) list[lcap - nb + lanes_below(mbb)] = (uint16_t)(t + rstep * TP);
-#endif
                 t += 2 * rstep * TP;
-#if ORBX_FAST_PEEL
             };
             for (; rem >= 2 * rstep; rem -= 2 * rstep) trip(colmask, colmask);
             if (rem > 0) trip(colmask & ballot64(rlane < rem), colmask & ballot64(rlane_b < rem));
-#else
-            }
-#endif
-#if ORBX_FAST_BACKW == 2
             nb = (int)(bend - bptr) >> 1;
-#if ORBX_FAST_FRONTW
-            nf = (int)(fptr - fbeg) >> 1;
-#endif
-#endif
         };
-        if constexpr (ORBX_FAST_CWT && LD < 10) {   // (the 10-register prefetch kernels: 76 VGPRs, 6 waves per SIMD)
+        if constexpr (LD < 10) {   // (the 10-register prefetch kernels: 76 VGPRs, 6 waves per SIMD)
             if (dw <= 32) pass1(std::integral_constant<int, 5>{});
             else pass1(std::integral_constant<int, 6>{});
         } else {
             pass1(std::integral_constant<int, 0>{});
         }
-#else
-        const int cw_shift = dw <= 32 ? 5 : 6;
-        const int col = lane & ((1 << cw_shift) - 1);
-        const int rstep = 64 >> cw_shift;
-        const int rlane = lane >> cw_shift;
-        const bool col_ok = col < dw;
-        const unsigned long long colmask = ballot64(col_ok);
-        int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
-        for (int r0 = 0; r0 < dh; r0 += 2 * rstep) {
-            const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
-            const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
-            const bool oka = col_ok & (rlane < dh - r0), okb = col_ok & (rlane < dh - r0 - rstep);
-            const bool fa = oka & (qa > f_hi), ba = oka & (qa > f_lo) & !(qa > f_hi);
-            const bool fb = okb & (qb > f_hi), bb = okb & (qb > f_lo) & !(qb > f_hi);
-            // masks from the compares themselves, combined in scalar code (a ballot of an and-chain
-            // would materialise the bool in a VGPR first)
-            const unsigned long long va = colmask & ballot64(rlane < dh - r0);
-            const unsigned long long vb = colmask & ballot64(rlane < dh - r0 - rstep);
-            const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
-            const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
-            const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
-            if (fa) list[nf + lanes_below(mfa)] = (uint16_t)t;
-            nf += __popcll(mfa);
-            if (fb) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
-            nf += __popcll(mfb);
-            if (ba) list[lcap - 1 - nb - lanes_below(mba)] = (uint16_t)t;
-            nb += __popcll(mba);
-            if (bb) list[lcap - 1 - nb - lanes_below(mbb)] = (uint16_t)(t + rstep * TP);
-            nb += __popcll(mbb);
-            t += 2 * rstep * TP;
-        }
-#endif
         wave_lds_sync();
         FP_STAMP(2);
 
@@ -1187,31 +958,8 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         // place (a trip writes at or before what it has read).  Returns the compacted count.
         auto strengths = [&](int n, bool back) {
             int n2 = 0;
-#if ORBX_FAST_SPT == 2
-            for (int j0 = 0; j0 < n; j0 += 128) {   // two entries per lane per trip
-                const int ja = j0 + lane, jb = ja + 64;
-                // lanes past the list re-test its last entry, masked out below
-                const int pa = back ? lcap - 1 - min(ja, n - 1) : min(ja, n - 1);
-                const int pb = back ? lcap - 1 - min(jb, n - 1) : min(jb, n - 1);
-                const int ka = list[pa], kb = list[pb];
-                const int sa = fast_strength<TP>(tile + ka + (3 * TP + 3));
-                const int sb = fast_strength<TP>(tile + kb + (3 * TP + 3));
-                // masks before any branch (an i1 live across a divergent branch is materialised in a VGPR)
-                const unsigned long long ma = ballot64(ja < n) & ballot64(sa > t_lo);
-                const unsigned long long mb = ballot64(jb < n) & ballot64(sb > t_lo);
-                const bool ina = (ja < n) & (sa > t_lo), inb = (jb < n) & (sb > t_lo);
-                if (ina) map[ka + (TP + 1)] = (uint8_t)sa;
-                if (inb) map[kb + (TP + 1)] = (uint8_t)sb;
-                wave_lds_sync();   // both entries are read before the compaction overwrites the list
-                if (ina) list[back ? lcap - 1 - (n2 + lanes_below(ma)) : n2 + lanes_below(ma)] = (uint16_t)ka;
-                n2 += __popcll(ma);
-                if (inb) list[back ? lcap - 1 - (n2 + lanes_below(mb)) : n2 + lanes_below(mb)] = (uint16_t)kb;
-                n2 += __popcll(mb);
-            }
-#else
             // one entry per lane per trip: the strength's 16 ring values and their arc maxima are the
             // kernel's register peak, and only ~15% of the window gets here
-#if ORBX_FAST_PEEL2 && ORBX_FAST_BF2
             // full trips (64 entries) without the tail clamp and its mask; the last, partial trip peeled (the
             // 8-register prefetch only: 67 VGPRs; the 10-register ones would drop to 6 waves per SIMD)
             if constexpr (LD < 10) {
@@ -1231,7 +979,6 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             for (; j0 + 64 <= n; j0 += 64) trip(j0, std::true_type{});
             if (j0 < n) trip(j0, std::false_type{});
             } else
-#endif
             for (int j0 = 0; j0 < n; j0 += 64) {
                 const int ja = j0 + lane;
                 // lanes past the list re-test its last entry, masked out below
@@ -1240,20 +987,12 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 const int sa = fast_strength<TP>(tile + ka + (3 * TP + 3));
                 // mask before any branch (an i1 live across a divergent branch is materialised in a VGPR)
                 const unsigned long long ma = ballot64(ja < n) & ballot64(sa > t_lo);
-#if ORBX_FAST_BF2
                 // both stores by every lane through address selects (the masked-off lanes into scratch)
                 *(uint8_t*)lds_select(ma, (uint16_t*)(map + ka + (TP + 1)), bscratch) = (uint8_t)sa;
                 wave_lds_sync();   // the entries are read before the compaction overwrites the list
                 *lds_select(ma, &list[back ? lcap - 1 - (n2 + lanes_below(ma)) : n2 + lanes_below(ma)], bscratch) = (uint16_t)ka;
-#else
-                const bool ina = (ja < n) & (sa > t_lo);
-                if (ina) map[ka + (TP + 1)] = (uint8_t)sa;
-                wave_lds_sync();   // the entries are read before the compaction overwrites the list
-                if (ina) list[back ? lcap - 1 - (n2 + lanes_below(ma)) : n2 + lanes_below(ma)] = (uint16_t)ka;
-#endif
                 n2 += __popcll(ma);
             }
-#endif
             wave_lds_sync();
             return n2;
         };
@@ -1268,18 +1007,10 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             keepm[0] = keepm[1] = 0;
             for (int r = 0; r < rounds; ++r) {
                 const int j = lane + (r << 6);
-#if ORBX_FAST_BF2
                 // branch-free: lanes past the entries re-test the last one, masked out of the ballot
                 const int jc = min(j, nfr + nbk - 1);
                 const int k = list[jc < nfr ? jc : lcap - 1 - (jc - nfr)];
                 const bool keep = (j < nfr + nbk) & nms_keep<TP>(map + k + (TP + 1), (uint32_t)max(th, 1));
-#else
-                bool keep = false;
-                if (j < nfr + nbk) {
-                    const int k = list[j < nfr ? j : lcap - 1 - (j - nfr)];
-                    keep = nms_keep<TP>(map + k + (TP + 1), (uint32_t)max(th, 1));
-                }
-#endif
                 keepm[r >> 6] |= (unsigned long long)keep << (r & 63);
                 kept_n += __popcll(ballot64(keep));
             }
@@ -1448,9 +1179,8 @@ void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, in
     // small batches (the per-frame host path) are latency-bound: one cell per wave, 3x the waves
     const int cpw = fast_cells_per_wave(batch);
     // small batches: every cell in one launch sized for the largest ROI (one launch latency fewer; the
-    // occupancy split only pays when the chip is full).  ORBX_FAST_ONE=0: the groups as for large batches.
-    static const int one = getenv("ORBX_FAST_ONE") ? atoi(getenv("ORBX_FAST_ONE")) : 1;
-    if (one && batch <= kLatencyMaxBatch && g.fast_groups > 1) {
+    // occupancy split only pays when the chip is full)
+    if (batch <= kLatencyMaxBatch && g.fast_groups > 1) {
         const int rw = std::max(g.fast_rw[0], g.fast_rw[1]), rh = std::max(g.fast_rh[0], g.fast_rh[1]);
         const int rpp = 64 / fast_lanes_per_row(fast_tile_pitch(rw)), ld = (rh + rpp - 1) / rpp;
         if (fast_tile_pitch(rw) == 40) {
@@ -1593,6 +1323,8 @@ __device__ __forceinline__ int next_pow2(int v)
 // word cell_slot_word (the cell's own slot base | kCellDirect for a directly written cell, else its wave's first
 // cell's slot base), after it cell_slot_fix (the run offset: the counts of the wave's cells before c).  cpw:
 // FAST's cells per wave for this batch (fast_cells_per_wave); level cell lists start at multiples of it.
+static_assert(offsetof(Cell, slot_base) == 16 && alignof(Cell) >= 4 && sizeof(Cell) % 4 == 0,
+              "cell_slot_base reads Cell::slot_base as dword 4");
 __device__ __forceinline__ uint32_t cell_slot_base(const Cell* cells, int c)
 {
     return ((const uint32_t*)(cells + c))[4];   // Cell::slot_base (a whole-dword scalar-friendly load)
@@ -1684,9 +1416,6 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 #ifndef ORBX_QT2_WPE
 #define ORBX_QT2_WPE 5
 #endif
-#ifndef ORBX_QT3_WPE
-#define ORBX_QT3_WPE 5   // <128, 8> (ORBX_QT2_SHAPE=1)
-#endif
 // Minimum waves per SIMD (HIP's second __launch_bounds__ argument), i.e. a VGPR budget per template:
 //   <512,16> (level 0) 4: 128 VGPRs (7 dwords spilled) instead of the compiler's 172, so two workgroups
 //            share a CU and a 384-frame launch runs every frame at once: 106 -> 68 us;
@@ -1699,11 +1428,9 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 #define ORBX_QT_WPE(NT, KPT, G) ((G) ? 1                                          \
                                  : ((NT) == 512 && (KPT) == 16) ? ORBX_QT0_WPE  \
                                  : ((NT) == 512 && (KPT) == 8) ? ORBX_QT1_WPE   \
-                                 : ((NT) == 256) ? ORBX_QT2_WPE : ((NT) == 128) ? ORBX_QT3_WPE : 1)
+                                 : ((NT) == 256) ? ORBX_QT2_WPE : 1)
 //
-// The node-list form of DistributeOctTree, one workgroup per (frame l's level l), used for the levels the
-// path-code kernel (k_qt_paths) does not take: node lists in global memory (kG), keys too wide for its
-// packed sort key, and more candidates than it holds.
+// The node-list form of DistributeOctTree, one workgroup per (frame, level).
 // kG: the node arrays live in the level's global region (LevelGeom::qtg_off) instead of LDS, with 32-bit
 // node indices, for budgets whose node list outgrows a workgroup's LDS (e.g. Tracking's
 // 2 * nFeatures initialisation extractor, src/Tracking.cc:133, at 4000 features).  The algorithm and its
@@ -2298,738 +2025,21 @@ __global__ __launch_bounds__(QT_NT, ORBX_QT_WPE(QT_NT, QT_KPT, kG)) void k_quadt
     int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
     const int* __restrict__ cell_counts, uint32_t* __restrict__ spill,
     uint32_t* __restrict__ spill_node, uint8_t* __restrict__ gnodes, uint32_t* __restrict__ qt_out,
-    int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap,
-    int only_flagged)
+    int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap)
 {
-    // only_flagged: the path-code kernel's fallback launch, for the (frame, level)s it left (count -1)
-    if (only_flagged && qt_cnt[(size_t)blockIdx.y * G->nlevels + level0 + blockIdx.x] != -1) return;
     qt_nodes<QT_NT, QT_KPT, kG>(level0 + blockIdx.x, blockIdx.y, G, cells, slots, cell_counts, spill,
                                 spill_node, gnodes, qt_out, qt_cnt, frame_counts, status, lcap, cellcap);
 }
 
-// ---------------------------------------------------------------------------
-// K3 on path codes (k_qt_paths): DistributeOctTree, src/ORBextractor.cc:644-907, one workgroup per
-// (frame, level), restated in tests/test_qt_pathcode.py (which checks it against the oracle).
-//
-// Every split halves a node's x range at UL.x + ceil((UR.x - UL.x) / 2) and its y range likewise
-// (ExtractorNode::DivideNode, :569-629), independently, so a keypoint's whole path down the tree is a
-// function of its x (and root, x / hX, :679) and of its y: two per-level tables (qp_tables) give it as a
-// sort key, root and the interleaved (right, bottom) digits above the FAST score.  Sorted by that key the
-// keypoints of any node at any depth are one contiguous run, and
-//   1. sort: a counting sort on the key's top bits (LDS atomics, one per run of equal bins in consecutive
-//      lanes), then each key's rank inside its bin;
-//   2. phase 1 (:710-803) needs no rounds: with fd(i) = the first depth at which sorted keys i - 1 and i
-//      lie in different cells, the node count after round d is #{fd <= d} and the expandable count
-//      #{fd <= d} - #{max(fd(i), fd(i + 1)) <= d}, two histograms of fd settle where phase 1 stops, and
-//      the list after round D is reverse(B_D) ++ S_{D-1} ++ ... ++ S_0 (children of round D in reverse
-//      creation order, then the single-keypoint nodes of each earlier round): a rank of per-node keys;
-//   3. phase 2 (:805-874) runs on nodes as in the node-list kernel, a split's four children being the
-//      digit runs inside its key range (binary searches instead of a pass over the keypoints);
-//   4. retain (:882-906): per node the highest score, ties to the first candidate in reference order
-//      (cell row, cell column, y, x).
-// Levels the packed key cannot hold (root bits + 2 digits per depth + 8 > 32), node lists in global memory
-// and more candidates than NT * KPT run the node-list body (qt_nodes) instead.
-// ---------------------------------------------------------------------------
-struct QpLayout {
-    size_t k, x, cscan, cbase, wsum, sh, hist;
-    // inside x, once the sort is done: the node arrays, then the fd bytes (later the inverse tables)
-    size_t nst, ncnt, ndep, srank, snode, ccnt, vprev, vnew, skey, scan, scan2, zst, lkey, fdv;
-    size_t total;
-};
-
-// k: the candidates' keys (gather: owner map and key tables; then sorted in place).  x: the sort bins, then
-// the node arrays and the fd bytes / inverse tables.  ncap: candidates a workgroup holds; ninv: the largest
-// level's inverse-table entries (u32); nbins: the largest level's sort bins.
-__host__ __device__ inline QpLayout qp_layout(int ncap, int lcap, int cellcap, int ninv, int nbins)
-{
-    QpLayout L;
-    size_t q = 0;
-    auto sub = [&](size_t bytes) {
-        const size_t r = q;
-        q += (bytes + 15) & ~(size_t)15;
-        return r;
-    };
-    const size_t l4 = ((size_t)lcap + 3) & ~(size_t)3;
-    L.nst = sub(sizeof(uint16_t) * 2 * lcap);
-    L.ncnt = sub(sizeof(uint16_t) * 2 * lcap);
-    L.ndep = sub(2 * (size_t)lcap);
-    L.srank = sub(sizeof(uint16_t) * lcap);
-    L.snode = sub(sizeof(uint16_t) * lcap);
-    // child counts (u16 x 4 per node); before phase 2 the list keys (u32, padded to 4) and the run starts
-    L.ccnt = sub(std::max(sizeof(uint16_t) * 4 * lcap, sizeof(uint32_t) * (2 * l4 + 4)));
-    L.vprev = sub(sizeof(uint16_t) * lcap);
-    L.vnew = sub(sizeof(uint16_t) * lcap);
-    L.skey = sub(sizeof(uint32_t) * (lcap + 4));
-    L.scan = sub(sizeof(uint32_t) * (lcap + 1));
-    L.scan2 = sub(sizeof(uint32_t) * (lcap + 1));
-    L.lkey = L.ccnt;
-    L.zst = L.ccnt + sizeof(uint32_t) * l4;
-    L.fdv = q;
-    q += std::max((size_t)ncap + 16, 4 * (size_t)ninv + 16);
-    size_t o = 0;
-    auto take = [&](size_t bytes) {
-        const size_t r = o;
-        o += (bytes + 15) & ~(size_t)15;
-        return r;
-    };
-    L.x = take(std::max(q, sizeof(uint32_t) * (size_t)nbins));
-    L.nst += L.x;
-    L.ncnt += L.x;
-    L.ndep += L.x;
-    L.srank += L.x;
-    L.snode += L.x;
-    L.ccnt += L.x;
-    L.vprev += L.x;
-    L.vnew += L.x;
-    L.skey += L.x;
-    L.scan += L.x;
-    L.scan2 += L.x;
-    L.lkey += L.x;
-    L.zst += L.x;
-    L.fdv += L.x;
-    L.k = take(sizeof(uint32_t) * (size_t)ncap);
-    L.cscan = take(sizeof(uint32_t) * cellcap);
-    L.cbase = take(sizeof(uint32_t) * cellcap);
-    L.wsum = take(sizeof(uint32_t) * 17);
-    L.sh = take(sizeof(int) * 16);
-    L.hist = take(sizeof(uint32_t) * 32);
-    L.total = o;
-    return L;
-}
-
-// ctr[key] += 1 for every lane with key >= 0, one LDS atomic per run of equal keys in consecutive lanes;
-// returns the lane's arrival slot (the counter before its own increment).  Called by whole waves.
-__device__ __forceinline__ uint32_t wave_run_slot(uint32_t* ctr, int key)
-{
-    const int lane = threadIdx.x & 63;
-    const int prev = __builtin_amdgcn_update_dpp(-2, key, 0x138, 0xF, 0xF, false);   // wave_shr:1, lane 0 <- -2
-    const unsigned long long heads = __ballot(key != prev);
-    uint32_t base = 0;
-    if (key >= 0 && key != prev) {
-        const unsigned long long later = lane == 63 ? 0ull : heads >> (lane + 1);
-        const int len = later ? (int)__builtin_ctzll(later) + 1 : 64 - lane;
-        base = atomicAdd(&ctr[key], (uint32_t)len);
-    }
-    const unsigned long long upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-    const int head = 63 - (int)__builtin_clzll(upto);   // this lane's run head
-    base = (uint32_t)__shfl((int)base, head);
-    return base + (uint32_t)(lane - head);
-}
-
-// wave sum of a u32 (DPP row reductions, then the four rows by readlane; all lanes active)
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true);   // row_half_mirror
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true);   // row_mirror
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
-           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
-}
-
-__device__ __forceinline__ uint32_t compact_even(uint32_t x)   // bits 0, 2, 4, ... -> 0, 1, 2, ...
-{
-    x &= 0x55555555u;
-    x = (x | (x >> 1)) & 0x33333333u;
-    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
-    x = (x | (x >> 4)) & 0x00FF00FFu;
-    x = (x | (x >> 8)) & 0x0000FFFFu;
-    return x;
-}
-
-// minimum waves per SIMD by workgroup size: 1024 threads, two per CU (LDS); 256, three per CU; 64 (one wave,
-// its barriers free), five per CU
-#define ORBX_QP_WPE(NT) ((NT) >= 1024 ? 8 : (NT) >= 512 ? 4 : (NT) >= 256 ? 4 : 2)
-template <int NT, int KPT>
-__global__ __launch_bounds__(NT, ORBX_QP_WPE(NT)) void k_qt_paths(
-    int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
-    const int* __restrict__ cell_counts, const uint32_t* __restrict__ qpt,
-    uint32_t* __restrict__ spill, uint32_t* __restrict__ spill_node, uint32_t* __restrict__ qt_out,
-    int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap,
-    int ninv, int nbins)
-{
-    constexpr int NCAP = NT * KPT;
-    constexpr int NW = NT / 64;
-    constexpr uint16_t kNone = 0xFFFF;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int l = level0 + blockIdx.x, f = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const LevelGeom& LG = G->lv[l];
-    if (!LG.qp_ok) {   // level-uniform: the node-list kernel's fallback launch takes it
-        if (tid == 0) qt_cnt[(size_t)f * G->nlevels + l] = -1;
-        return;
-    }
-    const QpLayout Ly = qp_layout(NCAP, lcap, cellcap, ninv, nbins);
-    uint32_t* K = (uint32_t*)(smem + Ly.k);
-    uint32_t* bins = (uint32_t*)(smem + Ly.x);
-    uint32_t* cscan = (uint32_t*)(smem + Ly.cscan);
-    uint32_t* cbase = (uint32_t*)(smem + Ly.cbase);
-    uint32_t* wsum = (uint32_t*)(smem + Ly.wsum);
-    int* sh = (int*)(smem + Ly.sh);
-    uint32_t* hist = (uint32_t*)(smem + Ly.hist);
-    uint8_t* fdv = smem + Ly.fdv;
-    const int ncl = LG.ncells, cb = LG.cell_begin;
-    const int D = LG.qp_D, RB = LG.qp_rb, PB = RB + 2 * D;
-    const int bshift = 8 + PB - LG.qp_bb;
-    const int NB = 1 << LG.qp_bb;
-#ifdef ORBX_QT_PROF
-    unsigned long long qt_acc[16] = {};
-    long long qt_t = clock64();
-#define QP_STAMP(slot)                                             \
-    do {                                                           \
-        __syncthreads();                                           \
-        const long long t1_ = clock64();                           \
-        qt_acc[slot] += (unsigned long long)(t1_ - qt_t);          \
-        qt_t = t1_;                                                \
-    } while (0)
-#define QP_STAMP1(slot)                                            \
-    do {                                                           \
-        const long long t1_ = clock64();                           \
-        qt_acc[slot] += (unsigned long long)(t1_ - qt_t);          \
-        qt_t = t1_;                                                \
-    } while (0)
-#else
-#define QP_STAMP(slot) ((void)0)
-#define QP_STAMP1(slot) ((void)0)
-#endif
-
-    // ---- 1. candidate counts and run starts of the level's cells; the key tables into LDS ----------
-    for (int c = tid; c < ncl; c += NT) {
-        const uint32_t raw = (uint32_t)cell_counts[(size_t)f * G->ncells + cb + c];
-        cscan[c] = raw & ~kCellDirect;
-        cbase[c] = cell_slot_word(cells, cb, c, raw, fast_cells_per_wave(gridDim.y));
-    }
-    // xkey[w], ykey[h] staged in K's high half (free until the scatter; the owner map takes the low half)
-    // when they fit: the keys then cost an LDS lookup instead of an L2 round trip behind the candidate loads
-    const bool tab_lds = LG.w + LG.h <= NCAP / 2;   // block-uniform
-    const uint32_t* xk = qpt + LG.qp_xk;
-    const uint32_t* yk = qpt + LG.qp_yk;
-    if (tab_lds) {
-        uint32_t* tk = K + NCAP / 2;
-        for (int i = tid; i < LG.w + LG.h; i += NT) tk[i] = i < LG.w ? xk[i] : yk[i - LG.w];
-        xk = tk;
-        yk = tk + LG.w;
-    }
-    for (int b = tid; b < NB; b += NT) bins[b] = 0u;
-    if (tid < 32) hist[tid] = 0u;
-    __syncthreads();
-    const int n = (int)block_scan_excl<NT>(cscan, ncl, wsum);
-    QP_STAMP(0);
-    if (n > NCAP) {   // block-uniform: more candidates than this workgroup holds (the fallback launch)
-        if (tid == 0) qt_cnt[(size_t)f * G->nlevels + l] = -1;
-        return;
-    }
-    uint32_t* out = qt_out + (size_t)f * G->out_per_frame + LG.out_off;
-    if (n == 0) {   // block-uniform
-        if (tid == 0) qt_cnt[(size_t)f * G->nlevels + l] = 0;
-        return;
-    }
-    // ---- 2. gather in reference order, keys, bin counts --------------------------------------------
-    uint16_t* owner = (uint16_t*)K;   // candidate -> cell (K's low half)
-    for (int c = tid; c < ncl; c += NT) {
-        const int base = (int)cscan[c], cnt = (c + 1 < ncl ? (int)cscan[c + 1] : n) - base;
-        cbase[c] = cell_slot_fix(cbase[c], cscan, c, fast_cells_per_wave(gridDim.y));
-        for (int j = 0; j < cnt; ++j) owner[base + j] = (uint16_t)c;
-    }
-    __syncthreads();
-    const uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
-    uint32_t v[KPT];
-#pragma unroll
-    for (int r = 0; r < KPT; ++r) {
-        const int ii = min(tid + r * NT, n - 1);
-        const int c = owner[ii];
-        v[r] = fslots[cbase[c] + (uint32_t)(ii - (int)cscan[c])];
-    }
-    QP_STAMP(1);
-#pragma unroll
-    for (int r = 0; r < KPT; ++r) v[r] = xk[v[r] & 0xFFFu] | yk[(v[r] >> 12) & 0xFFFu] | (v[r] >> 24);
-    uint32_t ps[KPT];   // arrival slot in the bin; after the scan: bin start << 16 | bin size
-    const int wave_i0 = tid - lane;
-    // bin counts: one LDS atomic per run of equal bins in consecutive lanes (run heads), every slot's
-    // atomic issued before any result is used; then each lane's slot = its head's result + its offset
-    auto bin_of = [&](int r) { return tid + r * NT < n ? (int)(v[r] >> bshift) : -1; };
-#pragma unroll
-    for (int r = 0; r < KPT; ++r) {
-        if (wave_i0 + r * NT >= n) break;   // wave-uniform
-        const int bin = bin_of(r);
-        const int prev = __builtin_amdgcn_update_dpp(-2, bin, 0x138, 0xF, 0xF, false);   // wave_shr:1
-        const unsigned long long heads = __ballot(bin != prev);
-        uint32_t base = 0;
-        if (bin >= 0 && bin != prev) {
-            const unsigned long long later = lane == 63 ? 0ull : heads >> (lane + 1);
-            const int len = later ? (int)__builtin_ctzll(later) + 1 : 64 - lane;
-            base = atomicAdd(&bins[bin], (uint32_t)len);
-        }
-        ps[r] = base;
-    }
-#pragma unroll
-    for (int r = 0; r < KPT; ++r) {
-        if (wave_i0 + r * NT >= n) break;   // wave-uniform
-        const int bin = bin_of(r);
-        const int prev = __builtin_amdgcn_update_dpp(-2, bin, 0x138, 0xF, 0xF, false);
-        const unsigned long long heads = __ballot(bin != prev);
-        const unsigned long long upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-        const int head = 63 - (int)__builtin_clzll(upto);
-        ps[r] = (uint32_t)__shfl((int)ps[r], head) + (uint32_t)(lane - head);
-    }
-    __syncthreads();
-    QP_STAMP(2);
-    block_scan_excl<NT>(bins, NB, wsum);
-#pragma unroll
-    for (int r = 0; r < KPT; ++r)
-        if (tid + r * NT < n) {
-            const uint32_t bin = v[r] >> bshift;
-            const uint32_t s0 = bins[bin], e0 = (int)bin + 1 < NB ? bins[bin + 1] : (uint32_t)n;
-            K[s0 + ps[r]] = v[r];
-            ps[r] = (s0 << 16) | (e0 - s0);
-        }
-    __syncthreads();
-    QP_STAMP(3);
-    // ---- 3. each key's rank inside its bin (the run it was scattered into); the keys then move to their
-    // sorted places in K (a barrier between: every rank reads the bin as scattered) --------------------
-    // (bins are small: a lone key needs no reads; the others read their run four keys at a time)
-#pragma unroll
-    for (int r = 0; r < KPT; ++r) {
-        if (tid + r * NT < n) {
-            const uint32_t key = v[r];
-            const int s0 = (int)(ps[r] >> 16), cnt = (int)(ps[r] & 0xFFFFu);
-            int rk = 0;
-            for (int q0 = 0; q0 < cnt; q0 += 4) {
-                uint32_t u[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) u[k] = K[s0 + min(q0 + k, cnt - 1)];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) rk += (q0 + k < cnt) & (u[k] < key);
-            }
-            ps[r] = (uint32_t)(s0 + rk);
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < KPT; ++r)
-        if (tid + r * NT < n) K[ps[r]] = v[r];
-    __syncthreads();
-    QP_STAMP(4);
-    // ---- 4. phase 1 (:710-803) from the fd histograms ----------------------------------------------
-    // fd(i): the first depth at which sorted keys i - 1 and i lie in different cells (0: another root)
-    auto fd = [&](int i) -> int {
-        if (i <= 0 || i >= n) return 0;
-        const uint32_t t = (K[i - 1] ^ K[i]) >> 8;
-        const int hb = 31 - (int)__builtin_clz(t);
-        return hb >= 2 * D ? 0 : D - (hb >> 1);
-    };
-    {
-        // per-thread byte histograms of fd(i) (L) and max(fd(i), fd(i + 1)) (M), values <= 15, then
-        // widened to 16-bit pairs and summed over the wave
-        unsigned long long hl0 = 0, hl1 = 0, hm0 = 0, hm1 = 0;
-#pragma unroll
-        for (int r = 0; r < KPT; ++r) {
-            const int i = tid + r * NT;
-            if (i < n) {
-                const int a = fd(i), a1 = fd(i + 1), m = a > a1 ? a : a1;
-                fdv[i] = (uint8_t)a;
-                const unsigned long long ba = 1ull << (8 * (a & 7)), bm = 1ull << (8 * (m & 7));
-                if (a < 8) hl0 += ba; else hl1 += ba;
-                if (m < 8) hm0 += bm; else hm1 += bm;
-            }
-        }
-        if (tid == 0) fdv[n] = 0;
-        const unsigned long long hh[4] = {hl0, hl1, hm0, hm1};
-        uint32_t tot[16];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t lo = (uint32_t)hh[k], hi = (uint32_t)(hh[k] >> 32);
-            tot[4 * k + 0] = wave_sum_u32(lo & 0x00FF00FFu);          // values 0, 2 (+8k/2 ...)
-            tot[4 * k + 1] = wave_sum_u32((lo >> 8) & 0x00FF00FFu);   // values 1, 3
-            tot[4 * k + 2] = wave_sum_u32(hi & 0x00FF00FFu);          // values 4, 6
-            tot[4 * k + 3] = wave_sum_u32((hi >> 8) & 0x00FF00FFu);   // values 5, 7
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int h0 = (k >> 1) * 16 + (k & 1) * 8;   // L: 0..15, M: 16..31
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int v0 = (e >> 1) * 4 + (e & 1);   // value of the low 16 bits
-                    const uint32_t t = tot[4 * k + e];
-                    if (t & 0xFFFFu) atomicAdd(&hist[h0 + v0], t & 0xFFFFu);
-                    if (t >> 16) atomicAdd(&hist[h0 + v0 + 2], t >> 16);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    QP_STAMP(5);
-    const int N = LG.nfeat;
-    int Dp = D, ph2 = 0;
-    {
-        int cumL = (int)hist[0], cumM = (int)hist[16];
-        for (int d = 1; d <= D + 1; ++d) {   // round 1 always runs
-            const int Ld = cumL + (d <= D ? (int)hist[d] : 0), Md = cumM + (d <= D ? (int)hist[16 + d] : 0);
-            if (Ld >= N || Ld == cumL) {
-                Dp = d;
-                break;
-            }
-            if (Ld + 3 * (Ld - Md) > N) {
-                Dp = d;
-                ph2 = 1;
-                break;
-            }
-            cumL = Ld;
-            cumM = Md;
-        }
-        Dp = Dp < D ? Dp : D;   // past D every run is one keypoint: nothing changes
-    }
-    // ---- 5. the depth-Dp runs (the nodes) in key order ---------------------------------------------
-    uint32_t* zst = (uint32_t*)(smem + Ly.zst);
-    uint32_t* lkey = (uint32_t*)(smem + Ly.lkey);
-    int L = 0;
-    {
-        // thread t's positions [t * KPT, t * KPT + KPT) (n <= NT * KPT): whole dwords of fd bytes when KPT is a
-        // multiple of 4, bytes otherwise
-        constexpr int KW = (KPT + 3) / 4;
-        const int b0 = tid * KPT;
-        uint32_t fw[KW];
-        uint32_t local = 0;
-#pragma unroll
-        for (int w = 0; w < KW; ++w) {
-            if constexpr (KPT % 4 == 0) {
-                fw[w] = b0 + 4 * w < n ? ((const uint32_t*)fdv)[tid * (KPT / 4) + w] : 0xFFFFFFFFu;
-            } else {
-                fw[w] = 0xFFFFFFFFu;
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (4 * w + k < KPT && b0 + 4 * w + k < n)
-                        fw[w] = (fw[w] & ~(0xFFu << (8 * k))) | ((uint32_t)fdv[b0 + 4 * w + k] << (8 * k));
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                local += (4 * w + k < KPT) & (b0 + 4 * w + k < n) & ((int)((fw[w] >> (8 * k)) & 0xFFu) <= Dp);
-        }
-        const uint32_t inc = wave_incl_scan(local);
-        if (lane == 63) wsum[tid >> 6] = inc;
-        __syncthreads();
-        uint32_t run = inc - local, total = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t t = wsum[w];
-            run += w < (tid >> 6) ? t : 0u;
-            total += t;
-        }
-#pragma unroll
-        for (int w = 0; w < KW; ++w)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if ((4 * w + k < KPT) & (b0 + 4 * w + k < n) & ((int)((fw[w] >> (8 * k)) & 0xFFu) <= Dp))
-                    zst[run++] = (uint32_t)(b0 + 4 * w + k);
-        L = (int)total;
-        if (tid == 0) zst[L] = (uint32_t)n;
-    }
-    __syncthreads();
-    QP_STAMP(6);
-    // list keys: group Dp - b (b = the round that created the node) above the first b digits with
-    // reverse(B_b)'s directions (digit j ascending iff b - j is odd, the root like digit 1), left-aligned
-    const int L4 = (L + 3) & ~3;
-    for (int id = tid; id < L4; id += NT) {
-        uint32_t key = 0xFFFFFFFFu;   // padding: above every key
-        if (id < L) {
-            const int s = (int)zst[id], c = (int)zst[id + 1] - s;
-            int b = Dp;
-            if (c == 1) {
-                const int f0 = fdv[s], f1 = fdv[s + 1];
-                b = f0 > f1 ? f0 : f1;
-            }
-            const uint32_t path = K[s] >> 8;
-            uint32_t root = path >> (2 * D);
-            uint32_t pd = (path & ((1u << (2 * D)) - 1u)) >> (2 * (D - b));
-            if (b & 1) root ^= (1u << RB) - 1u;
-            pd ^= 0x33333333u & ((1u << (2 * b)) - 1u);
-            key = ((uint32_t)(Dp - b) << PB) | (((root << (2 * b)) | pd) << (2 * (D - b)));
-        }
-        lkey[id] = key;
-    }
-    __syncthreads();
-    uint16_t* nst0 = (uint16_t*)(smem + Ly.nst);
-    uint16_t* ncnt0 = (uint16_t*)(smem + Ly.ncnt);
-    uint8_t* ndep0 = smem + Ly.ndep;
-    uint32_t* scan = (uint32_t*)(smem + Ly.scan);
-    {
-        const uint4* k4 = (const uint4*)lkey;
-        for (int id = tid; id < L; id += NT) {
-            const uint32_t key = lkey[id];
-            int pos = 0;
-            for (int j = 0; j < L4 / 4; ++j) {
-                const uint4 u = k4[j];
-                pos += (int)(u.x < key) + (int)(u.y < key) + (int)(u.z < key) + (int)(u.w < key);
-            }
-            const int s = (int)zst[id], c = (int)zst[id + 1] - s;
-            nst0[pos] = (uint16_t)s;
-            ncnt0[pos] = (uint16_t)c;
-            ndep0[pos] = (uint8_t)Dp;
-            scan[pos] = (key >> PB) == 0 && c > 1 ? 1u : 0u;   // phase 2's first vPrev (group 0, expandable)
-        }
-    }
-    __syncthreads();
-    // the inverse tables (path digits -> cell column << 12 | x, cell row << 12 | y) into LDS over the fd
-    // bytes by LDS-DMA (global_load_lds_dword: lane i of a wave instruction lands at dst + 4 i), so they
-    // arrive under phase 2; retain waits for them
-    const int nxi = LG.nIni << D, nyi = 1 << D;
-    uint32_t* inv = (uint32_t*)fdv;
-    for (int b = (tid >> 6) * 64; b < nxi + nyi; b += NT) {   // wave-uniform
-        const int i = b + lane;
-        if (i < nxi + nyi) {
-            const uint32_t* src = qpt + (i < nxi ? LG.qp_xi + i : LG.qp_yi + (i - nxi));
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                             (__attribute__((address_space(3))) void*)(inv + b), 4, 0, 0);
-        }
-    }
-    QP_STAMP(7);
-    // ---- 6. phase 2 on nodes (:805-874) -------------------------------------------------------------
-    // (Measured and not kept: the whole phase by one wave with wave-level ordering instead of block
-    // barriers: level 0 75 against 63 us, the ranking of ~200 candidates serialised on 64 lanes.)
-    int cur = 0;
-    bool ok = true;
-    if (ph2) {   // block-uniform
-        uint16_t* vprev = (uint16_t*)(smem + Ly.vprev);
-        uint16_t* vnew = (uint16_t*)(smem + Ly.vnew);
-        uint16_t* srank = (uint16_t*)(smem + Ly.srank);
-        uint16_t* snode = (uint16_t*)(smem + Ly.snode);
-        uint16_t* ccnt = (uint16_t*)(smem + Ly.ccnt);
-        uint32_t* skey = (uint32_t*)(smem + Ly.skey);
-        uint32_t* scan2 = (uint32_t*)(smem + Ly.scan2);
-        // vPrev in creation order = group 0's expandable nodes in descending list position
-        const uint32_t m0 = block_scan_fn<NT>(scan2, L, wsum, [&](int p) { return scan[p]; });
-        for (int p = tid; p < L; p += NT)
-            if (scan[p]) vprev[m0 - 1 - scan2[p]] = (uint16_t)p;
-        if (tid == 0) {
-            sh[SH_L] = L;
-            sh[SH_M] = (int)m0;
-            sh[SH_DONE] = 0;
-            sh[SH_ERR] = 0;
-        }
-        QP_STAMP(15);
-        while (true) {
-            __syncthreads();
-            if (sh[SH_DONE]) break;
-            const int Lc = sh[SH_L];
-            const int m = sh[SH_M];
-            uint16_t* stc = (uint16_t*)(smem + Ly.nst) + (size_t)cur * lcap;
-            uint16_t* stn = (uint16_t*)(smem + Ly.nst) + (size_t)(cur ^ 1) * lcap;
-            uint16_t* cntc = (uint16_t*)(smem + Ly.ncnt) + (size_t)cur * lcap;
-            uint16_t* cntn = (uint16_t*)(smem + Ly.ncnt) + (size_t)(cur ^ 1) * lcap;
-            uint8_t* dpc = smem + Ly.ndep + (size_t)cur * lcap;
-            uint8_t* dpn = smem + Ly.ndep + (size_t)(cur ^ 1) * lcap;
-            const uint16_t* vin = cur ? vnew : vprev;
-            uint16_t* vout = cur ? vprev : vnew;
-            // A: vPrev ranked by (size, creation) descending (unique keys: one barrier); the ranking thread
-            // also finds the candidate's four child runs (digit dp + 1 inside its key range)
-            const int m4 = (m + 3) >> 2;
-            for (int k = tid; k < 4 * m4; k += NT) skey[k] = k < m ? ((uint32_t)cntc[vin[k]] << 16) | (uint32_t)k : 0u;
-            for (int p = tid; p < Lc; p += NT) srank[p] = kNone;
-            if (tid == 0) sh[SH_KK] = m;
-            __syncthreads();
-            {
-                const uint4* k4 = (const uint4*)skey;
-                for (int k = tid; k < m; k += NT) {
-                    const uint32_t key = skey[k];
-                    int j = 0;
-                    for (int i4 = 0; i4 < m4; ++i4) {
-                        const uint4 u = k4[i4];
-                        j += (int)(u.x > key) + (int)(u.y > key) + (int)(u.z > key) + (int)(u.w > key);
-                    }
-                    const int p = vin[k];
-                    srank[p] = (uint16_t)j;
-                    snode[j] = (uint16_t)p;
-                    const int s0 = (int)stc[p], c = (int)cntc[p];
-                    const int sd = 8 + 2 * (D - (dpc[p] + 1));   // the child digit's bit position
-                    int lo = s0;
-                    for (int q = 0; q < 3; ++q) {   // first key with digit > q
-                        int a = lo, e = s0 + c;
-                        while (a < e) {
-                            const int mid = (a + e) >> 1;
-                            if ((int)((K[mid] >> sd) & 3u) <= q) a = mid + 1; else e = mid;
-                        }
-                        ccnt[4 * p + q] = (uint16_t)(a - lo);
-                        lo = a;
-                    }
-                    ccnt[4 * p + 3] = (uint16_t)(s0 + c - lo);
-                }
-            }
-            __syncthreads();
-            QP_STAMP(12);
-            // C: children (low half) and expandable children (high half) per split rank
-            const int S = m;
-            auto kids = [&](int sr) -> uint32_t {
-                const int p = snode[sr];
-                uint32_t v2 = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t c = ccnt[4 * p + q];
-                    v2 += (c > 0 ? 1u : 0u) + (c > 1 ? 0x10000u : 0u);
-                }
-                return v2;
-            };
-            const uint32_t T = block_scan_fn<NT>(scan, S, wsum, kids);
-            // how many candidates are split: the size after splitting j grows with j (a split node leaves
-            // >= 1 child), so the one j that crosses N writes (:843-845)
-            for (int j = tid; j < S; j += NT) {
-                const int cs = (int)(kids(j) & 0xFFFFu), sj = (int)(scan[j] & 0xFFFFu);
-                if (Lc + sj + cs - (j + 1) >= N && Lc + sj - j < N) sh[SH_KK] = j + 1;
-            }
-            __syncthreads();
-            const int kk = sh[SH_KK];
-            const uint32_t pre = kk < S ? scan[kk] : T;
-            block_scan_fn<NT>(scan2, Lc, wsum, [&](int p) {
-                return (srank[p] != kNone && (int)srank[p] < kk) ? 1u : 0u;
-            });
-            const int Ctot = (int)(pre & 0xFFFFu), nexp = (int)(pre >> 16);
-            const int newL = Ctot + (Lc - kk);
-            QP_STAMP(13);
-            if (newL > lcap) {
-                if (tid == 0) {
-                    sh[SH_ERR] |= kStatusListOverflow;
-                    sh[SH_DONE] = 1;
-                }
-                continue;
-            }
-            // D: the new list: children of split rank s at Ctot - prefix(s) - children(s) (later splits in
-            // front, n4..n1), the rest after them in order; expandable children in creation order
-            for (int sr = tid; sr < kk; sr += NT) {
-                const int p = snode[sr];
-                const uint32_t pss = scan[sr];
-                uint32_t c4[4];
-                int cs = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    c4[q] = ccnt[4 * p + q];
-                    cs += c4[q] > 0;
-                }
-                const int pos0 = Ctot - (int)(pss & 0xFFFFu) - cs;
-                int e = (int)(pss >> 16);
-                int np = pos0 + cs;   // n1 lands last (it was pushed first)
-                uint32_t st = stc[p];
-                const uint8_t dch = (uint8_t)(dpc[p] + 1);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t c = c4[q];
-                    if (c == 0) continue;
-                    --np;
-                    stn[np] = (uint16_t)st;
-                    cntn[np] = (uint16_t)c;
-                    dpn[np] = dch;
-                    st += c;
-                    if (c > 1) vout[e++] = (uint16_t)np;   // creation order: split rank, then n1..n4
-                }
-            }
-            for (int p = tid; p < Lc; p += NT) {
-                const bool split = srank[p] != kNone && (int)srank[p] < kk;
-                if (!split) {
-                    const int np = Ctot + p - (int)scan2[p];
-                    stn[np] = stc[p];
-                    cntn[np] = cntc[p];
-                    dpn[np] = dpc[p];
-                }
-            }
-            if (tid == 0) {
-                sh[SH_L] = newL;
-                if (newL >= N || newL == Lc) sh[SH_DONE] = 1;
-                sh[SH_M] = nexp;
-            }
-            __syncthreads();
-            QP_STAMP(14);
-            cur ^= 1;
-#ifdef ORBX_QT_PROF
-            qt_acc[10] += 1;
-#endif
-        }
-        __syncthreads();
-        L = sh[SH_L];
-        ok = sh[SH_ERR] == 0;
-    }
-    QP_STAMP(9);
-    // ---- 7. retain the best keypoint per node (:882-906) ----------------------------------------------
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the inverse tables' DMA
-    __syncthreads();
-    const uint16_t* stf = (const uint16_t*)(smem + Ly.nst) + (size_t)cur * lcap;
-    const uint16_t* cntf = (const uint16_t*)(smem + Ly.ncnt) + (size_t)cur * lcap;
-    const int outn = ok ? (L < LG.cap ? L : LG.cap) : 0;
-    const uint32_t dmask = (1u << (2 * D)) - 1u;
-    for (int p = tid; p < outn; p += NT) {
-        const int s = (int)stf[p], c = (int)cntf[p];
-        uint32_t ms = 0;
-#pragma unroll 8
-        for (int j = 0; j < c; ++j) ms = max(ms, K[s + j] & 0xFFu);
-        // among the keys at the highest score, the first in reference order: cell row, cell column
-        // (src/ORBextractor.cc:952-1000), then cv::FAST's row-major order inside the cell
-        unsigned long long bo = ~0ull;
-        for (int j0 = 0; j0 < c; j0 += 8) {   // eight loads in flight, then the (rare) ties decoded
-            uint32_t kk[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) kk[k] = K[s + min(j0 + k, c - 1)];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                if (j0 + k >= c || (kk[k] & 0xFFu) != ms) continue;
-                const uint32_t path = kk[k] >> 8, dg = path & dmask;
-                const uint32_t xv = inv[((path >> (2 * D)) << D) | compact_even(dg)];
-                const uint32_t yv = inv[nxi + compact_even(dg >> 1)];
-                const unsigned long long o = ((unsigned long long)(yv >> 12) << 40) |
-                                             ((unsigned long long)(xv >> 12) << 24) |
-                                             ((unsigned long long)(yv & 0xFFFu) << 12) | (xv & 0xFFFu);
-                bo = o < bo ? o : bo;
-            }
-        }
-        out[p] = pack_kp((uint32_t)(bo & 0xFFFu) + kMinBorder, (uint32_t)((bo >> 12) & 0xFFFu) + kMinBorder, ms);
-    }
-    QP_STAMP(11);
-    if (tid == 0) {
-#ifdef ORBX_QT_PROF
-        qt_acc[8] = 1;
-        for (int q = 0; q < 16; ++q) atomicAdd(&g_qt_prof[l][q], qt_acc[q]);
-#endif
-        qt_cnt[(size_t)f * G->nlevels + l] = outn;
-        atomicAdd(&frame_counts[f], outn);
-        int err = ok ? 0 : kStatusListOverflow;
-        if (ok && L > LG.cap) err |= kStatusOutOverflow;
-        if (err) atomicOr(status, err);
-    }
-#undef QP_STAMP
-#undef QP_STAMP1
-}
-
 template <int NT, int KPT, bool kG>
-static void qt_launch_nodes(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
-                            hipStream_t s, int only_flagged)
+static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
+                      hipStream_t s)
 {
     const size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap, 2, qt_kpn(NT, KPT, 0)).total;
     hipFuncSetAttribute((const void*)k_quadtree<NT, KPT, kG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL((k_quadtree<NT, KPT, kG>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
                        b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt,
-                       frame_counts, b.status, q.lcap, q.cellcap, only_flagged);
-}
-
-// The path-code kernel for a group of the node-list plan (same candidate capacity NT * KPT, its own
-// workgroup shape PNT x PKPT), then, if some level of the group may not fit it, the node-list kernel over the
-// (frame, level)s it flagged.
-template <int NT, int KPT, int PNT, int PKPT>
-static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts, const QtGroup& q, int batch,
-                      hipStream_t s)
-{
-    static_assert(PNT * PKPT >= NT * KPT, "at least the node-list kernel's capacity");
-    // Round 4: measured slower than the node-list kernel once FAST writes each wave's candidates as one run
-    // (DESIGN.md §6), so it runs only when ORBX_QT_PATHS=1 asks for it.
-    static const bool paths = getenv("ORBX_QT_PATHS") && atoi(getenv("ORBX_QT_PATHS")) != 0;
-    if (q.ninv == 0 || !paths) {
-        qt_launch_nodes<NT, KPT, false>(g, b, frame_counts, q, batch, s, 0);
-        return;
-    }
-    const size_t smem = qp_layout(PNT * PKPT, q.lcap, q.cellcap, q.ninv, q.nbins).total;
-    hipFuncSetAttribute((const void*)k_qt_paths<PNT, PKPT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL((k_qt_paths<PNT, PKPT>), dim3(q.nl, batch), dim3(PNT), smem, s, q.l0, b.geom, b.cells, b.slots,
-                       b.cell_counts, b.qpt, b.spill, b.spill_node, b.qt_out, b.qt_cnt, frame_counts,
-                       b.status, q.lcap, q.cellcap, q.ninv, q.nbins);
-    bool fb = false;
-    for (int l = q.l0; l < q.l0 + q.nl; ++l) fb |= !g.lv[l].qp_ok || g.lv[l].slot_cap > PNT * PKPT;
-    if (fb) qt_launch_nodes<NT, KPT, false>(g, b, frame_counts, q, batch, s, 1);
+                       frame_counts, b.status, q.lcap, q.cellcap);
 }
 
 // Launch groups.  A group's node capacity is the largest cap + 4 of its levels: a level's list never holds
@@ -3041,15 +2051,9 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
     auto caps = [&](QtGroup& q) {
         q.lcap = 8;
         q.cellcap = 1;
-        q.ninv = 0;   // 0: no level of the group takes the path-code kernel
-        q.nbins = 0;
         for (int l = q.l0; l < q.l0 + q.nl; ++l) {
             q.lcap = std::max(q.lcap, g.lv[l].cap + 4);
             q.cellcap = std::max(q.cellcap, g.lv[l].ncells);
-            if (g.lv[l].qp_ok) {
-                q.ninv = std::max(q.ninv, (g.lv[l].nIni << g.lv[l].qp_D) + (1 << g.lv[l].qp_D));
-                q.nbins = std::max(q.nbins, 1 << g.lv[l].qp_bb);
-            }
         }
     };
     bool anyg = false;
@@ -3058,7 +2062,7 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
     // the levels run concurrently instead of as dependent launches (latency, not throughput).
     // A level run with more register capacity than qt_regcap(g, l) spills less than its region holds.
     if (batch <= kQtMergedMaxBatch && !anyg) {
-        QtGroup q{0, g.nlevels, 512, g.qt_kpt0, 0, 0, 0, 0, 0};
+        QtGroup q{0, g.nlevels, 512, g.qt_kpt0, 0, 0, 0};
         caps(q);
         if (qt_layout(q.lcap, q.cellcap, 2, qt_kpn(q.nt, q.kpt, 0)).total <= kQtLdsMax) {
             out[0] = q;
@@ -3072,7 +2076,7 @@ int qt_plan(const Geometry& g, int batch, QtGroup* out)
         const int nt = qt_nt(g, l0), kpt = qt_kpt(g, l0), gl = g.lv[l0].qt_glob;
         int l1 = l0 + 1;
         while (l1 < g.nlevels && qt_nt(g, l1) == nt && qt_kpt(g, l1) == kpt && g.lv[l1].qt_glob == gl) ++l1;
-        QtGroup q{l0, l1 - l0, nt, kpt, gl, 0, 0, 0, 0};
+        QtGroup q{l0, l1 - l0, nt, kpt, gl, 0, 0};
         caps(q);
         out[n++] = q;
         l0 = l1;
@@ -3119,85 +2123,6 @@ bool qt_prepare(Geometry& g)
     }
 }
 
-// K3 path tables (tests/test_qt_pathcode.py restates them).  DivideNode (src/ORBextractor.cc:569-629) splits
-// an axis range [lo, hi] at lo + ceil((hi - lo) / 2), keypoints below the midline going to the first half;
-// the roots are [(int)(hX * i), (int)(hX * (i + 1))] x [0, qh] (:663-675), a keypoint's root (int)(x / hX)
-// (:681).  D = the depth at which every root range and the y range are down to single coordinates.
-static int qp_depth(int npts)
-{
-    if (npts <= 1) return 0;
-    const int h = (int)std::ceil((float)(npts - 1) / 2);
-    return 1 + std::max(qp_depth(h), qp_depth(npts - h));
-}
-
-void qp_tables(Geometry& g, std::vector<uint32_t>& tab)
-{
-    tab.clear();
-    for (int l = 0; l < g.nlevels; ++l) {
-        LevelGeom& L = g.lv[l];
-        L.qp_ok = 0;
-        const int nIni = L.nIni;
-        const float hX = L.hX;
-        std::vector<int> rx0(nIni), rx1(nIni);
-        int D = qp_depth(L.qh + 1);
-        for (int i = 0; i < nIni; ++i) {
-            rx0[i] = (int)(hX * (float)i);
-            rx1[i] = (int)(hX * (float)(i + 1));
-            D = std::max(D, qp_depth(rx1[i] - rx0[i] + 1));
-        }
-        int rb = 1;
-        while ((1 << rb) < nIni) ++rb;
-        if (L.qt_glob || rb + 2 * D + 8 > 32 || D < 1) continue;
-        int bb = 0;   // sort bins: about a quarter of the candidates a workgroup holds
-        while ((8 << bb) <= qt_regcap(g, l)) ++bb;
-        L.qp_ok = 1;
-        L.qp_D = D;
-        L.qp_rb = rb;
-        L.qp_bb = std::min(bb, rb + 2 * D);
-        L.qp_xk = (int)tab.size();
-        tab.resize(tab.size() + L.w);
-        L.qp_yk = (int)tab.size();
-        tab.resize(tab.size() + L.h);
-        L.qp_xi = (int)tab.size();
-        tab.resize(tab.size() + ((size_t)nIni << D), 0xFFFFFFFFu);
-        L.qp_yi = (int)tab.size();
-        tab.resize(tab.size() + ((size_t)1 << D), 0xFFFFFFFFu);
-        for (int x = 0; x < L.w; ++x) {
-            const int r = std::min((int)((float)x / hX), nIni - 1);
-            int x0 = rx0[r], x1 = rx1[r];
-            uint32_t code = (uint32_t)r, bits = 0;
-            for (int j = 0; j < D; ++j) {
-                const int mid = x0 + (int)std::ceil((float)(x1 - x0) / 2);
-                const uint32_t bit = x >= mid ? 1u : 0u;
-                code = (code << 2) | bit;
-                bits = (bits << 1) | bit;
-                if (bit) x0 = mid; else x1 = mid;
-            }
-            tab[L.qp_xk + x] = code << 8;
-            // a candidate's FAST cell column: x = j * wCell + 3 + (its column in the cell's detection window),
-            // src/ORBextractor.cc:952-1000
-            const uint32_t col = x >= 3 ? (uint32_t)((x - 3) / L.qp_wc) : 0u;
-            uint32_t& inv = tab[L.qp_xi + (((size_t)r << D) | bits)];
-            if (inv == 0xFFFFFFFFu) inv = (col << 12) | (uint32_t)x;   // the smallest coordinate of a code is the keypoints'
-        }
-        for (int y = 0; y < L.h; ++y) {
-            int y0 = 0, y1 = L.qh;
-            uint32_t code = 0, bits = 0;
-            for (int j = 0; j < D; ++j) {
-                const int mid = y0 + (int)std::ceil((float)(y1 - y0) / 2);
-                const uint32_t bit = y >= mid ? 1u : 0u;
-                code = (code << 2) | (bit << 1);
-                bits = (bits << 1) | bit;
-                if (bit) y0 = mid; else y1 = mid;
-            }
-            tab[L.qp_yk + y] = code << 8;
-            const uint32_t row = y >= 3 ? (uint32_t)((y - 3) / L.qp_hc) : 0u;
-            uint32_t& inv = tab[L.qp_yi + bits];
-            if (inv == 0xFFFFFFFFu) inv = (row << 12) | (uint32_t)y;
-        }
-    }
-}
-
 #ifdef ORBX_QT_PROF
 }  // namespace orbx
 extern "C" int orbx_debug_qt_prof(unsigned long long* out, int reset)
@@ -3218,15 +2143,11 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
     const int ng = qt_plan(g, batch, grp);
     for (int i = 0; i < ng; ++i) {
         const QtGroup& q = grp[i];
-        if (q.glob) qt_launch_nodes<kQtGlobNT, kQtGlobKPT, true>(g, b, frame_counts, q, batch, s, 0);
-        else if (q.nt == 512 && q.kpt == 24) qt_launch<512, 24, 1024, 12>(g, b, frame_counts, q, batch, s);
-        else if (q.nt == 512 && q.kpt == 16) qt_launch<512, 16, 1024, 11>(g, b, frame_counts, q, batch, s);
-        else if (q.nt == 512) qt_launch<512, 8, 1024, 4>(g, b, frame_counts, q, batch, s);
-#if ORBX_QT2_SHAPE
-        else qt_launch<128, 8, 256, 4>(g, b, frame_counts, q, batch, s);
-#else
-        else qt_launch<256, 4, 256, 4>(g, b, frame_counts, q, batch, s);
-#endif
+        if (q.glob) qt_launch<kQtGlobNT, kQtGlobKPT, true>(g, b, frame_counts, q, batch, s);
+        else if (q.nt == 512 && q.kpt == 24) qt_launch<512, 24, false>(g, b, frame_counts, q, batch, s);
+        else if (q.nt == 512 && q.kpt == 16) qt_launch<512, 16, false>(g, b, frame_counts, q, batch, s);
+        else if (q.nt == 512) qt_launch<512, 8, false>(g, b, frame_counts, q, batch, s);
+        else qt_launch<256, 4, false>(g, b, frame_counts, q, batch, s);
     }
 }
 
@@ -3252,13 +2173,8 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 constexpr int kRawP = 48;                             // LDS row pitch (bytes): the 43 columns + shift slack
 constexpr int kRawRows = 44;                          // 43 rows used (row 43 repeats row 42)
 constexpr int kRawSlots = kRawRows * kRawP / 4;
-#ifndef ORBX_DESC_ROW1
-#define ORBX_DESC_ROW1 0
-#endif
-// row-blurred, transposed: [col][row pairs], 22 dwords per column; ORBX_DESC_ROW1=1: one dword per row y
-// holding rows (y, y + 1), at dword y + 1 of its column (dword 0 a pad), so a sample's seven taps are dwords
-// y + 1, y + 3, y + 5, y + 7 with fixed weights whatever y's parity
-constexpr int kTCols = 40, kTP = ORBX_DESC_ROW1 ? 44 : 22;
+// row-blurred, transposed: [col][row pairs], 22 dwords per column
+constexpr int kTCols = 40, kTP = 22;
 #ifndef ORBX_DESC_KPW
 #define ORBX_DESC_KPW 4
 #endif
@@ -3270,9 +2186,6 @@ constexpr int kDescPerWave = ORBX_DESC_KPW;           // keypoints per wave (lan
 // and no wave waits on slower siblings (4 waves: 863 us per 384 frames, 2: 815, 1: 768; pipelined 169.1k ->
 // 176.4k frames/s)
 constexpr int kDescWaves = ORBX_DESC_WAVES;
-#ifndef ORBX_DESC_ICG
-#define ORBX_DESC_ICG 1   // IC_Angle and the angle's trigonometry once per wave (0: per keypoint, round 2)
-#endif
 
 // Horizontal-pass items (row pair rp << 8 | column group cg) that BRIEF can read: a sample
 // (18 + xx, 18 + yy) has |(x, y)| <= 18.39 before rounding (the pattern's largest radius), so a
@@ -3351,7 +2264,6 @@ __device__ __forceinline__ int wave_sum(int v)
            __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
 }
 
-
 // Sample coordinates as float bits: fl + 1.5 * 2^23 rounds fl to the nearest integer, ties to even
 // (one f32 addition into [2^23, 2^24), whose ulp is 1; the magic number is even, so the tie parity
 // is fl's), exactly __float2int_rn for |fl| < 2^22, and leaves that integer in the low mantissa
@@ -3366,22 +2278,6 @@ constexpr uint32_t kRoundBits = 0x4B400000u;
 // The LDS byte address in three VALU: bfe of by's bits 1..23 (0x200000 + (yy >> 1)), shifted and added to
 // mad24(bx, 4 kTP, C) with C = rowT + 4 (9 - 0x200000 + (18 - 0x400000) kTP) (mod 2^32); the compiler's
 // form of (by >> 1) + bx * kTP + rowT took five.
-#if ORBX_DESC_ROW1
-// dword (18 + xx) * kTP + (18 + yy) + 1: by << 2 is 4 * (0x4B400000 + yy) (mod 2^32)
-constexpr uint32_t kBlurByte0 = 4u * (19u + (18u - 0x400000u) * (uint32_t)kTP) - 4u * 0x4B400000u;
-__device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t bx)
-{
-    const uint32_t t = __umul24(bx, 4u * (uint32_t)kTP) + C;
-    uint32_t a;
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"(by), "v"(t));
-    const __attribute__((address_space(3))) uint32_t* col = (const __attribute__((address_space(3))) uint32_t*)(uintptr_t)a;
-    const uint32_t d0 = col[0], d1 = col[2], d2 = col[4], d3 = col[6];
-    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), ushort2_t{18, 34}, 1u << 15, false);
-    acc = __builtin_amdgcn_udot2(as_us2(d1), ushort2_t{49, 55}, acc, false);
-    acc = __builtin_amdgcn_udot2(as_us2(d2), ushort2_t{49, 34}, acc, false);
-    return __builtin_amdgcn_udot2(as_us2(d3), ushort2_t{18, 0}, acc, false);
-}
-#else
 constexpr uint32_t kBlurByte0 = 4u * (9u - 0x200000u + (18u - 0x400000u) * (uint32_t)kTP);
 __device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t bx)
 {
@@ -3415,48 +2311,8 @@ __device__ __forceinline__ uint32_t blur_taps(uint32_t d0, uint32_t d1, uint32_t
     acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
     return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
 }
-// A test's two samples with their LDS reads in inline asm (ORBX_DESC_ASMRD=1).  The compiler treats the next
-// keypoint's patch DMA (in flight under BRIEF, into the raw rows) as a store that may alias any LDS read and
-// waits for it (vmcnt(0)) before the first BRIEF read it can see; reads it cannot see keep the DMA in flight.
-// The asm waits for its own reads (lgkmcnt) and orders after the transpose's stores ("memory").
-__device__ __forceinline__ void blur_pair(uint32_t C, uint32_t by0, uint32_t bx0, uint32_t by1, uint32_t bx1,
-                                          uint32_t& r0, uint32_t& r1)
-{
-    const uint32_t t0 = __umul24(bx0, 4u * (uint32_t)kTP) + C, f0 = __builtin_amdgcn_ubfe(by0, 1, 23);
-    const uint32_t t1 = __umul24(bx1, 4u * (uint32_t)kTP) + C, f1 = __builtin_amdgcn_ubfe(by1, 1, 23);
-    uint32_t a0, a1;
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a0) : "v"(f0), "v"(t0));
-    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a1) : "v"(f1), "v"(t1));
-    unsigned long long p0, p1, q0, q1;
-    asm volatile("ds_read2_b32 %0, %4 offset1:1\n\t"
-                 "ds_read2_b32 %1, %4 offset0:2 offset1:3\n\t"
-                 "ds_read2_b32 %2, %5 offset1:1\n\t"
-                 "ds_read2_b32 %3, %5 offset0:2 offset1:3\n\t"
-                 "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(p0), "=&v"(p1), "=&v"(q0), "=&v"(q1)
-                 : "v"(a0), "v"(a1)
-                 : "memory");
-    r0 = blur_taps((uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32), by0);
-    r1 = blur_taps((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32), by1);
-}
-#endif
-
 #ifndef ORBX_DESC_WPE
 #define ORBX_DESC_WPE 1
-#endif
-#ifndef ORBX_DESC_DEFER
-#define ORBX_DESC_DEFER 0
-#endif
-#ifndef ORBX_DESC_STW
-#define ORBX_DESC_STW 1
-#endif
-#ifndef ORBX_DESC_KEEPVA
-#define ORBX_DESC_KEEPVA 1
-#endif
-#ifndef ORBX_DESC_ASMRD
-#define ORBX_DESC_ASMRD 0   // 1: BRIEF's LDS reads and the transpose's stores in inline asm (blur_pair), so the
-                            // compiler cannot wait for the next patch's DMA before them: 585.0 -> 580.9 us
-                            // alone, no gain in the pipelined step (263.6k against 264.9k frames/s)
 #endif
 __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
                                                const uint32_t* __restrict__ qt_out,
@@ -3465,9 +2321,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                                                int cap, int* __restrict__ status, int kpw)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_raw[kDescWaves][kRawSlots];
-    // (ORBX_DESC_ROW1: + 4, the last column's item 21 writes one dword past its column)
-    __shared__ __attribute__((aligned(16))) uint32_t s_rowT[kDescWaves][kTCols * kTP + (ORBX_DESC_ROW1 ? 4 : 0)];
-    __shared__ uint32_t s_out[kDescWaves][15 * kDescPerWave];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rowT[kDescWaves][kTCols * kTP];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x, bx = lb - f * gridDim.x;
@@ -3532,11 +2386,9 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     };
     // raw patch rows cy-21..cy+21 from column cx-21 (48 bytes used per row); sets the
     // wave-uniform row-shift state: row r starts at byte (sb + r*sp) & 3 of its LDS row
-#if ORBX_DESC_KEEPVA
     // the DMA's address registers kept live until the loop-top wait for it, so no later write to them makes
     // the compiler wait for the DMA (a write-after-read on a VMEM source register) before BRIEF
     uint32_t dma_va[3] = {0u, 0u, 0u};
-#endif
     auto fill = [&](int l, uint32_t pk, int& sb, int& sp) {
         const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF);
         const int w = G->lv[l].w, h = G->lv[l].h;
@@ -3565,9 +2417,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                     const uint32_t o = (uint32_t)((sb + min(row, 42) * pitch) & ~3) + 16u * (uint32_t)k;
                     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ub + o),
                                                      (__attribute__((address_space(3))) void*)(raw32 + 256 * t), 16, 0, 0);
-#if ORBX_DESC_KEEPVA
                     dma_va[t] = o;
-#endif
                 }
             }
         } else {
@@ -3596,7 +2446,6 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     uint32_t npk = 0;
     bool nvalid = lookup(0, nl, npk);
     if (nvalid) fill(nl, npk, sb, sp);
-#if ORBX_DESC_ICG
     // IC_Angle (src/ORBextractor.cc:84-128) of the wave's keypoints up front, from the level images in
     // global memory: a keypoint lies >= 19 px inside its level (FAST's cell windows), so its radius-15 disc
     // never leaves it (lanes 62-63 read row 16 with zero weights).  cv::fastAtan2 and sincosf then run
@@ -3645,13 +2494,6 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         kp_ang = fast_atan2_deg((float)ic_m01, (float)ic_m10);
         glibc_sincosf_pair(kp_ang * kFactorPI, &kp_sin, &kp_cos);   // (src/ORBextractor.cc:148)
     }
-#endif
-    // The wave's outputs stay in LDS until its last keypoint (s_out: 8 descriptor dwords per keypoint, then
-    // 7 cv::KeyPoint dwords per keypoint).  A global store inside the loop would make the next keypoint's
-    // wait for its patch DMA (vmcnt counts loads and stores, completed in issue order) wait for the store's
-    // round trip as well.
-    uint32_t* sout = s_out[wave];
-    int nout = 0;
 #pragma unroll 1
     for (int jj = 0; jj < kpw && nvalid; ++jj) {
         const int oidx = g0 + jj, l = nl;
@@ -3661,38 +2503,14 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF), score = (int)(pk >> 24);
         // this keypoint's DMA has landed.  vmcnt counts loads and stores and retires them in issue order, and
         // the previous keypoint's three output stores (desc dwordx2, cv::KeyPoint dwordx4 + dwordx3) were issued
-        // after this DMA: waiting down to 3 leaves their round trip in flight (ORBX_DESC_STW=0: wait for all)
+        // after this DMA: waiting down to 3 leaves their round trip in flight
         // (the builtin, not inline asm: the compiler's wait-count pass sees it, and does not wait again for
         // loads it already covers -- an inline-asm wait is opaque to it; gfx9 simm16: vmcnt[3:0], expcnt[6:4]
         // = 7, lgkmcnt[11:8] = 15, vmcnt[5:4] at [15:14])
-#if ORBX_DESC_STW && !ORBX_DESC_DEFER
         // (also right for jj = 0: the IC_Angle loads issued after the first keypoint's DMA were waited for)
         __builtin_amdgcn_s_waitcnt(0x0F73);   // vmcnt(3)
-#else
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-#endif
-#if ORBX_DESC_KEEPVA
         asm volatile("" ::"v"(dma_va[0]), "v"(dma_va[1]), "v"(dma_va[2]));
-#endif
         wave_lds_sync();
-
-#if !ORBX_DESC_ICG
-        // IC_Angle (src/ORBextractor.cc:84-128): integer moments over the disc, any order
-        const int icb0 = ic_row * kRawP + ((csb + ic_row * csp) & 3) + ic_col;
-        const uint32_t* icq = raw32 + (icb0 >> 2);
-        const uint32_t icsh = (uint32_t)(icb0 & 3);
-        const uint32_t q0 = icq[0], q1 = icq[1], q2 = icq[2], q3 = icq[3], q4 = icq[4];
-        const uint32_t iw[4] = {__builtin_amdgcn_alignbyte(q1, q0, icsh), __builtin_amdgcn_alignbyte(q2, q1, icsh),
-                                __builtin_amdgcn_alignbyte(q3, q2, icsh), __builtin_amdgcn_alignbyte(q4, q3, icsh)};
-        uint32_t s1 = 0u, s0 = 0u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            s1 = __builtin_amdgcn_udot4(iw[k], W1[k], s1, false);
-            s0 = __builtin_amdgcn_udot4(iw[k], W0[k], s0, false);
-        }
-        const int m10 = wave_sum((int)s1 - 16 * (int)s0);
-        const int m01 = wave_sum(vrow * (int)s0);
-#endif
 
         // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns.
         // Output column j of the realigned bytes R0 | R1 | R2 is sum_t w[t] * byte[j + t]: a dot4 of each
@@ -3703,9 +2521,6 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             {18u << 8 | 34u << 16 | 49u << 24, 55u | 49u << 8 | 34u << 16 | 18u << 24, 0u},
             {18u << 16 | 34u << 24, 49u | 55u << 8 | 49u << 16 | 34u << 24, 18u},
             {18u << 24, 34u | 49u << 8 | 55u << 16 | 49u << 24, 34u | 18u << 8}};
-#ifdef ORBX_DIAG_NOHPASS   // diagnostic build (wrong results): the horizontal pass's cost
-        if (lane < 32) rowT[lane * 23] = raw32[lane];
-#else
         // Rows that all start at the same byte shift S (csp == 0: the level pitch is a multiple of 4, or the
         // reflect-101 byte path) skip the realignment: output column j is a dot4 of each raw dword with the
         // kernel shifted by S + j bytes, still 10 dot4 per row (2 or 3 per column) and no alignbyte.
@@ -3748,35 +2563,8 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-#if ORBX_DESC_ROW1
-                    // rows (2rp, 2rp + 1) at dword 2rp + 1, row 2rp + 1 also in the low half of dword 2rp + 2 and
-                    // row 2rp in the high half of dword 2rp (one address, three immediate offsets)
-                    const uint32_t pr = o[0][j] | (o[1][j] << 16);
-                    uint8_t* b = (uint8_t*)(rowT + (4 * cg + j) * kTP + 2 * rp) + 2;
-                    *(uint16_t*)b = (uint16_t)pr;
-                    *(uint32_t*)(b + 2) = pr;
-                    *(uint16_t*)(b + 6) = (uint16_t)(pr >> 16);
-#elif ORBX_DESC_ASMRD
-                    (void)0;
-#else
                     rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
-#endif
                 }
-#if ORBX_DESC_ASMRD && !ORBX_DESC_ROW1
-                {   // the transpose's stores in inline asm as well: the compiler's wait-count pass would wait
-                    // for the next patch's DMA (a store to LDS it cannot tell apart) before them
-                    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(rowT + 4 * cg * kTP + rp);
-                    asm volatile("ds_write_b32 %0, %1\n\t"
-                                 "ds_write_b32 %0, %2 offset:%5\n\t"
-                                 "ds_write_b32 %0, %3 offset:%6\n\t"
-                                 "ds_write_b32 %0, %4 offset:%7"
-                                 :
-                                 : "v"(a), "v"(o[0][0] | (o[1][0] << 16)), "v"(o[0][1] | (o[1][1] << 16)),
-                                   "v"(o[0][2] | (o[1][2] << 16)), "v"(o[0][3] | (o[1][3] << 16)), "i"(4 * kTP),
-                                   "i"(8 * kTP), "i"(12 * kTP)
-                                 : "memory");
-                }
-#endif
             }
         };
         if (csp != 0) hpass(std::integral_constant<int, -1>{});
@@ -3784,28 +2572,14 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         else if (csb == 1) hpass(std::integral_constant<int, 1>{});
         else if (csb == 2) hpass(std::integral_constant<int, 2>{});
         else hpass(std::integral_constant<int, 3>{});
-#endif
-#if ORBX_DESC_ASMRD && !ORBX_DESC_ROW1
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the asm stores above are not tracked by the compiler
-#endif
         wave_lds_sync();   // raw is free: start the next keypoint's patch, it lands under BRIEF
         nvalid = lookup(jj + 1, nl, npk);
         if (nvalid) fill(nl, npk, sb, sp);
 
         // rBRIEF with the reference's contracted FMAs; blur evaluated at each sample point
-#if ORBX_DESC_ICG
         const float angle = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_ang), jj));
         const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_cos), jj));
         const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_sin), jj));
-#elif defined(ORBX_DIAG_NOTRIG)   // diagnostic build (wrong results): the angle's cost
-        const float angle = (float)m01 * 1e-3f;
-        const float a = (float)m10 * 1e-3f, b = angle;
-#else
-        const float angle = fast_atan2_deg((float)m01, (float)m10);
-        const float ang = angle * kFactorPI;
-        float a, b;
-        glibc_sincosf_pair(ang, &b, &a);   // a = cosf, b = sinf (src/ORBextractor.cc:148)
-#endif
         // GaussianBlur's u8 saturation: min(t0, 255) < min(t1, 255) iff t0 < min(t1, 255)
         const uint32_t cblur = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)rowT + kBlurByte0;
         unsigned long long words[4];
@@ -3819,18 +2593,10 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             const f2v BY = __builtin_elementwise_fma(PX, vb, PY * va) + mg;
             const f2v BX = __builtin_elementwise_fma(PX, va, -(PY * vb)) + mg;
             uint32_t t2[2];
-#if ORBX_DESC_ASMRD && !ORBX_DESC_ROW1
-            blur_pair(cblur, __float_as_uint(BY[0]), __float_as_uint(BX[0]), __float_as_uint(BY[1]), __float_as_uint(BX[1]),
-                      t2[0], t2[1]);
-            t2[0] >>= 16;
-            t2[1] >>= 16;
-#else
 #pragma unroll
             for (int e = 0; e < 2; ++e) t2[e] = blur_acc(cblur, __float_as_uint(BY[e]), __float_as_uint(BX[e])) >> 16;
-#endif
             words[wd] = __ballot(t2[0] < (t2[1] < 255u ? t2[1] : 255u));
         }
-#if ORBX_DESC_DEFER == 0
         {   // A/B knob: per-keypoint stores (round 2)
             const size_t o = (size_t)f * cap + oidx;
             if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
@@ -3851,30 +2617,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                 kps[o] = k;
             }
         }
-#else
-        if (lane < 8) {
-            const unsigned long long v = lane < 2 ? words[0] : lane < 4 ? words[1] : lane < 6 ? words[2] : words[3];
-            sout[8 * jj + lane] = (lane & 1) ? (uint32_t)(v >> 32) : (uint32_t)v;
-        } else if (lane < 15) {
-            float x = (float)cx, y = (float)cy;
-            if (l != 0) {
-                x *= LG.scale;
-                y *= LG.scale;
-            }
-            const int k = lane - 8;   // cv::KeyPoint fields: x y size angle response octave class_id
-            sout[8 * kDescPerWave + 7 * jj + k] =
-                k == 0 ? __float_as_uint(x) : k == 1 ? __float_as_uint(y) : k == 2 ? __float_as_uint(LG.patch_size)
-                : k == 3 ? __float_as_uint(angle) : k == 4 ? __float_as_uint((float)score) : k == 5 ? (uint32_t)l
-                : 0xFFFFFFFFu;
-        }
-#endif
-        nout = jj + 1;
         wave_lds_sync();   // rowT is rewritten by the next keypoint
-    }
-    if (ORBX_DESC_DEFER && nout > 0) {   // the wave's keypoints are consecutive outputs: one contiguous run of each array
-        const size_t o = (size_t)f * cap + g0;
-        if (lane < 8 * nout) reinterpret_cast<uint32_t*>(desc + o * 32)[lane] = sout[lane];
-        if (lane < 7 * nout) reinterpret_cast<uint32_t*>(kps + o)[lane] = sout[8 * kDescPerWave + lane];
     }
 }
 

@@ -46,12 +46,6 @@ struct LevelGeom {
     // in a per-(frame, level) global region of qtg_bytes at qtg_off inside the frame's node block
     int qt_glob;
     long long qtg_off, qtg_bytes;
-    // K3 path codes (k_qt_paths): D digits below the root, rootbits root bits; a keypoint's sort key is
-    // xkey[x] | ykey[y] | score with the path above bit 8.  Tables (uint32) in the geometry's path-table
-    // buffer at the offsets below; qp_ok 0: the level runs the node-list kernel body.
-    int qp_ok, qp_D, qp_rb, qp_bb;          // bb: sort bin bits (the path's top bits)
-    int qp_xk, qp_yk, qp_xi, qp_yi;         // xkey[w], ykey[h], xinv[nIni << D], yinv[1 << D]
-    int qp_wc, qp_hc;                       // FAST cell width / height (the candidates' reference order)
 };
 
 // K1 small-batch launch group: levels s+1 .. s+n resized from level s in one launch (k_pyramid_fused).  A

@@ -30,7 +30,6 @@ struct ExtractBufs {
     uint32_t* spill;            // [B][spill_per_frame] quadtree overflow (packed kp)
     uint32_t* spill_node;       // [B][spill_per_frame]
     uint8_t* qt_nodes;          // [B][qtg_per_frame] K3 node arrays of the levels whose list outgrows LDS
-    const uint32_t* qpt;        // K3 path tables (LevelGeom::qp_*)
     uint32_t* qt_out;           // [B][out_per_frame] retained keypoints (level coords)
     int* qt_cnt;                // [B][nlevels]
     int* status;                // device error word (bit flags)
@@ -58,16 +57,12 @@ enum : int {
 // live in global memory (ExtractBufs::qt_nodes) because lcap nodes need more LDS than a workgroup has.
 struct QtGroup {
     int l0, nl, nt, kpt, glob, lcap, cellcap;
-    int ninv;    // path-code kernel: the group's largest inverse-table size (entries); 0: node-list kernel only
-    int nbins;   // path-code kernel: the group's largest sort-bin count
 };
 constexpr int kQtMaxGroups = kMaxLevels + 1;
 int qt_plan(const Geometry& g, int batch, QtGroup* out);   // returns the group count
 // host: decides qt_glob per level and lays out the per-frame global node block (qtg_*); false if a
 // level cannot be run at all
 bool qt_prepare(Geometry& g);
-// host: K3 path tables of every level (after qt_prepare); sets LevelGeom::qp_*
-void qp_tables(Geometry& g, std::vector<uint32_t>& tab);
 // quadtree workgroup size and keypoints held in registers per thread at level l (the rest spill
 // to global): level 0 holds most candidates, levels >= 2 a few hundred
 // (level 0: 16 per thread, or 24 for frames above kQtBigArea pixels, whose level-0 candidates

@@ -1008,9 +1008,7 @@ void launch_search_init(const orbx_keypoint* kps, const uint8_t* desc, const int
     hipLaunchKernelGGL(k_si_grid, dim3(nframes), dim3(256), si_grid_smem(cap), s, kps, counts, cap, G, gkeys, gxy, gn);
     const size_t bsmem = si_build_smem_bytes();
     // query slices per pair: about 8 waves per SIMD over the chip, at least 4 queries per wave
-    // (ORBX_SI_QSPLIT: A/B knob)
-    static const int qs_env = getenv("ORBX_SI_QSPLIT") ? atoi(getenv("ORBX_SI_QSPLIT")) : 0;
-    const int qsplit = qs_env > 0 ? qs_env : std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
+    const int qsplit = std::max(1, std::min((2048 + npairs - 1) / npairs, (cap + 15) / 16));
     hipLaunchKernelGGL(k_si_build, dim3(npairs, qsplit), dim3(SI_BUILD_NT), bsmem, s, kps, desc, cap, pa, pb, G,
                        window, (const float2*)prev, gkeys, gxy, gn, qcnt, qtop);
     const int ldscap = std::min(cap, si_lds_max_cap());

@@ -456,3 +456,60 @@ def test_stage_times_cover_stage_split_calls(orbref, cuda):
         ref = orbref.extract(kitti[f], p, want_pyramid=False)
         n = len(ref.keypoints)
         assert_same_keypoints(klist[f], ref.keypoints, d[f, :n], ref.descriptors, "stage-split frame %d" % f)
+
+
+@pytest.mark.parametrize("kind,W,H,nfeat", [("noise", 640, 480, 1000), ("kitti", 1241, 376, 2000)])
+def test_candidates_multi_cell_waves(orbref, cuda, kind, W, H, nfeat):
+    """Batches above kLatencyMaxBatch run kCellsPerWave (3) FAST cells per wave: the wave's buffered run from
+    its first cell's slot base, cells written at their own base after a buffer overflow (kCellDirect; uniform
+    noise overflows it), and the run decoding of orbx_debug_candidates.  Candidates per level, reference order."""
+    frames = _frames(kind, W, H, 10, seed0=3)
+    if kind == "noise":   # mixed batch: noise frames overflow the wave buffers, textured ones do not
+        import orbx_synth
+        frames[5:] = np.stack([orbx_synth.gen_image(50 + i, W, H) for i in range(5)])
+    ex = _extractor(nfeat)
+    p = orbref.make_params(nfeat, 1.2, 8, 20, 7)
+    _, _, _, _, klist, dlist = _run_batch(ex, frames, cuda)
+    for f in (0, 4, 5, 9):
+        ref = orbref.extract(frames[f], p)
+        for l in range(8):
+            want = orbref.level_candidates(ref.pyramid[l])
+            got = ex.debug_candidates(f, l)
+            assert len(got) == len(want), "%s f%d level %d: %d candidates vs %d" % (kind, f, l, len(got), len(want))
+            assert np.array_equal(got, want), "%s f%d level %d candidates differ" % (kind, f, l)
+        assert_same_keypoints(klist[f], ref.keypoints, dlist[f], ref.descriptors, "%s f%d" % (kind, f))
+
+
+def test_pyramid_per_level_launches_small_batch(orbref, cuda):
+    """ORBX_PYR_FUSED=0 (read when a handle first sees an image size): small batches take the per-level pyramid
+    launches of large batches instead of the fused groups (k_pyramid_fused).  Both settings are the oracle's
+    bytes; this is the library's only runtime kernel switch besides ORBX_NO_GRAPH."""
+    import os
+    import orbx_synth
+    img = orbx_synth.gen_image(61, 640, 480)
+    p = orbref.make_params(1000, 1.2, 8, 20, 7)
+    ref = orbref.extract(img, p)
+    for setting in ("0", None):
+        if setting is None:
+            os.environ.pop("ORBX_PYR_FUSED", None)
+        else:
+            os.environ["ORBX_PYR_FUSED"] = setting
+        try:
+            ex = _extractor(1000)
+            kps, desc = ex(img)
+        finally:
+            os.environ.pop("ORBX_PYR_FUSED", None)
+        assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "ORBX_PYR_FUSED=%s" % setting)
+        for l in range(8):
+            assert np.array_equal(ex.mvImagePyramid[l], ref.pyramid[l]), "ORBX_PYR_FUSED=%s level %d" % (setting, l)
+    # a 4-frame batch (still a small batch) the same way
+    os.environ["ORBX_PYR_FUSED"] = "0"
+    try:
+        ex = _extractor(1000)
+        frames = _frames("gen", 640, 480, 4, seed0=70)
+        _, _, _, _, klist, dlist = _run_batch(ex, frames, cuda)
+    finally:
+        os.environ.pop("ORBX_PYR_FUSED", None)
+    for f in range(4):
+        r = orbref.extract(frames[f], p, want_pyramid=False)
+        assert_same_keypoints(klist[f], r.keypoints, dlist[f], r.descriptors, "per-level batch f%d" % f)

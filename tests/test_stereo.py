@@ -403,3 +403,46 @@ def test_gpu_stereo_band_batch(orbref, cuda):
         n = c[2 * k]
         assert n == len(a.keypoints)
         assert np.array_equal(bi[k, :n].cpu().numpy(), wi) and np.array_equal(bd[k, :n].cpu().numpy(), wd)
+
+
+@pytest.mark.gpu
+def test_gpu_batch_stereo_cross_stream_then_next_batch(orbref, cuda):
+    """Stereo on stream B (behind a long kernel) reads the handle's pyramids; the next batch on stream A
+    rewrites them.  The extractor orders the next batch after the stereo search (orbx_stereo_batch_device
+    marks itself as the handle's last work), so stereo still sees the first batch's pyramids."""
+    import torch
+    import orbx
+    W, H, nfeat = 752, 480, 1000
+    pairs = [_pair(s, W, H) for s in (3, 4)]
+    frames = np.stack([im for pr in pairs for im in pr])
+    other = np.stack([_pair(s, W, H)[k] for s in (8, 9) for k in (0, 1)])
+    ex = orbx.ORBextractor(nfeat, 1.2, 8, 20, 7)
+    A = torch.cuda.current_stream()
+    Bs = torch.cuda.Stream(device=cuda)
+    imgs = torch.from_numpy(frames).to(cuda)
+    imgs2 = torch.from_numpy(other).to(cuda)
+    cap = ex.capacity(H, W)
+    bufs = [(torch.empty((4, cap, 7), dtype=torch.int32, device=cuda), torch.empty((4, cap, 32), dtype=torch.uint8,
+             device=cuda), torch.empty((4,), dtype=torch.int32, device=cuda)) for _ in range(2)]
+    li = torch.tensor([0, 2], dtype=torch.int32, device=cuda)
+    ri = torch.tensor([1, 3], dtype=torch.int32, device=cuda)
+    torch.cuda.synchronize()
+    ex.extract_batch_device(imgs, *bufs[0], stream=A)
+    with torch.cuda.stream(Bs):
+        torch.cuda._sleep(200_000_000)   # ~0.1 s: the stereo search is still queued when batch 2 is issued
+        ur, dp, ng = ex.stereo_batch_device(*bufs[0], li, ri, EUROC_BF, EUROC_FX, stream=Bs)
+    ex.extract_batch_device(imgs2, *bufs[1], stream=A)
+    torch.cuda.synchronize()
+    p = orbref.make_params(nfeat, 1.2, 8, 20, 7)
+    for k, (L, R) in enumerate(pairs):
+        a, b = orbref.extract(L, p), orbref.extract(R, p)
+        wur, wdp, _, wgood = orbref.compute_stereo_matches(p, a, b, H, W, EUROC_BF, EUROC_FX)
+        n = len(a.keypoints)
+        assert int(ng[k].item()) == wgood and wgood > 0
+        assert np.array_equal(ur[k, :n].cpu().numpy(), wur)
+        assert np.array_equal(dp[k, :n].cpu().numpy(), wdp)
+    klist = orbx.keypoints_from_device(bufs[1][0], bufs[1][2])
+    for f in range(4):
+        ref = orbref.extract(other[f], p, want_pyramid=False)
+        for fld in ("x", "y", "octave", "response"):
+            assert np.array_equal(klist[f][fld], ref.keypoints[fld]), (f, fld)
