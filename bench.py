@@ -127,7 +127,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # per SIMD), plain ALU ops (v_xor_b32, v_fma_f32) once per 2 (about 990-1050).  A kernel's VALU fraction is taken
 # against the measured rate of its dominant instruction.
 VALU_RATES = os.path.join(ROOT, "profiles", "r02", "valu_rate.json")
-VALU_DOMINANT = {"k_fast_cells": "v_pk_maximum3_f16", "k_describe": "v_dot4_u32_u8", "k_pyramid_level": "v_dot4_u32_u8",
+VALU_DOMINANT = {"k_fast_cells": "v_pk_maximum3_f16", "k_blur_levels+k_describe": "v_dot4_u32_u8", "k_pyramid_level": "v_dot4_u32_u8",
                  "k_quadtree<512,16|512,8|256,4>": "v_xor_b32", "k_si_grid+k_si_build+k_si_greedy": "v_bcnt_u32_b32"}
 
 
@@ -144,22 +144,47 @@ WINDOW, NNRATIO = 100, 0.9
 
 
 def copy_bandwidth(dev, nbytes: int = 1 << 30, reps: int = 10):
-    """Achievable HBM bandwidth on this GPU: a device-to-device copy of a 1 GiB buffer (read + write bytes
-    per second), the practical ceiling beside the 8 TB/s spec peak."""
+    """Achievable HBM bandwidth on this GPU, the practical ceiling beside the 8 TB/s spec peak:
+    the best of a 16-byte-per-lane streaming copy kernel (tools/probes/hbm_copy.hip; grid sizes, loads per
+    trip and non-temporal hints swept) over a 1 GiB buffer, read + write bytes per second.  The torch
+    device-to-device copy of the same buffers is reported beside it."""
+    import ctypes
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
     a.fill_(1)
     b.copy_(a)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+    out = {"torch_copy_GBps": round(timed(lambda: b.copy_(a)), 1)}
+    lib_path = os.path.join(ROOT, "tools", "probes", "libhbm_copy.so")
+    best, cfg = 0.0, None
+    if os.path.exists(lib_path):
+        lib = ctypes.CDLL(lib_path)
+        lib.hbm_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_void_p]
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        for blocks in (1024, 2048, 4096, 8192):
+            for unroll in (1, 4, 8):
+                for nt in (0, 1):
+                    def run():
+                        if lib.hbm_copy(b.data_ptr(), a.data_ptr(), nbytes // 16, blocks, unroll, nt, st) != 0:
+                            raise RuntimeError("hbm_copy launch failed")
+                    g = timed(run)
+                    if g > best:
+                        best, cfg = g, {"blocks": blocks, "threads": 256, "uint4_per_trip": unroll, "nontemporal": nt}
     del a, b
-    return gbs
+    out.update({"kernel_copy_GBps": round(best, 1), "kernel_copy_config": cfg})
+    return (best if best > 0 else out["torch_copy_GBps"]), out
 
 
 def log(*a):
@@ -522,9 +547,10 @@ def main():
         "pyramid": B * (sum(A[l] for l in range(NLEVELS) if n_launch["pyramid_sources"] >> l & 1) + sum(A[1:])),
         "fast": B * (sum(A) + 4 * cand),
         "quadtree": B * (4 * cand + 4 * kept),
-        # compulsory bytes: every level pixel once (patches overlap), the packed keypoint in,
-        # the 28 B keypoint + 32 B descriptor out
-        "describe": B * (sum(A) + kept * (4 + 60)),
+        # the stage is K1b (GaussianBlur of every level) + K4: every level pixel read once (the blur and
+        # IC_Angle's discs), every blurred pixel written once and read once (BRIEF's patches overlap), the
+        # packed keypoint in, the 28 B keypoint + 32 B descriptor out
+        "describe": B * (3 * sum(A) + kept * (4 + 60)),
         "match": (B - 1) * 2 * kept * 60,
     }
     def roofline(st):
@@ -537,9 +563,9 @@ def main():
         achieved = alg[dom] / launches / t_launch / 1e9
         qk = "k_quadtree"
         kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": qk + "<512,16|512,8|256,4>",
-                 "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
+                 "describe": "k_blur_levels+k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
         # stages made of several kernels: their per-launch counters add up
-        PARTS = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"],
+        PARTS = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"], "describe": ["k_blur_levels", "k_describe"],
                  "quadtree": [qk + "<512, 16", qk + "<512, 8", qk + "<256, 4"]}
 
         def per_launch(K, dom, kname, field):
@@ -643,8 +669,9 @@ def main():
         out["roofline"] = dict(roofline(iso), timing="isolated one-stream pass after the timed region "
                                                         "(same batches); see roofline_pipelined")
     try:   # after the timed region; not part of `value`
-        cbw = copy_bandwidth(dev)
+        cbw, cinfo = copy_bandwidth(dev)
         out["roofline"]["hbm_copy_GBps"] = round(cbw, 1)
+        out["roofline"]["hbm_copy"] = cinfo
         out["roofline"]["frac_of_copy"] = round(out["roofline"]["achieved"] / cbw, 5)
     except Exception:
         pass

@@ -33,6 +33,13 @@ typedef enum {
     ORBX_ENOSPC = -28      /* caller capacity too small */
 } orbx_status;
 
+/* Keypoints per frame the matcher searches take (SearchByBoW / SearchForTriangulation views and the
+ * projection searches' frames): per-frame state of the greedy replays lives in a workgroup's LDS.  The
+ * vocabulary transform takes up to ORBV_MAX_FEATURES descriptors per frame.  The reference has neither
+ * limit (src/ORBmatcher.cc:45-129, 159-288; TemplatedVocabulary::transform); INTEGRATION.md §6. */
+#define ORBM_MAX_FEATURES 16384
+#define ORBV_MAX_FEATURES 65536
+
 /* Layout-identical to cv::KeyPoint {Point2f pt; float size, angle, response; int octave, class_id;} */
 typedef struct {
     float x, y, size, angle, response;
@@ -134,6 +141,9 @@ orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n);
  * reference order (vToDistributeKeys); cand_counts[l]. */
 orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t out_size);
 orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys, int cap, int* n);
+/* blurred: GaussianBlur(level, 7x7, 2, BORDER_REFLECT_101) of every level (src/ORBextractor.cc:1300-1306,
+ * the image rBRIEF samples), concatenated w_l*h_l like the pyramid dump. */
+orbx_status orbx_debug_blurred(orbx_handle* h, int frame, uint8_t* out, size_t out_size);
 /* Kernel launches per stage of one batched extract of `batch` frames of rows x cols (measurement
  * hook: per-launch roofline figures): counts[0] pyramid, [1] FAST, [2] quadtree, [3] describe;
  * counts[4]: bit l set if a pyramid launch reads level l. */
@@ -306,7 +316,7 @@ typedef struct {
 
 /* Batched device path: `npairs` searches; d_view1 / d_view2 / d_tp are device arrays of
  * the structs above whose pointers are device pointers (d_tp only for
- * ORBM_TRIANGULATION).  max_nodes1 >= every view1 fv_nnodes; every view2.n <= 8192.  Outputs d_match[p *
+ * ORBM_TRIANGULATION).  max_nodes1 >= every view1 fv_nnodes; every view2.n <= ORBM_MAX_FEATURES.  Outputs d_match[p *
  * match_stride + i] (i < view2.n for ORBM_BOW_KF_F, view1.n otherwise) and
  * d_nmatches[p].  nnratio = ORBmatcher::mfNNratio, check_ori = mbCheckOrientation.
  * Asynchronous on `stream`. */
@@ -341,7 +351,7 @@ typedef struct {
  * d_claimed (F.mvpMapPoints[i] && Observations() > 0) at f * cap; d_npts[f] MapPoints and their
  * descriptors at f * pcap.  Outputs d_match[f * cap + i] = the MapPoint (index) this call
  * assigned to feature i, -1 (the last one when it overwrote), and d_nmatches[f] (the
- * reference's return value).  cap <= 8192.  Asynchronous on `stream`. */
+ * reference's return value).  cap <= ORBM_MAX_FEATURES.  Asynchronous on `stream`. */
 orbx_status orbm_search_by_projection_device(const orbx_keypoint* d_kps, const uint8_t* d_desc, const float* d_uright,
                                              const uint8_t* d_claimed, const int* d_counts, int nframes, int cap,
                                              const orbm_proj_point* d_pts, const uint8_t* d_pdesc, const int* d_npts,
@@ -407,7 +417,7 @@ typedef struct {
  * Search modes: d_match[f * cap + i] = the MapPoint this call assigned to feature i (the last one),
  * -1 untouched, -2 set to NULL by the rotation filter; d_nmatches[f] = the reference's return value.
  * Fuse modes: d_match[f * pcap + m] = the feature MapPoint m fuses into (bestDist <= TH_LOW), -1;
- * d_nmatches[f] = nFused.  cap <= 8192.  Asynchronous on `stream`. */
+ * d_nmatches[f] = nFused.  cap <= ORBM_MAX_FEATURES.  Asynchronous on `stream`. */
 orbx_status orbm_project_search_device(int mode, const orbx_keypoint* d_kps, const uint8_t* d_desc,
                                        const float* d_uright, const uint8_t* d_claimed, const int* d_counts,
                                        int nframes, int cap, const float* d_pose, const orbm_map_point* d_pts,
@@ -463,7 +473,7 @@ orbx_status orbv_info(const orbx_vocabulary* v, int* k, int* L, int* scoring, in
                       int* nwords);
 
 /* TemplatedVocabulary::transform(features, BowVector&, FeatureVector&, levelsup) (:1125-1259) for
- * one host descriptor set (n <= 8192).  BowVector: bow_n words ascending with their weights
+ * one host descriptor set (n <= ORBV_MAX_FEATURES).  BowVector: bow_n words ascending with their weights
  * (n entries of room); FeatureVector as CSR: fv_nnodes node ids ascending, fv_ptr (n + 1),
  * fv_idx (n).  Synchronous. */
 orbx_status orbv_transform(const orbx_vocabulary* v, const uint8_t* desc, int n, int levelsup, int32_t* bow_word,
@@ -471,7 +481,7 @@ orbx_status orbv_transform(const orbx_vocabulary* v, const uint8_t* desc, int n,
                            int* fv_nnodes);
 
 /* Batched device path over an extract batch (d_desc [nframes][cap][32], d_counts[nframes],
- * cap <= 8192).  Per frame f: d_bow_word / d_bow_weight / d_fv_node / d_fv_idx at f * cap,
+ * cap <= ORBV_MAX_FEATURES).  Per frame f: d_bow_word / d_bow_weight / d_fv_node / d_fv_idx at f * cap,
  * d_fv_ptr at f * (cap + 1), counts d_bow_n[f] / d_fv_nnodes[f].  The FeatureVector CSR
  * plugs straight into orbm_bow_view.  Asynchronous on `stream`. */
 orbx_status orbv_transform_batch_device(const orbx_vocabulary* v, const uint8_t* d_desc, const int* d_counts,

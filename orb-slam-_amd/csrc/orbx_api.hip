@@ -140,6 +140,7 @@ struct orbx_handle {
     // batch workspace
     int batch_cap = 0;
     uint8_t* d_pyr = nullptr;
+    uint8_t* d_blur = nullptr;   // K1b blurred levels
     uint32_t* d_slots = nullptr;
     int* d_cell_counts = nullptr;
     uint32_t* d_spill = nullptr;
@@ -388,6 +389,7 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     std::vector<int4> pyrbt;
     if (!pyr_plan(g, yt.data(), pyrbt)) return ORBX_EINVAL;
     fast_groups(g);
+    blur_plan(g);
     g.slots_per_frame = (slot + 31) & ~31;   // frames' slot blocks start on 128-byte lines
     g.out_per_frame = out;
     g.max_cells_level = maxcells;
@@ -445,7 +447,8 @@ orbx_status ensure_batch(orbx_handle* h, int batch)
     if (batch <= h->batch_cap) return ORBX_OK;
     const Geometry& g = h->geom;
     const size_t B = (size_t)batch;
-    if (!dalloc(h, h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h, h->d_slots, (size_t)g.slots_per_frame * B) ||
+    if (!dalloc(h, h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h, h->d_blur, (size_t)g.bl_bytes * B) ||
+        !dalloc(h, h->d_slots, (size_t)g.slots_per_frame * B) ||
         !dalloc(h, h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h, h->d_spill, (size_t)g.spill_per_frame * B) ||
         !dalloc(h, h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h, h->d_qt_out, (size_t)g.out_per_frame * B) ||
         !dalloc(h, h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h, h->d_status, 16) ||
@@ -473,6 +476,7 @@ ExtractBufs bufs(orbx_handle* h)
     b.qt_out = h->d_qt_out;
     b.qt_cnt = h->d_qt_cnt;
     b.status = h->d_status;
+    b.blur = h->d_blur;
     return b;
 }
 
@@ -525,6 +529,7 @@ void enqueue_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoi
     if (ev) hipEventRecord(ev[2], s);
     launch_quadtree(g, b, counts, batch, s);
     if (ev) hipEventRecord(ev[3], s);
+    launch_blur(g, b, P, batch, s);
     launch_describe(g, b, P, kps, desc, cap, batch, s);
     if (ev) hipEventRecord(ev[4], s);
 }
@@ -604,6 +609,7 @@ void orbx_destroy(orbx_handle* h)
         dfree(b.d_pyrbt);
     }
     dfree(h->d_pyr);
+    dfree(h->d_blur);
     dfree(h->d_slots);
     dfree(h->d_cell_counts);
     dfree(h->d_spill);
@@ -761,7 +767,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     };
     // Replayed as a hipGraph: one submission instead of ~17 (launch overhead is most of a 640x480 frame's
     // latency).  The graph is re-captured when any buffer or size it holds changes.
-    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
+    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_blur, h->d_slots, h->d_cell_counts, h->d_spill,
                                           h->d_spill_node, h->d_qt_nodes, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
                                           h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
@@ -903,6 +909,7 @@ orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* 
         launch_quadtree(g, b, d_counts, batch, s);
         break;
     default:
+        launch_blur(g, b, P, batch, s);
         launch_describe(g, b, P, d_kps, d_desc, cap, batch, s);
         h->last = P;
         h->last_batch = batch;
@@ -974,6 +981,22 @@ orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t o
             sp = (size_t)L.pitch;
         }
         hipMemcpy2DAsync(out + o, L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, own_stream(h));
+        o += (size_t)L.w * L.h;
+    }
+    return hipStreamSynchronize(own_stream(h)) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
+}
+
+orbx_status orbx_debug_blurred(orbx_handle* h, int frame, uint8_t* out, size_t out_size)
+{
+    if (!h || !out || frame < 0 || frame >= h->last_batch || !h->d_blur) return ORBX_EINVAL;
+    DeviceGuard guard(h->device);
+    order_after_last(h, own_stream(h));
+    size_t o = 0;
+    for (int l = 0; l < h->geom.nlevels; ++l) {
+        const LevelGeom& L = h->geom.lv[l];
+        if (o + (size_t)L.w * L.h > out_size) return ORBX_ENOSPC;
+        const uint8_t* src = h->d_blur + (size_t)frame * (size_t)h->geom.bl_bytes + L.bl_off;
+        hipMemcpy2DAsync(out + o, L.w, src, (size_t)L.pitch, L.w, L.h, hipMemcpyDeviceToHost, own_stream(h));
         o += (size_t)L.w * L.h;
     }
     return hipStreamSynchronize(own_stream(h)) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
@@ -1154,7 +1177,7 @@ namespace {
 
 bool bow_view_ok(const orbm_bow_view* v)
 {
-    if (!v || v->n < 0 || v->fv_nnodes < 0 || v->n > 8192) return false;
+    if (!v || v->n < 0 || v->fv_nnodes < 0 || v->n > ORBM_MAX_FEATURES) return false;
     if (v->n > 0 && (!v->kps || !v->desc)) return false;
     if (v->fv_nnodes > 0 && (!v->fv_node || !v->fv_ptr || !v->fv_idx)) return false;
     for (int k = 0; k < v->fv_nnodes; ++k) {
@@ -1242,7 +1265,7 @@ orbx_status orbm_search_by_projection_device(const orbx_keypoint* d_kps, const u
                                              int pcap, const orbm_proj_params* params, int* d_match,
                                              int* d_nmatches, void* stream)
 {
-    if (!d_kps || !d_desc || !d_uright || !d_claimed || !d_counts || nframes < 0 || cap <= 0 || cap > 8192 ||
+    if (!d_kps || !d_desc || !d_uright || !d_claimed || !d_counts || nframes < 0 || cap <= 0 || cap > ORBM_MAX_FEATURES ||
         !d_pts || !d_pdesc || !d_npts || pcap <= 0 || !params || !d_match || !d_nmatches)
         return ORBX_EINVAL;
     if (nframes == 0) return ORBX_OK;
@@ -1259,7 +1282,7 @@ orbx_status orbm_search_by_projection(int device, const orbx_keypoint* kps, cons
                                       const uint8_t* claimed, int n, const orbm_proj_point* pts, const uint8_t* pdesc,
                                       int np, const orbm_proj_params* params, int* match, int* nmatches)
 {
-    if (n < 0 || n > 8192 || np < 0 || !params || !nmatches) return ORBX_EINVAL;
+    if (n < 0 || n > ORBM_MAX_FEATURES || np < 0 || !params || !nmatches) return ORBX_EINVAL;
     *nmatches = 0;
     if (n == 0) return ORBX_OK;
     if (!kps || !desc || !uright || !claimed || !match || (np > 0 && (!pts || !pdesc))) return ORBX_EINVAL;
@@ -1298,7 +1321,7 @@ orbx_status orbm_project_search_device(int mode, const orbx_keypoint* d_kps, con
                                        const orbm_pose_params* params, int* d_match, int* d_nmatches, void* stream)
 {
     if (mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_FUSE_SIM3 || !d_kps || !d_desc || !d_uright || !d_claimed ||
-        !d_counts || nframes < 0 || cap <= 0 || cap > 8192 || !d_pose || !d_pts || !d_pdesc || !d_npts ||
+        !d_counts || nframes < 0 || cap <= 0 || cap > ORBM_MAX_FEATURES || !d_pose || !d_pts || !d_pdesc || !d_npts ||
         pcap <= 0 || !params || !d_match || !d_nmatches || params->nlevels < 1 || params->nlevels > 16)
         return ORBX_EINVAL;
     if (nframes == 0) return ORBX_OK;
@@ -1316,7 +1339,7 @@ orbx_status orbm_project_search(int device, int mode, const orbx_keypoint* kps, 
                                 const orbm_map_point* pts, const uint8_t* pdesc, int np,
                                 const orbm_pose_params* params, int* match, int* nmatches)
 {
-    if (mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_FUSE_SIM3 || n < 0 || n > 8192 || np < 0 || !params ||
+    if (mode < ORBM_PROJ_LAST_FRAME || mode > ORBM_FUSE_SIM3 || n < 0 || n > ORBM_MAX_FEATURES || np < 0 || !params ||
         !nmatches || !pose || params->nlevels < 1 || params->nlevels > 16)
         return ORBX_EINVAL;
     const bool search = mode <= ORBM_PROJ_SIM3;

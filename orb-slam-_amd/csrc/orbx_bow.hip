@@ -21,7 +21,7 @@
 
 namespace orbx {
 
-constexpr int kBowMaxCand = 8192;                  // view2 features per node (LDS bitmap per wave)
+constexpr int kBowMaxCand = ORBM_MAX_FEATURES;     // view2 features per node (LDS bitmap per wave, 2 KiB)
 constexpr int kBowWords = kBowMaxCand / 32;
 constexpr int kTH_LOW = 50, kHisto = 30;
 

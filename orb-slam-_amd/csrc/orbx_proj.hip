@@ -369,19 +369,32 @@ struct ReplayLds {
     int* hist;        // [32] rotHist sizes
 };
 
-__device__ __forceinline__ ReplayLds replay_lds(int cap)
+// kBig (frames of more than kReplayLdsCap features): `mo` is the frame's output row in global memory (the
+// last-writer atomics go to it directly, and the final copy is in place), the rest stays in LDS: 9 bytes per
+// feature instead of 13, so up to kProjMaxFeatures features fit a workgroup's 160 KiB.
+constexpr int kReplayLdsCap = 8192;
+template <bool kBig>
+__device__ __forceinline__ ReplayLds replay_lds(int cap, int* mo_global)
 {
     extern __shared__ int s_replay[];
     ReplayLds S;
-    S.mo = s_replay;
-    S.bins = reinterpret_cast<uint32_t*>(s_replay + cap);
-    S.first = s_replay + 2 * cap;
-    S.hist = s_replay + 3 * cap;
-    S.taken = reinterpret_cast<uint8_t*>(s_replay + 3 * cap + 32);
+    if constexpr (kBig) {
+        S.mo = mo_global;
+        S.bins = reinterpret_cast<uint32_t*>(s_replay);
+        S.first = s_replay + cap;
+        S.hist = s_replay + 2 * cap;
+        S.taken = reinterpret_cast<uint8_t*>(s_replay + 2 * cap + 32);
+    } else {
+        S.mo = s_replay;
+        S.bins = reinterpret_cast<uint32_t*>(s_replay + cap);
+        S.first = s_replay + 2 * cap;
+        S.hist = s_replay + 3 * cap;
+        S.taken = reinterpret_cast<uint8_t*>(s_replay + 3 * cap + 32);
+    }
     return S;
 }
 
-inline size_t replay_lds_bytes(int cap) { return (size_t)13 * cap + 128; }
+inline size_t replay_lds_bytes(int cap) { return cap > kReplayLdsCap ? (size_t)9 * cap + 128 : (size_t)13 * cap + 128; }
 
 struct ReplayPick {
     int g, accept, bin;
@@ -479,6 +492,7 @@ __device__ __forceinline__ int replay_chunks(int n, int np, const TopResult* __r
     return count;
 }
 
+template <bool kBig>
 __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restrict__ kps,
                                                    const uint8_t* __restrict__ desc, const float* __restrict__ uright,
                                                    const uint8_t* __restrict__ claimed, const int* __restrict__ counts,
@@ -490,7 +504,8 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
 {
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(counts[f], cap), np = min(npts[f], pcap);
-    const ReplayLds S = replay_lds(cap);
+    int* Mo = match + (size_t)f * cap;
+    const ReplayLds S = replay_lds<kBig>(cap, Mo);
     const uint32_t* keys = gkeys + (size_t)f * pj_grid_stride(cap);
     const orbx_keypoint* K = kps + (size_t)f * cap;
     const float* U = uright + (size_t)f * cap;
@@ -538,8 +553,8 @@ __global__ __launch_bounds__(64) void k_pj_resolve(const orbx_keypoint* __restri
         return pk;
     };
     const int count = replay_chunks<true, false>(n, np, res + (size_t)f * pcap, S, obs_of, accept_of, rescan);
-    int* Mo = match + (size_t)f * cap;
-    for (int i = lane; i < n; i += 64) Mo[i] = S.mo[i];
+    if constexpr (!kBig)
+        for (int i = lane; i < n; i += 64) Mo[i] = S.mo[i];
     if (lane == 0) nmatches[f] = count;
 }
 
@@ -559,10 +574,13 @@ void launch_proj(const orbx_keypoint* kps, const uint8_t* desc, const float* uri
     launch_pj_grid(kps, counts, nframes, cap, P.min_x, P.min_y, P.grid_w_inv, P.grid_h_inv, gkeys, gn, s);
     hipLaunchKernelGGL(k_pj_points, dim3((pcap + 256 / kSub - 1) / (256 / kSub), nframes), dim3(256), 0, s, kps, desc,
                        uright, claimed, cap, pts, pdesc, npts, pcap, P, gkeys, gn, res);
-    hipFuncSetAttribute((const void*)k_pj_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)replay_lds_bytes(cap));
-    hipLaunchKernelGGL(k_pj_resolve, dim3(nframes), dim3(64), replay_lds_bytes(cap), s, kps, desc, uright, claimed,
-                       counts, cap, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+    auto resolve = [&](auto kern) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)replay_lds_bytes(cap));
+        hipLaunchKernelGGL(kern, dim3(nframes), dim3(64), replay_lds_bytes(cap), s, kps, desc, uright, claimed, counts,
+                           cap, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+    };
+    if (cap > kReplayLdsCap) resolve(k_pj_resolve<true>);
+    else resolve(k_pj_resolve<false>);
 }
 
 // =====================================================================================
@@ -851,7 +869,7 @@ __global__ __launch_bounds__(256) void k_ps_points(const orbx_keypoint* __restri
     }
 }
 
-template <int MODE>
+template <int MODE, bool kBig>
 __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restrict__ kps,
                                                    const uint8_t* __restrict__ desc, const float* __restrict__ uright,
                                                    const uint8_t* __restrict__ claimed, const int* __restrict__ counts,
@@ -865,7 +883,8 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
     constexpr bool kRotMode = MODE == ORBM_PROJ_LAST_FRAME || MODE == ORBM_PROJ_KEYFRAME;
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(counts[f], cap), np = min(npts[f], pcap);
-    const ReplayLds S = replay_lds(cap);
+    int* Mo = match + (size_t)f * cap;
+    const ReplayLds S = replay_lds<kBig>(cap, Mo);
     const uint32_t* keys = gkeys + (size_t)f * pj_grid_stride(cap);
     const orbx_keypoint* K = kps + (size_t)f * cap;
     const float* U = uright + (size_t)f * cap;
@@ -928,8 +947,7 @@ __global__ __launch_bounds__(64) void k_ps_resolve(const orbx_keypoint* __restri
         for (int i = 0; i < 30; ++i)
             if ((drop >> i) & 1u) count -= S.hist[i];
     }
-    int* Mo = match + (size_t)f * cap;
-    for (int i = lane; i < n; i += 64) Mo[i] = (S.bins[i] & drop) ? -2 : S.mo[i];   // NULL-ed by the filter
+    for (int i = lane; i < n; i += 64) Mo[i] = (S.bins[i] & drop) ? -2 : S.mo[i];   // NULL-ed by the filter (in place when kBig)
     if (lane == 0) nmatches[f] = count;
 }
 
@@ -950,10 +968,13 @@ static void ps_launch(const orbx_keypoint* kps, const uint8_t* desc, const float
                        kps, desc, uright,
                        claimed, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
     if (MODE <= ORBM_PROJ_SIM3) {
-        hipFuncSetAttribute((const void*)k_ps_resolve<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)replay_lds_bytes(cap));
-        hipLaunchKernelGGL(k_ps_resolve<MODE>, dim3(nframes), dim3(64), replay_lds_bytes(cap), s, kps, desc, uright,
-                           claimed, counts, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+        auto resolve = [&](auto kern) {
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)replay_lds_bytes(cap));
+            hipLaunchKernelGGL(kern, dim3(nframes), dim3(64), replay_lds_bytes(cap), s, kps, desc, uright, claimed,
+                               counts, cap, pose, pts, pdesc, npts, pcap, P, gkeys, gn, res, match, nmatches);
+        };
+        if (cap > kReplayLdsCap) resolve(k_ps_resolve<MODE, true>);
+        else resolve(k_ps_resolve<MODE, false>);
     }
 }
 

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_voc_descend(const int* __restrict__ cbe
     out_nid[o] = nid;
 }
 
-__device__ void voc_bitonic_u64(unsigned long long* k, int p2)
+__device__ __forceinline__ void voc_bitonic_u64(unsigned long long* k, int p2)
 {
     for (int size = 2; size <= p2; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -120,15 +120,19 @@ __device__ int voc_scan(int* s_tmp, int v)
 
 constexpr int kVocNT = 512;
 
+// kG: frames whose p2 keys and weights (16 bytes each) outgrow a workgroup's LDS sort them in a per-frame
+// global scratch region of p2max entries (the same network; only the memory differs)
+template <bool kG>
 __global__ __launch_bounds__(kVocNT) void k_voc_vectors(const int* __restrict__ counts, int cap, int scoring,
                                                         int weighting, const int* __restrict__ fword,
                                                         const double* __restrict__ fw, const int* __restrict__ fnid,
                                                         int* __restrict__ bow_word, double* __restrict__ bow_weight,
                                                         int* __restrict__ bow_n, int* __restrict__ fv_node,
                                                         int* __restrict__ fv_ptr, int* __restrict__ fv_idx,
-                                                        int* __restrict__ fv_nn)
+                                                        int* __restrict__ fv_nn, unsigned long long* __restrict__ gsort,
+                                                        int p2max)
 {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_key[];
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_dyn[];
     __shared__ int s_tmp[kVocNT];
     __shared__ int s_total, s_run;
     __shared__ double s_norm;
@@ -136,6 +140,7 @@ __global__ __launch_bounds__(kVocNT) void k_voc_vectors(const int* __restrict__ 
     const int n = min(counts[fr], cap);
     int p2 = 1;
     while (p2 < n) p2 <<= 1;
+    unsigned long long* s_key = kG ? gsort + (size_t)fr * 2 * p2max : s_dyn;
     double* s_w = reinterpret_cast<double*>(s_key + p2);   // [p2] BowVector weights
     const size_t base = (size_t)fr * cap;
     const unsigned long long kNone = ~0ull;
@@ -348,28 +353,39 @@ orbx_status orbv_transform_batch_device(const orbx_vocabulary* v, const uint8_t*
                                         double* d_bow_weight, int* d_bow_n, int32_t* d_fv_node, int32_t* d_fv_ptr,
                                         int32_t* d_fv_idx, int* d_fv_nnodes, void* stream)
 {
-    if (!v || !d_desc || !d_counts || nframes < 0 || cap <= 0 || cap > 8192 || !d_bow_word || !d_bow_weight ||
+    if (!v || !d_desc || !d_counts || nframes < 0 || cap <= 0 || cap > ORBV_MAX_FEATURES || !d_bow_word || !d_bow_weight ||
         !d_bow_n || !d_fv_node || !d_fv_ptr || !d_fv_idx || !d_fv_nnodes)
         return ORBX_EINVAL;
     if (nframes == 0) return ORBX_OK;
     orbx::DeviceGuard guard(v->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t nf = (size_t)nframes * cap;
+    int p2 = 1;
+    while (p2 < cap) p2 <<= 1;
+    // sort keys + weights: in LDS up to 8192 features (128 KiB), else in global scratch
+    const bool glob = (size_t)p2 * 16 > 128 * 1024;
     void* scratch = nullptr;
-    if (hipMallocAsync(&scratch, nf * (4 + 8 + 4), s) != hipSuccess) return ORBX_ENOMEM;
-    double* fw = (double*)scratch;
+    const size_t sort_b = glob ? (size_t)nframes * p2 * 16 : 0;
+    if (hipMallocAsync(&scratch, sort_b + nf * (4 + 8 + 4), s) != hipSuccess) return ORBX_ENOMEM;
+    unsigned long long* gsort = (unsigned long long*)scratch;
+    double* fw = (double*)((uint8_t*)scratch + sort_b);
     int* fword = (int*)(fw + nf);
     int* fnid = fword + nf;
     hipLaunchKernelGGL(orbx::k_voc_descend, dim3((cap + 255) / 256, nframes), dim3(256), 0, s, v->d_cbegin,
                        v->d_child, v->d_desc, v->d_word, v->d_weight, v->L - levelsup, d_desc, d_counts, cap, fword,
                        fw, fnid);
-    int p2 = 1;
-    while (p2 < cap) p2 <<= 1;
-    const size_t smem = (size_t)p2 * 16;
-    hipFuncSetAttribute((const void*)orbx::k_voc_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL(orbx::k_voc_vectors, dim3(nframes), dim3(orbx::kVocNT), smem, s, d_counts, cap, v->scoring,
-                       v->weighting, fword, fw, fnid, d_bow_word, d_bow_weight, d_bow_n, d_fv_node, d_fv_ptr, d_fv_idx,
-                       d_fv_nnodes);
+    if (glob) {
+        hipLaunchKernelGGL(orbx::k_voc_vectors<true>, dim3(nframes), dim3(orbx::kVocNT), 0, s, d_counts, cap,
+                           v->scoring, v->weighting, fword, fw, fnid, d_bow_word, d_bow_weight, d_bow_n, d_fv_node,
+                           d_fv_ptr, d_fv_idx, d_fv_nnodes, gsort, p2);
+    } else {
+        const size_t smem = (size_t)p2 * 16;
+        hipFuncSetAttribute((const void*)orbx::k_voc_vectors<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)smem);
+        hipLaunchKernelGGL(orbx::k_voc_vectors<false>, dim3(nframes), dim3(orbx::kVocNT), smem, s, d_counts, cap,
+                           v->scoring, v->weighting, fword, fw, fnid, d_bow_word, d_bow_weight, d_bow_n, d_fv_node,
+                           d_fv_ptr, d_fv_idx, d_fv_nnodes, gsort, p2);
+    }
     hipFreeAsync(scratch, s);
     return hipGetLastError() == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
 }
@@ -378,7 +394,7 @@ orbx_status orbv_transform(const orbx_vocabulary* v, const uint8_t* desc, int n,
                            double* bow_weight, int* bow_n, int32_t* fv_node, int32_t* fv_ptr, int32_t* fv_idx,
                            int* fv_nnodes)
 {
-    if (!v || n < 0 || n > 8192 || !bow_n || !fv_nnodes || !fv_ptr) return ORBX_EINVAL;
+    if (!v || n < 0 || n > ORBV_MAX_FEATURES || !bow_n || !fv_nnodes || !fv_ptr) return ORBX_EINVAL;
     *bow_n = 0;
     *fv_nnodes = 0;
     fv_ptr[0] = 0;
