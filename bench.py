@@ -127,7 +127,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # per SIMD), plain ALU ops (v_xor_b32, v_fma_f32) once per 2 (about 990-1050).  A kernel's VALU fraction is taken
 # against the measured rate of its dominant instruction.
 VALU_RATES = os.path.join(ROOT, "profiles", "r02", "valu_rate.json")
-VALU_DOMINANT = {"k_fast_cells": "v_pk_maximum3_f16", "k_blur_levels+k_describe": "v_dot4_u32_u8", "k_pyramid_level": "v_dot4_u32_u8",
+VALU_DOMINANT = {"k_fast_cells": "v_pk_maximum3_f16", "k_describe": "v_dot4_u32_u8", "k_pyramid_level": "v_dot4_u32_u8",
                  "k_quadtree<512,16|512,8|256,4>": "v_xor_b32", "k_si_grid+k_si_build+k_si_greedy": "v_bcnt_u32_b32"}
 
 
@@ -547,10 +547,9 @@ def main():
         "pyramid": B * (sum(A[l] for l in range(NLEVELS) if n_launch["pyramid_sources"] >> l & 1) + sum(A[1:])),
         "fast": B * (sum(A) + 4 * cand),
         "quadtree": B * (4 * cand + 4 * kept),
-        # the stage is K1b (GaussianBlur of every level) + K4: every level pixel read once (the blur and
-        # IC_Angle's discs), every blurred pixel written once and read once (BRIEF's patches overlap), the
-        # packed keypoint in, the 28 B keypoint + 32 B descriptor out
-        "describe": B * (3 * sum(A) + kept * (4 + 60)),
+        # compulsory bytes: every level pixel once (patches overlap), the packed keypoint in,
+        # the 28 B keypoint + 32 B descriptor out
+        "describe": B * (sum(A) + kept * (4 + 60)),
         "match": (B - 1) * 2 * kept * 60,
     }
     def roofline(st):
@@ -563,9 +562,9 @@ def main():
         achieved = alg[dom] / launches / t_launch / 1e9
         qk = "k_quadtree"
         kname = {"pyramid": "k_pyramid_level", "fast": "k_fast_cells", "quadtree": qk + "<512,16|512,8|256,4>",
-                 "describe": "k_blur_levels+k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
+                 "describe": "k_describe", "match": "k_si_grid+k_si_build+k_si_greedy"}[dom]
         # stages made of several kernels: their per-launch counters add up
-        PARTS = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"], "describe": ["k_blur_levels", "k_describe"],
+        PARTS = {"match": ["k_si_grid", "k_si_build", "k_si_greedy"],
                  "quadtree": [qk + "<512, 16", qk + "<512, 8", qk + "<256, 4"]}
 
         def per_launch(K, dom, kname, field):

@@ -141,9 +141,6 @@ orbx_status orbx_get_stage_times(orbx_handle* h, float* ms, int n);
  * reference order (vToDistributeKeys); cand_counts[l]. */
 orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t out_size);
 orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys, int cap, int* n);
-/* blurred: GaussianBlur(level, 7x7, 2, BORDER_REFLECT_101) of every level (src/ORBextractor.cc:1300-1306,
- * the image rBRIEF samples), concatenated w_l*h_l like the pyramid dump. */
-orbx_status orbx_debug_blurred(orbx_handle* h, int frame, uint8_t* out, size_t out_size);
 /* Kernel launches per stage of one batched extract of `batch` frames of rows x cols (measurement
  * hook: per-launch roofline figures): counts[0] pyramid, [1] FAST, [2] quadtree, [3] describe;
  * counts[4]: bit l set if a pyramid launch reads level l. */

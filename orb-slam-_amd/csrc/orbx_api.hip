@@ -140,7 +140,6 @@ struct orbx_handle {
     // batch workspace
     int batch_cap = 0;
     uint8_t* d_pyr = nullptr;
-    uint8_t* d_blur = nullptr;   // K1b blurred levels
     uint32_t* d_slots = nullptr;
     int* d_cell_counts = nullptr;
     uint32_t* d_spill = nullptr;
@@ -389,7 +388,6 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     std::vector<int4> pyrbt;
     if (!pyr_plan(g, yt.data(), pyrbt)) return ORBX_EINVAL;
     fast_groups(g);
-    blur_plan(g);
     g.slots_per_frame = (slot + 31) & ~31;   // frames' slot blocks start on 128-byte lines
     g.out_per_frame = out;
     g.max_cells_level = maxcells;
@@ -447,8 +445,7 @@ orbx_status ensure_batch(orbx_handle* h, int batch)
     if (batch <= h->batch_cap) return ORBX_OK;
     const Geometry& g = h->geom;
     const size_t B = (size_t)batch;
-    if (!dalloc(h, h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h, h->d_blur, (size_t)g.bl_bytes * B) ||
-        !dalloc(h, h->d_slots, (size_t)g.slots_per_frame * B) ||
+    if (!dalloc(h, h->d_pyr, (size_t)g.pyr_bytes * B) || !dalloc(h, h->d_slots, (size_t)g.slots_per_frame * B) ||
         !dalloc(h, h->d_cell_counts, (size_t)g.ncells * B) || !dalloc(h, h->d_spill, (size_t)g.spill_per_frame * B) ||
         !dalloc(h, h->d_spill_node, (size_t)g.spill_per_frame * B) || !dalloc(h, h->d_qt_out, (size_t)g.out_per_frame * B) ||
         !dalloc(h, h->d_qt_cnt, (size_t)g.nlevels * B) || !dalloc(h, h->d_status, 16) ||
@@ -476,7 +473,6 @@ ExtractBufs bufs(orbx_handle* h)
     b.qt_out = h->d_qt_out;
     b.qt_cnt = h->d_qt_cnt;
     b.status = h->d_status;
-    b.blur = h->d_blur;
     return b;
 }
 
@@ -529,7 +525,6 @@ void enqueue_pipeline(orbx_handle* h, const FramePtrs& P, int batch, orbx_keypoi
     if (ev) hipEventRecord(ev[2], s);
     launch_quadtree(g, b, counts, batch, s);
     if (ev) hipEventRecord(ev[3], s);
-    launch_blur(g, b, P, batch, s);
     launch_describe(g, b, P, kps, desc, cap, batch, s);
     if (ev) hipEventRecord(ev[4], s);
 }
@@ -609,7 +604,6 @@ void orbx_destroy(orbx_handle* h)
         dfree(b.d_pyrbt);
     }
     dfree(h->d_pyr);
-    dfree(h->d_blur);
     dfree(h->d_slots);
     dfree(h->d_cell_counts);
     dfree(h->d_spill);
@@ -767,7 +761,7 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     };
     // Replayed as a hipGraph: one submission instead of ~17 (launch overhead is most of a 640x480 frame's
     // latency).  The graph is re-captured when any buffer or size it holds changes.
-    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_blur, h->d_slots, h->d_cell_counts, h->d_spill,
+    const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
                                           h->d_spill_node, h->d_qt_nodes, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
                                           h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, (const void*)(uintptr_t)rows,
                                           (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
@@ -909,7 +903,6 @@ orbx_status orbx_extract_stage_device(orbx_handle* h, int stage, const uint8_t* 
         launch_quadtree(g, b, d_counts, batch, s);
         break;
     default:
-        launch_blur(g, b, P, batch, s);
         launch_describe(g, b, P, d_kps, d_desc, cap, batch, s);
         h->last = P;
         h->last_batch = batch;
@@ -981,22 +974,6 @@ orbx_status orbx_debug_pyramid(orbx_handle* h, int frame, uint8_t* out, size_t o
             sp = (size_t)L.pitch;
         }
         hipMemcpy2DAsync(out + o, L.w, src, sp, L.w, L.h, hipMemcpyDeviceToHost, own_stream(h));
-        o += (size_t)L.w * L.h;
-    }
-    return hipStreamSynchronize(own_stream(h)) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;
-}
-
-orbx_status orbx_debug_blurred(orbx_handle* h, int frame, uint8_t* out, size_t out_size)
-{
-    if (!h || !out || frame < 0 || frame >= h->last_batch || !h->d_blur) return ORBX_EINVAL;
-    DeviceGuard guard(h->device);
-    order_after_last(h, own_stream(h));
-    size_t o = 0;
-    for (int l = 0; l < h->geom.nlevels; ++l) {
-        const LevelGeom& L = h->geom.lv[l];
-        if (o + (size_t)L.w * L.h > out_size) return ORBX_ENOSPC;
-        const uint8_t* src = h->d_blur + (size_t)frame * (size_t)h->geom.bl_bytes + L.bl_off;
-        hipMemcpy2DAsync(out + o, L.w, src, (size_t)L.pitch, L.w, L.h, hipMemcpyDeviceToHost, own_stream(h));
         o += (size_t)L.w * L.h;
     }
     return hipStreamSynchronize(own_stream(h)) == hipSuccess ? ORBX_OK : ORBX_EDEVICE;

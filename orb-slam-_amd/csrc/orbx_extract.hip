@@ -42,31 +42,6 @@ __device__ __forceinline__ const uint8_t* level_base(const FramePtrs& P, const G
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
-// GaussianBlur's 7 taps starting at byte `off` of four consecutive raw dwords: the weight bytes of dword d
-__host__ __device__ constexpr uint32_t blur_wshift(int off, int d)
-{
-    constexpr uint32_t k[7] = {18, 34, 49, 55, 49, 34, 18};
-    uint32_t w = 0;
-    for (int b = 0; b < 4; ++b) {
-        const int t = 4 * d + b - off;
-        if (t >= 0 && t < 7) w |= k[t] << (8 * b);
-    }
-    return w;
-}
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b)
-{
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
-}
-
-// BORDER_REFLECT_101 index (OpenCV borderInterpolate): ... 2 1 | 0 1 2 ... n-1 | n-2 n-3 ...
-__device__ __forceinline__ int reflect101_px(int p, int len)
-{
-    if (len == 1) return 0;
-    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
-    return p;
-}
-
 __device__ __forceinline__ ushort2_t as_us2(uint32_t v)
 {
     ushort2_t r;
@@ -565,185 +540,6 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         else
             hipLaunchKernelGGL((k_pyramid_level<false, false>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
     }
-}
-
-// ---------------------------------------------------------------------------
-// K1b: GaussianBlur(level, 7x7, sigma 2, BORDER_REFLECT_101) of every level
-// (src/ORBextractor.cc:1300-1306), OpenCV's u8 fixed-point path: the row pass with the
-// integer kernel k = [18 34 49 55 49 34 18] (getGaussianKernel(7, 2) x 256, rounded), the
-// column pass with the same kernel, (sum + 2^15) >> 16 saturated to u8.
-// The blurred levels feed rBRIEF (K4 samples them directly), so each pixel is blurred once
-// instead of once per keypoint patch that covers it.
-//
-// One wave per (frame, level, band of kBlurRows rows, chunk of 256 columns); a lane owns 4
-// output columns.  The band's rows and 3 more above and below (reflected at the level's
-// edges) are staged in LDS with columns x0 - 4 .. x0 + 259 (reflected likewise), so output
-// column x0 + 4 lane + j reads LDS bytes 4 lane + j + 1 .. + 7: three aligned dwords and
-// a dot4 with the kernel shifted by 1 + j bytes (10 dot4 per row for 4 columns).  A row's
-// 4 sums (<= 255 * 257 < 2^16) are paired with the next row's as u16 pairs, so an output
-// is three v_dot2_u32_u16 and one v_mad_u32_u24 over rows Y .. Y + 6.
-// ---------------------------------------------------------------------------
-constexpr int kBlurRows = kBlurRowsHost;      // output rows per wave
-constexpr int kBlurChunk = kBlurChunkHost;    // output columns per wave
-constexpr int kBlurLD = kBlurChunk / 4 + 2;   // LDS dwords per staged row (columns x0 - 4 .. x0 + 259)
-
-// reflect-101 row of a staged row y in [-3, h + kBlurRows + 2]: exact for -3 <= y <= h + 2 (h >= 4; every level
-// is taller than 2 * EDGE_THRESHOLD); rows further out feed only rows past the level's last, which are not stored
-__device__ __forceinline__ int reflect_row(int y, int h)
-{
-    const int a = y < 0 ? -y : y;
-    return max(min(a, 2 * h - 2 - a), 0);
-}
-
-__global__ __launch_bounds__(64) void k_blur_levels(const Geometry* __restrict__ G, FramePtrs P,
-                                                    uint8_t* __restrict__ out, size_t out_fstride)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t s_t[(kBlurRows + 6) * kBlurLD];
-    const int lane = threadIdx.x;
-    const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-    const int f = lb / gridDim.x, u = lb - f * gridDim.x;
-    int l = 0;   // wave-uniform: the level whose unit range holds u
-    while (l + 1 < G->nlevels && u >= G->lv[l + 1].bl_ub) ++l;
-    const LevelGeom& LG = G->lv[l];
-    const int k = u - LG.bl_ub;
-    const int band = k / LG.bl_nc, chunk = k - band * LG.bl_nc;
-    const int x0 = chunk * kBlurChunk, y0 = band * kBlurRows;
-    const int w = LG.w, h = LG.h;
-    int pitch;
-    const uint8_t* img = level_base(P, G, f, l, pitch);
-
-    // ---- stage: lane loads dword `lane` of each row (columns x0 - 4 + 4 lane ..), lanes 0, 1 also dwords
-    // 64, 65.  Interior dwords are one (possibly unaligned: gfx950 serves it exactly) dword load; a dword
-    // that crosses the level's left or right edge is four reflected byte loads.
-    const int c0 = x0 - 4 + 4 * lane, c1 = x0 + 252 + 4 * lane;
-    const bool in0 = c0 >= 0 && c0 + 3 < w, in1 = lane < 2 && c1 >= 0 && c1 + 3 < w;
-    const bool edge = __builtin_amdgcn_ballot_w64(!in0 || (lane < 2 && !in1)) != 0;   // wave-uniform
-    int rx0[4], rx1[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        rx0[b] = edge ? reflect101_px(c0 + b, w) : 0;
-        rx1[b] = edge ? reflect101_px(c1 + b, w) : 0;
-    }
-    const __attribute__((address_space(1))) uint8_t* gimg = (const __attribute__((address_space(1))) uint8_t*)img;
-    // a batch of rows' loads is issued before any of them is stored (one memory latency per batch, not per row)
-    constexpr int kSR = kBlurRows + 6;
-    if (!edge) {
-        constexpr int RB = (kSR + 1) / 2;
-#pragma unroll
-        for (int r0 = 0; r0 < kSR; r0 += RB) {
-            uint32_t v0[RB], v1[RB];
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                if (r0 + i >= kSR) break;
-                const int y = reflect_row(y0 - 3 + r0 + i, h);   // wave-uniform
-                const __attribute__((address_space(1))) uint8_t* row = gimg + (size_t)y * pitch;
-                v0[i] = *(const __attribute__((address_space(1))) uint32_t*)(row + c0);
-                v1[i] = lane < 2 ? *(const __attribute__((address_space(1))) uint32_t*)(row + c1) : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                if (r0 + i >= kSR) break;
-                s_t[(r0 + i) * kBlurLD + lane] = v0[i];
-                if (lane < 2) s_t[(r0 + i) * kBlurLD + 64 + lane] = v1[i];
-            }
-        }
-    } else {
-        constexpr int RB = 4;
-        for (int r0 = 0; r0 < kSR; r0 += RB) {
-            uint32_t v0[RB], v1[RB];
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                const int y = reflect_row(y0 - 3 + min(r0 + i, kSR - 1), h);
-                const __attribute__((address_space(1))) uint8_t* row = gimg + (size_t)y * pitch;
-                v0[i] = in0 ? *(const __attribute__((address_space(1))) uint32_t*)(row + c0)
-                            : (uint32_t)row[rx0[0]] | (uint32_t)row[rx0[1]] << 8 | (uint32_t)row[rx0[2]] << 16 |
-                                  (uint32_t)row[rx0[3]] << 24;
-                v1[i] = lane >= 2 ? 0u
-                        : in1 ? *(const __attribute__((address_space(1))) uint32_t*)(row + c1)
-                              : (uint32_t)row[rx1[0]] | (uint32_t)row[rx1[1]] << 8 | (uint32_t)row[rx1[2]] << 16 |
-                                    (uint32_t)row[rx1[3]] << 24;
-            }
-#pragma unroll
-            for (int i = 0; i < RB; ++i) {
-                if (r0 + i >= kSR) break;
-                s_t[(r0 + i) * kBlurLD + lane] = v0[i];
-                if (lane < 2) s_t[(r0 + i) * kBlurLD + 64 + lane] = v1[i];
-            }
-        }
-    }
-    wave_lds_sync();
-
-    // ---- rows: 10 dot4 per staged row, u16 row pairs, 4 taps per output
-    __attribute__((address_space(1))) uint8_t* obase =
-        (__attribute__((address_space(1))) uint8_t*)(out + (size_t)f * out_fstride + LG.bl_off + (size_t)y0 * LG.pitch);
-    // columns past the level width: the lane's stores go to the row's pitch padding (pitch = align64(w) >= x0 + 4
-    // lane + 4 whenever x0 + 4 lane < w); lanes entirely past it write the padding's last dword instead
-    const uint32_t ocol = (uint32_t)min(x0 + 4 * lane, LG.pitch - 4);
-    const uint32_t opitch = (uint32_t)LG.pitch;
-    const int nrows = min(kBlurRows, h - y0);   // wave-uniform
-    uint32_t hp[4] = {0u, 0u, 0u, 0u};           // previous staged row's sums
-    uint32_t pr[kBlurRows + 6][4];               // pr[r]: rows (r, r + 1) as u16 pairs
-    constexpr ushort2_t k01 = {18, 34}, k23 = {49, 55}, k45 = {49, 34};
-#pragma unroll
-    for (int r = 0; r < kBlurRows + 6; ++r) {
-        const uint32_t* t = s_t + r * kBlurLD + lane;
-        const uint32_t d0 = t[0], d1 = t[1], d2 = t[2];
-        uint32_t hc[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t acc = 0u;
-            if (blur_wshift(1 + j, 0)) acc = __builtin_amdgcn_udot4(d0, blur_wshift(1 + j, 0), acc, false);
-            if (blur_wshift(1 + j, 1)) acc = __builtin_amdgcn_udot4(d1, blur_wshift(1 + j, 1), acc, false);
-            if (blur_wshift(1 + j, 2)) acc = __builtin_amdgcn_udot4(d2, blur_wshift(1 + j, 2), acc, false);
-            hc[j] = acc;
-        }
-        if (r >= 1) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) pr[r - 1][j] = __builtin_amdgcn_perm(hc[j], hp[j], 0x05040100u);
-        }
-        if (r >= 6) {
-            const int Y = r - 6;   // output row Y: staged rows Y .. Y + 6
-            if (Y < nrows) {
-                uint32_t acc[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    uint32_t a = __builtin_amdgcn_udot2(as_us2(pr[Y][j]), k01, 1u << 15, false);
-                    a = __builtin_amdgcn_udot2(as_us2(pr[Y + 2][j]), k23, a, false);
-                    a = __builtin_amdgcn_udot2(as_us2(pr[Y + 4][j]), k45, a, false);
-                    acc[j] = __umul24(hc[j], 18u) + a;
-                }
-                // min((sum + 2^15) >> 16, 255): bytes 2..3 of each sum as u16 pairs, a packed min, two bytes each
-                const uint32_t t01 = __builtin_amdgcn_perm(acc[1], acc[0], 0x07060302u);
-                const uint32_t t23 = __builtin_amdgcn_perm(acc[3], acc[2], 0x07060302u);
-                const uint32_t m01 = pk_min_u16(t01, 0x00FF00FFu), m23 = pk_min_u16(t23, 0x00FF00FFu);
-                const uint32_t v = __builtin_amdgcn_perm(m23, m01, 0x06040200u);
-                if (x0 + 4 * lane < w) *(__attribute__((address_space(1))) uint32_t*)(obase + (__umul24((uint32_t)Y, opitch) + ocol)) = v;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hp[j] = hc[j];
-    }
-}
-
-void blur_plan(Geometry& g)
-{
-    long long off = 0;
-    int u = 0;
-    for (int l = 0; l < g.nlevels; ++l) {
-        LevelGeom& L = g.lv[l];
-        L.bl_off = off;
-        off += (long long)L.pitch * L.h;
-        L.bl_ub = u;
-        L.bl_nc = (L.w + kBlurChunk - 1) / kBlurChunk;
-        u += L.bl_nc * ((L.h + kBlurRows - 1) / kBlurRows);
-    }
-    g.bl_bytes = (off + 255) & ~255LL;
-    g.bl_units = u;
-}
-
-void launch_blur(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_blur_levels, dim3(g.bl_units, batch), dim3(64), 0, s, b.geom, p, b.blur, (size_t)g.bl_bytes);
 }
 
 // ---------------------------------------------------------------------------
@@ -2293,7 +2089,7 @@ bool qt_prepare(Geometry& g)
     // a level's own node list decides; a group whose shared capacity outgrows LDS moves to global too
     for (int l = 0; l < g.nlevels; ++l) {
         const int lc = g.lv[l].cap + 4;
-        const int kpn = qt_kpn(qt_nt(g, l), qt_kpt(g, l), 0);
+        const int kpn = qt_kpn(l == 0 ? 512 : 256, l == 0 ? g.qt_kpt0 : 4, 0);
         g.lv[l].qt_glob = lc > kQtLdsMaxList || qt_layout(lc, g.lv[l].ncells, 2, kpn).total > kQtLdsMax;
         g.lv[l].qtg_off = g.lv[l].qtg_bytes = 0;
     }
@@ -2357,27 +2153,58 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 
 // ---------------------------------------------------------------------------
 // K4: a wave describes kDescPerWave consecutive retained keypoints.
-//   angle IC_Angle: u*I and v*I over the 749-pixel disc of the level image as per-lane column
-//         sums (lane = disc row half), wave reduction, then cv::fastAtan2 and sincosf once per
-//         wave with lane j on keypoint j (src/ORBextractor.cc:84-128).
-//   patch the keypoint's 37 x 37 neighbourhood of the blurred level (K1b) in LDS by LDS-DMA
-//         (global_load_lds_dwordx4: 16-byte pieces, three per 48-byte row; the blurred levels'
-//         rows start 64-byte aligned, so every row has the same byte shift).  Two buffers: the
-//         next keypoint's patch lands while this one's tests run.
-//   BRIEF fmaf sample coordinates, 256 tests of two blurred bytes each -> four
-//         __ballot words = the descriptor's little-endian u64 words (:141-192).
-// A keypoint lies 19 .. size - 20 px inside its level (FAST's cell windows, :932-1000) and the
-// pattern's rotated samples within 18.39 px of it, so every sample and the whole IC_Angle disc are
-// inside the level: no border case.
+//   raw   the 43-row neighbourhood of the keypoint in LDS, 48 B per row.
+//         Interior keypoints arrive by LDS-DMA (global_load_lds_dwordx4: three
+//         instructions of 16-byte pieces, three per row, so row r starts at
+//         byte sh_r = (src + r*pitch) & 3 of its LDS row);
+//         border keypoints are filled with reflect-101 bytes at shift 0.  The next keypoint's DMA is issued as soon as the
+//         current one's raw reads are done, so it lands under the BRIEF work.
+//   angle IC_Angle: u*I and v*I over the 749-pixel disc as per-lane column
+//         sums (lane = disc column, half-wave = upper/lower rows), wave
+//         reduction, then cv::fastAtan2 (src/ORBextractor.cc:84-128).
+//   blur  GaussianBlur 7x7 integer kernel [18 34 49 55 49 34 18], >>16
+//         (SURVEY.md A.3): the horizontal pass is v_dot4_u32_u8 on 4 output
+//         columns x 2 rows per lane, stored transposed as u16 row pairs; the
+//         vertical pass is evaluated only at the 512 BRIEF sample points with
+//         four v_dot2_u32_u16 each.
+//   BRIEF fmaf sample coordinates, 256 tests -> four __ballot
+//         words = the descriptor's little-endian u64 words (:141-192).
 // ---------------------------------------------------------------------------
-constexpr int kPatchP = 48;                           // LDS row pitch (bytes): 37 columns + shift slack
-constexpr int kPatchRows = 37;                        // rows cy - 18 .. cy + 18
-constexpr int kPatchBytes = kPatchRows * kPatchP;     // 1776
+constexpr int kRawP = 48;                             // LDS row pitch (bytes): the 43 columns + shift slack
+constexpr int kRawRows = 44;                          // 43 rows used (row 43 repeats row 42)
+constexpr int kRawSlots = kRawRows * kRawP / 4;
+// row-blurred, transposed: [col][row pairs], 22 dwords per column
+constexpr int kTCols = 40, kTP = 22;
 #ifndef ORBX_DESC_KPW
 #define ORBX_DESC_KPW 4
 #endif
 constexpr int kDescPerWave = ORBX_DESC_KPW;           // keypoints per wave (lane state set up once per wave)
+#ifndef ORBX_DESC_WAVES
+#define ORBX_DESC_WAVES 1
+#endif
+// waves per describe workgroup: one, so a workgroup's LDS (6.3 KB) frees as soon as its own keypoints are done
+// and no wave waits on slower siblings (4 waves: 863 us per 384 frames, 2: 815, 1: 768; pipelined 169.1k ->
+// 176.4k frames/s)
+constexpr int kDescWaves = ORBX_DESC_WAVES;
+
+// Horizontal-pass items (row pair rp << 8 | column group cg) that BRIEF can read: a sample
+// (18 + xx, 18 + yy) has |(x, y)| <= 18.39 before rounding (the pattern's largest radius), so a
+// column group needs only the row pairs its disc chord reaches, plus the 7-tap reach of
+// blur_acc.  189 of the 22 x 10 items: three per lane, row-pair major so that the lanes of a
+// load read neighbouring raw dwords (distinct LDS banks).
+__constant__ uint16_t c_blur_items[192] = {2,3,4,5,6,257,258,259,260,261,262,263,513,514,515,516,517,518,519,768,769,770,771,772,773,774,775,776,1024,1025,1026,1027,1028,1029,1030,1031,1032,1280,1281,1282,1283,1284,1285,1286,1287,1288,1536,1537,1538,1539,1540,1541,1542,1543,1544,1545,1792,1793,1794,1795,1796,1797,1798,1799,1800,1801,2048,2049,2050,2051,2052,2053,2054,2055,2056,2057,2304,2305,2306,2307,2308,2309,2310,2311,2312,2313,2560,2561,2562,2563,2564,2565,2566,2567,2568,2569,2816,2817,2818,2819,2820,2821,2822,2823,2824,2825,3072,3073,3074,3075,3076,3077,3078,3079,3080,3081,3328,3329,3330,3331,3332,3333,3334,3335,3336,3337,3584,3585,3586,3587,3588,3589,3590,3591,3592,3593,3840,3841,3842,3843,3844,3845,3846,3847,3848,3849,4096,4097,4098,4099,4100,4101,4102,4103,4104,4352,4353,4354,4355,4356,4357,4358,4359,4360,4609,4610,4611,4612,4613,4614,4615,4616,4865,4866,4867,4868,4869,4870,4871,5122,5123,5124,5125,5126,5127,5379,5380,5381,5382,65535,65535,65535};
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+// GaussianBlur's 7 taps starting at byte `off` of four consecutive raw dwords: the weight bytes of dword d
+__host__ __device__ constexpr uint32_t blur_wshift(int off, int d)
+{
+    constexpr uint32_t k[7] = {18, 34, 49, 55, 49, 34, 18};
+    uint32_t w = 0;
+    for (int b = 0; b < 4; ++b) {
+        const int t = 4 * d + b - off;
+        if (t >= 0 && t < 7) w |= k[t] << (8 * b);
+    }
+    return w;
+}
 constexpr int kPattern[1024] = {
 #include "orb_pattern.inc"
 };
@@ -2385,7 +2212,7 @@ constexpr int kPattern[1024] = {
 // Keypoint-independent lane state of k_describe, a function of the lane alone, built at compile time
 // (the kernel loads it instead of computing ~235 VALU instructions per wave).
 //   IC_Angle: lane 2i + h owns disc row v = i - 15 (i < 31), half h: u = -15..0 or 1..15, as 4
-//   realigned dwords of the level row dotted (v_dot4_u32_u8) with per-lane weights that are zero
+//   realigned dwords of the raw row dotted (v_dot4_u32_u8) with per-lane weights that are zero
 //   outside |u| <= umax[|v|]: w1 = (u + 16) for m10 (minus 16 * sum I), w0 = 1 for sum I.
 //   rBRIEF: the lane's 8 pattern points (tests m = 64 wd + lane, wd = q >> 1; e = q & 1), as floats.
 struct DescLane {
@@ -2419,6 +2246,13 @@ constexpr DescLaneTable make_desc_lanes()
 }
 __constant__ DescLaneTable c_desc_lanes = make_desc_lanes();
 
+__device__ __forceinline__ int reflect101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+
 // wave sum: row (16-lane) sums with DPP, then the four rows by readlane (all lanes active)
 __device__ __forceinline__ int wave_sum(int v)
 {
@@ -2433,24 +2267,70 @@ __device__ __forceinline__ int wave_sum(int v)
 // Sample coordinates as float bits: fl + 1.5 * 2^23 rounds fl to the nearest integer, ties to even
 // (one f32 addition into [2^23, 2^24), whose ulp is 1; the magic number is even, so the tie parity
 // is fl's), exactly __float2int_rn for |fl| < 2^22, and leaves that integer in the low mantissa
-// bits: bits = 0x4B400000 + round(fl).  The patch lookup indexes with these bits directly:
-// v_mad_u32_u24(by, 48, bx) = 48 (0x400000 + yy) + 0x4B400000 + xx = 0x57400000 + 48 yy + xx.
+// bits: bits = 0x4B400000 + round(fl).  The blur lookup indexes with these bits directly.
 constexpr float kRoundMagic = 12582912.0f;
-constexpr uint32_t kSampleBias = 0x57400000u;
+constexpr uint32_t kRoundBits = 0x4B400000u;
 
-__global__ __launch_bounds__(64) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
-                                                 const uint8_t* __restrict__ blur, size_t blur_fstride,
-                                                 const uint32_t* __restrict__ qt_out, const int* __restrict__ qt_cnt,
-                                                 orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int cap,
-                                                 int* __restrict__ status, int kpw)
+// blurred value at patch row 18 + yy, column 18 + xx (|xx|, |yy| <= 19, given as kRoundMagic
+// bits by, bx): sum_t k[t] * rowblur[y+t][x], + 2^15 (the >> 16 rounding) folded into the sum.
+// The dword index is (18 + xx) * kTP + ((18 + yy) >> 1), in wrapping u32 arithmetic on the bits of
+// bx (its low 24 bits are 0x400000 + xx) and by (bits 1..23: 0x200000 + ((18 + yy) >> 1) - 9).
+// The LDS byte address in three VALU: bfe of by's bits 1..23 (0x200000 + (yy >> 1)), shifted and added to
+// mad24(bx, 4 kTP, C) with C = rowT + 4 (9 - 0x200000 + (18 - 0x400000) kTP) (mod 2^32); the compiler's
+// form of (by >> 1) + bx * kTP + rowT took five.
+constexpr uint32_t kBlurByte0 = 4u * (9u - 0x200000u + (18u - 0x400000u) * (uint32_t)kTP);
+__device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t bx)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_patch[2][kPatchBytes + 16];
-    const int lane = threadIdx.x;
+    const uint32_t t = __umul24(bx, 4u * (uint32_t)kTP) + C, f = __builtin_amdgcn_ubfe(by, 1, 23);
+    uint32_t a;
+    // one v_lshl_add_u32 (the compiler rewrites (f << 2) + t as (by << 1) & mask plus an add)
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"(f), "v"(t));
+    const __attribute__((address_space(3))) uint32_t* col = (const __attribute__((address_space(3))) uint32_t*)(uintptr_t)a;
+    const uint32_t d0 = col[0], d1 = col[1], d2 = col[2], d3 = col[3];
+    // even y: rows y..y+6 = (d0.lo d0.hi d1.lo d1.hi d2.lo d2.hi d3.lo); odd y: (d0.hi .. d3.hi)
+    const bool odd = by & 1u;
+    const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
+    const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
+    const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
+    const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
+    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), w0, 1u << 15, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d1), w1, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
+    return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
+}
+// The vertical taps of a sample from its four dwords (even or odd row parity)
+__device__ __forceinline__ uint32_t blur_taps(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t by)
+{
+    const bool odd = by & 1u;
+    const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
+    const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
+    const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
+    const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
+    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), w0, 1u << 15, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d1), w1, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
+    return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
+}
+#ifndef ORBX_DESC_WPE
+#define ORBX_DESC_WPE 1
+#endif
+__global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
+                                               const uint32_t* __restrict__ qt_out,
+                                               const int* __restrict__ qt_cnt,
+                                               orbx_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                               int cap, int* __restrict__ status, int kpw)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_raw[kDescWaves][kRawSlots];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rowT[kDescWaves][kTCols * kTP];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave: uniform (SGPR)
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x, bx = lb - f * gridDim.x;
     const int L = G->nlevels;
     const int* cnts = qt_cnt + (size_t)f * L;
-    const int g0 = bx * kpw;
+    uint32_t* raw32 = s_raw[wave];
+    uint8_t* raw = (uint8_t*)raw32;
+    uint32_t* rowT = s_rowT[wave];
+    const int g0 = (bx * kDescWaves + wave) * kpw;
 
     // ---- keypoint-independent lane state (c_desc_lanes), loaded once for the wave's keypoints ----
     const int icv = lane >> 1, ich = lane & 1;
@@ -2468,10 +2348,15 @@ __global__ __launch_bounds__(64) void k_describe(const Geometry* __restrict__ G,
         ppx[q] = DL.px[q];
         ppy[q] = DL.py[q];
     }
+    const int ic_row = 21 + vrow, ic_col = ich ? 22 : 6;   // raw row, patch column of the first pixel
+    int bitem[3];
+#pragma unroll
+    for (int it = 0; it < 3; ++it) bitem[it] = c_blur_items[lane + 64 * it];
 
     // output index g (level-major, as the reference concatenates levels) -> level, keypoint: lane j < kpw
-    // looks up the wave's keypoint j once, up front.  The wave's indices are consecutive, so past the
-    // frame's total (or the output capacity) the rest are too, and the valid lanes are a prefix.
+    // looks up the wave's keypoint j once, up front, so no keypoint waits for its packed entry's global load
+    // before its patch DMA can go out.  The wave's indices are consecutive, so past the frame's total (or
+    // the output capacity) the rest are too, and the valid lanes are a prefix.
     int my_l = 0;
     uint32_t my_pk = 0;
     bool my_ok = false;
@@ -2493,37 +2378,82 @@ __global__ __launch_bounds__(64) void k_describe(const Geometry* __restrict__ G,
         }
     }
     const int nkp = __builtin_popcountll(__ballot(my_ok));
-    if (nkp == 0) return;
-    const uint8_t* bframe = blur + (size_t)f * blur_fstride;
-    // keypoint jj's blurred patch (rows cy - 18 .. cy + 18, the 4-byte aligned run from column cx - 18) into
-    // buffer jj & 1; 16-byte piece c = 64 t + lane of DMA instruction t is piece c % 3 of row c / 3 (a row
-    // reads 48 bytes from its aligned start, at most cx + 30: inside the level row, or the next row of the
-    // level, since cx <= w - 20 and cy + 18 <= h - 2).  Returns the patch's byte shift.
-    auto fill = [&](int jj) -> int {
-        const int l = __builtin_amdgcn_readlane(my_l, jj);
-        const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)my_pk, jj);
-        const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF);
-        const LevelGeom& LG = G->lv[l];
-        const uintptr_t s0 = (uintptr_t)(bframe + LG.bl_off + (size_t)(cy - 18) * LG.pitch + (cx - 18));
-        const uint8_t* ub = (const uint8_t*)(s0 & ~(uintptr_t)3);   // wave-uniform, aligned
-        uint32_t* dst = (uint32_t*)s_patch[jj & 1];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int c = 64 * t + lane, row = c / 3, k = c - 3 * row;
-            if (t == 0 || c < 3 * kPatchRows) {
-                const uint32_t o = (uint32_t)(row * LG.pitch) + 16u * (uint32_t)k;
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ub + o),
-                                                 (__attribute__((address_space(3))) void*)(dst + 256 * t), 16, 0, 0);
-            }
-        }
-        return (int)(s0 & 3);
+    auto lookup = [&](int jj, int& l, uint32_t& pk) -> bool {
+        if (jj >= nkp) return false;
+        l = __builtin_amdgcn_readlane(my_l, jj);
+        pk = (uint32_t)__builtin_amdgcn_readlane((int)my_pk, jj);
+        return true;
     };
-    int shift_cur = fill(0);
+    // raw patch rows cy-21..cy+21 from column cx-21 (48 bytes used per row); sets the
+    // wave-uniform row-shift state: row r starts at byte (sb + r*sp) & 3 of its LDS row
+    // the DMA's address registers kept live until the loop-top wait for it, so no later write to them makes
+    // the compiler wait for the DMA (a write-after-read on a VMEM source register) before BRIEF
+    uint32_t dma_va[3] = {0u, 0u, 0u};
+    auto fill = [&](int l, uint32_t pk, int& sb, int& sp) {
+        const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF);
+        const int w = G->lv[l].w, h = G->lv[l].h;
+        int pitch;
+        const uint8_t* img = level_base(P, G, f, l, pitch);
+        // Interior keypoints, and right-border ones whose 43 columns are all inside the level (cx + 21 < w):
+        // those read up to 9 bytes past the row end, which land in the next row of the same level (cy + 22 < h)
+        // and only feed blurred columns BRIEF never samples (|x| <= 18 + the 3-tap reach).  About 2/3 of the
+        // 6.5% of KITTI keypoints the reflect-101 byte path took before (13% of the describe launch).
+        if (cx >= 21 && cy >= 21 && cy + 21 < h && (cx + 31 <= w || (cx + 21 < w && cy + 22 < h))) {
+            // 16-byte piece c = 64 t + lane of DMA instruction t (global_load_lds_dwordx4: lane L's 16 bytes
+            // land at byte 16 L of the instruction's 1 KiB) is piece c % 3 of row c / 3, so three instructions
+            // fill rows 0..43 (the third with lanes 0..3 only; row 43 repeats row 42).  Each row's aligned
+            // bytes start at or after the 4-byte aligned allocation; a row reads 48 bytes from its aligned
+            // start, at most cx + 26 (inside the level row, or in the next row of the same level for the
+            // right-border case).  (Round 2: eleven 4-row global_load_lds_dword instructions into 64-byte
+            // rows, 2816 B; the 48-byte rows take the wave to 5.6 KB of LDS, 7 waves per SIMD.)
+            const uintptr_t s0 = (uintptr_t)(img + (size_t)(cy - 21) * pitch + (cx - 21));
+            const uint8_t* ub = (const uint8_t*)(s0 & ~(uintptr_t)3);   // wave-uniform, aligned
+            sb = (int)(s0 & 3);
+            sp = pitch & 3;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int c = 64 * t + lane, row = c / 3, k = c - 3 * row;
+                if (t < 2 || lane < 4) {
+                    const uint32_t o = (uint32_t)((sb + min(row, 42) * pitch) & ~3) + 16u * (uint32_t)k;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ub + o),
+                                                     (__attribute__((address_space(3))) void*)(raw32 + 256 * t), 16, 0, 0);
+                    dma_va[t] = o;
+                }
+            }
+        } else {
+            sb = 0;
+            sp = 0;
+            // reflect-101 bytes, lane = column (43 of the 48 per row), the column reflection once per lane,
+            // the row's per row (wave-uniform), and 11 rows' loads in flight before their LDS stores
+            static_assert(kRawRows >= 44, "rows 0..43 filled");
+            const uint8_t* col = img + reflect101(cx - 21 + min(lane, 42), w);
+            for (int s0 = 0; s0 < 44; s0 += 11) {
+                uint8_t v[11];
+#pragma unroll
+                for (int u = 0; u < 11; ++u) v[u] = col[(size_t)reflect101(cy - 21 + min(s0 + u, 42), h) * pitch];   // row 43 repeats row 42
+                if (lane < kRawP) {
+#pragma unroll
+                    for (int u = 0; u < 11; ++u) raw[(s0 + u) * kRawP + lane] = v[u];
+                }
+            }
+            // (no-op at run time: every byte load above is consumed; it tells the compiler's wait-count pass so,
+            // which otherwise waits for the DMA path's loads before BRIEF reuses these registers)
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+    };
+
+    int nl = 0, sb = 0, sp = 0;
+    uint32_t npk = 0;
+    bool nvalid = lookup(0, nl, npk);
+    if (nvalid) fill(nl, npk, sb, sp);
     // IC_Angle (src/ORBextractor.cc:84-128) of the wave's keypoints up front, from the level images in
-    // global memory (the disc never leaves the level; lanes 62-63 read row 16 with zero weights).
-    // cv::fastAtan2 and sincosf then run once per wave with lane j on keypoint j.
+    // global memory: a keypoint lies >= 19 px inside its level (FAST's cell windows), so its radius-15 disc
+    // never leaves it (lanes 62-63 read row 16 with zero weights).  cv::fastAtan2 and sincosf then run
+    // once per wave with lane j on keypoint j, instead of once per keypoint on every lane (the angle was
+    // 17% of the launch).  Loads of every keypoint first, then the sums.
     float kp_ang = 0.f, kp_cos = 1.f, kp_sin = 0.f;
     int ic_m10 = 0, ic_m01 = 0;   // lane j: keypoint j's moments
+    // (keypoints in groups of 4: one group's 20 row dwords in registers at a time)
     constexpr int kIcGroup = kDescPerWave < 4 ? kDescPerWave : 4;
 #pragma unroll 1
     for (int j0 = 0; j0 < kDescPerWave && j0 < nkp; j0 += kIcGroup) {
@@ -2560,34 +2490,98 @@ __global__ __launch_bounds__(64) void k_describe(const Geometry* __restrict__ G,
             }
         }
     }
-    kp_ang = fast_atan2_deg((float)ic_m01, (float)ic_m10);
-    glibc_sincosf_pair(kp_ang * kFactorPI, &kp_sin, &kp_cos);   // (src/ORBextractor.cc:148)
-
+    if (nkp > 0) {
+        kp_ang = fast_atan2_deg((float)ic_m01, (float)ic_m10);
+        glibc_sincosf_pair(kp_ang * kFactorPI, &kp_sin, &kp_cos);   // (src/ORBextractor.cc:148)
+    }
 #pragma unroll 1
-    for (int jj = 0; jj < nkp; ++jj) {
-        const int shift = shift_cur;
-        const int oidx = g0 + jj;
-        const int l = __builtin_amdgcn_readlane(my_l, jj);
-        const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)my_pk, jj);
+    for (int jj = 0; jj < kpw && nvalid; ++jj) {
+        const int oidx = g0 + jj, l = nl;
+        const uint32_t pk = npk;
+        const int csb = sb, csp = sp;
         const LevelGeom& LG = G->lv[l];
         const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF), score = (int)(pk >> 24);
-        // the next keypoint's patch goes out before this one's wait: vmcnt retires in issue order, so waiting
-        // down to the next patch's own loads (1 or 2 DMA instructions) plus the previous keypoint's three output
-        // stores leaves those in flight
-        if (jj + 1 < nkp) {
-            shift_cur = fill(jj + 1);
-            __builtin_amdgcn_s_waitcnt(0x0F75);   // vmcnt(5): this patch's DMA has landed
-        } else {
-            __builtin_amdgcn_s_waitcnt(0x0F73);   // vmcnt(3)
-        }
+        // this keypoint's DMA has landed.  vmcnt counts loads and stores and retires them in issue order, and
+        // the previous keypoint's three output stores (desc dwordx2, cv::KeyPoint dwordx4 + dwordx3) were issued
+        // after this DMA: waiting down to 3 leaves their round trip in flight
+        // (the builtin, not inline asm: the compiler's wait-count pass sees it, and does not wait again for
+        // loads it already covers -- an inline-asm wait is opaque to it; gfx9 simm16: vmcnt[3:0], expcnt[6:4]
+        // = 7, lgkmcnt[11:8] = 15, vmcnt[5:4] at [15:14])
+        // (also right for jj = 0: the IC_Angle loads issued after the first keypoint's DMA were waited for)
+        __builtin_amdgcn_s_waitcnt(0x0F73);   // vmcnt(3)
+        asm volatile("" ::"v"(dma_va[0]), "v"(dma_va[1]), "v"(dma_va[2]));
         wave_lds_sync();
-        // rBRIEF with the reference's contracted FMAs, each sample one blurred byte of the patch
+
+        // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns.
+        // Output column j of the realigned bytes R0 | R1 | R2 is sum_t w[t] * byte[j + t]: a dot4 of each
+        // dword with the kernel shifted by j (zero outside the 7 taps), 10 dot4 per row instead of 8
+        // byte-realignments and 8 dot4.
+        constexpr uint32_t kW[4][3] = {
+            {18u | 34u << 8 | 49u << 16 | 55u << 24, 49u | 34u << 8 | 18u << 16, 0u},
+            {18u << 8 | 34u << 16 | 49u << 24, 55u | 49u << 8 | 34u << 16 | 18u << 24, 0u},
+            {18u << 16 | 34u << 24, 49u | 55u << 8 | 49u << 16 | 34u << 24, 18u},
+            {18u << 24, 34u | 49u << 8 | 55u << 16 | 49u << 24, 34u | 18u << 8}};
+        // Rows that all start at the same byte shift S (csp == 0: the level pitch is a multiple of 4, or the
+        // reflect-101 byte path) skip the realignment: output column j is a dot4 of each raw dword with the
+        // kernel shifted by S + j bytes, still 10 dot4 per row (2 or 3 per column) and no alignbyte.
+        auto hpass = [&](auto s_tag) {
+            constexpr int S = decltype(s_tag)::value;   // -1: per-row shifts
+#pragma unroll
+            for (int it = 0; it < 3; ++it) {
+                if (bitem[it] == 0xFFFF) break;
+                const int rp = bitem[it] >> 8, cg = bitem[it] & 0xFF;
+                uint32_t o[2][4];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int r = 2 * rp + e;
+                    const uint32_t* rr = raw32 + r * (kRawP / 4) + cg;
+                    const uint32_t W[4] = {rr[0], rr[1], rr[2], rr[3]};
+                    if constexpr (S < 0) {
+                        const uint32_t sh = ((uint32_t)csb + __umul24((uint32_t)r, (uint32_t)csp)) & 3u;
+                        const uint32_t R[3] = {__builtin_amdgcn_alignbyte(W[1], W[0], sh),
+                                               __builtin_amdgcn_alignbyte(W[2], W[1], sh),
+                                               __builtin_amdgcn_alignbyte(W[3], W[2], sh)};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            uint32_t acc = __builtin_amdgcn_udot4(R[0], kW[j][0], 0u, false);
+                            acc = __builtin_amdgcn_udot4(R[1], kW[j][1], acc, false);
+                            if (j >= 2) acc = __builtin_amdgcn_udot4(R[2], kW[j][2], acc, false);
+                            o[e][j] = acc;
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            uint32_t acc = 0u;
+#pragma unroll
+                            for (int d = 0; d < 4; ++d) {
+                                const uint32_t w = blur_wshift(S + j, d);   // folds to a constant
+                                if (w) acc = __builtin_amdgcn_udot4(W[d], w, acc, false);
+                            }
+                            o[e][j] = acc;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    rowT[(4 * cg + j) * kTP + rp] = o[0][j] | (o[1][j] << 16);
+                }
+            }
+        };
+        if (csp != 0) hpass(std::integral_constant<int, -1>{});
+        else if (csb == 0) hpass(std::integral_constant<int, 0>{});
+        else if (csb == 1) hpass(std::integral_constant<int, 1>{});
+        else if (csb == 2) hpass(std::integral_constant<int, 2>{});
+        else hpass(std::integral_constant<int, 3>{});
+        wave_lds_sync();   // raw is free: start the next keypoint's patch, it lands under BRIEF
+        nvalid = lookup(jj + 1, nl, npk);
+        if (nvalid) fill(nl, npk, sb, sp);
+
+        // rBRIEF with the reference's contracted FMAs; blur evaluated at each sample point
         const float angle = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_ang), jj));
         const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_cos), jj));
         const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_sin), jj));
-        // LDS byte of sample (yy, xx): patch + 18 * 48 + 18 + shift + 48 yy + xx
-        const uint32_t cbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)s_patch[jj & 1] +
-                               (uint32_t)(18 * kPatchP + 18 + shift) - kSampleBias;
+        // GaussianBlur's u8 saturation: min(t0, 255) < min(t1, 255) iff t0 < min(t1, 255)
+        const uint32_t cblur = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)rowT + kBlurByte0;
         unsigned long long words[4];
 #pragma unroll
         for (int wd = 0; wd < 4; ++wd) {
@@ -2600,31 +2594,30 @@ __global__ __launch_bounds__(64) void k_describe(const Geometry* __restrict__ G,
             const f2v BX = __builtin_elementwise_fma(PX, va, -(PY * vb)) + mg;
             uint32_t t2[2];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const uint32_t ad = __umul24(__float_as_uint(BY[e]), (uint32_t)kPatchP) + __float_as_uint(BX[e]) + cbase;
-                t2[e] = *(const __attribute__((address_space(3))) uint8_t*)(uintptr_t)ad;
-            }
-            words[wd] = __ballot(t2[0] < t2[1]);
+            for (int e = 0; e < 2; ++e) t2[e] = blur_acc(cblur, __float_as_uint(BY[e]), __float_as_uint(BX[e])) >> 16;
+            words[wd] = __ballot(t2[0] < (t2[1] < 255u ? t2[1] : 255u));
         }
-        const size_t o = (size_t)f * cap + oidx;
-        if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
-        if (lane == 0) {
-            float x = (float)cx, y = (float)cy;
-            if (l != 0) {
-                x *= LG.scale;
-                y *= LG.scale;
+        {   // A/B knob: per-keypoint stores (round 2)
+            const size_t o = (size_t)f * cap + oidx;
+            if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
+            if (lane == 0) {
+                float x = (float)cx, y = (float)cy;
+                if (l != 0) {
+                    x *= LG.scale;
+                    y *= LG.scale;
+                }
+                orbx_keypoint k;
+                k.x = x;
+                k.y = y;
+                k.size = LG.patch_size;
+                k.angle = angle;
+                k.response = (float)score;
+                k.octave = l;
+                k.class_id = -1;
+                kps[o] = k;
             }
-            orbx_keypoint k;
-            k.x = x;
-            k.y = y;
-            k.size = LG.patch_size;
-            k.angle = angle;
-            k.response = (float)score;
-            k.octave = l;
-            k.class_id = -1;
-            kps[o] = k;
         }
-        wave_lds_sync();   // buffer jj & 1 is refilled for keypoint jj + 2
+        wave_lds_sync();   // rowT is rewritten by the next keypoint
     }
 }
 
@@ -2633,9 +2626,9 @@ void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p
 {
     // small batches (the per-frame host path) are latency-bound: one keypoint per wave
     const int kpw = batch <= kLatencyMaxBatch ? 1 : kDescPerWave;
-    dim3 grid((g.out_per_frame + kpw - 1) / kpw, batch);
-    hipLaunchKernelGGL(k_describe, grid, dim3(64), 0, s, b.geom, p, b.blur, (size_t)g.bl_bytes, b.qt_out, b.qt_cnt,
-                       kps, desc, cap, b.status, kpw);
+    dim3 grid((g.out_per_frame + kDescWaves * kpw - 1) / (kDescWaves * kpw), batch);
+    hipLaunchKernelGGL(k_describe, grid, dim3(64 * kDescWaves), 0, s, b.geom, p, b.qt_out, b.qt_cnt, kps, desc, cap,
+                       b.status, kpw);
 }
 
 }  // namespace orbx

@@ -46,10 +46,6 @@ struct LevelGeom {
     // in a per-(frame, level) global region of qtg_bytes at qtg_off inside the frame's node block
     int qt_glob;
     long long qtg_off, qtg_bytes;
-    // K1b blurred level: at bl_off inside the frame's blurred block, row pitch `pitch`; waves bl_ub ..
-    // bl_ub + bl_nc * ceil(h / kBlurRows) - 1 of the blur launch, bl_nc column chunks per band
-    long long bl_off;
-    int bl_ub, bl_nc;
 };
 
 // K1 small-batch launch group: levels s+1 .. s+n resized from level s in one launch (k_pyramid_fused).  A
@@ -81,8 +77,6 @@ struct Geometry {
     int qt_kpt0;              // level-0 quadtree keypoints per thread (16, or 24 for large frames)
     long long pyr_bytes;      // bytes per frame for levels 1..L-1
     long long qtg_per_frame;  // K3 global node block per frame (0: every level's node list fits LDS)
-    long long bl_bytes;       // blurred levels 0..L-1 per frame (K1b)
-    int bl_units;             // K1b waves per frame
     int pyr_ngroups;          // K1 small-batch launches (0: per-level launches for every batch)
     PyrGroup pg[kMaxLevels];
     int umax[16];

@@ -33,7 +33,6 @@ struct ExtractBufs {
     uint32_t* qt_out;           // [B][out_per_frame] retained keypoints (level coords)
     int* qt_cnt;                // [B][nlevels]
     int* status;                // device error word (bit flags)
-    uint8_t* blur;              // [B][bl_bytes] GaussianBlur of every level (K1b), read by K4
 };
 
 // XCD-aware workgroup order.  The dispatcher hands flat workgroup id b to XCD b % 8;
@@ -104,10 +103,6 @@ __host__ __device__ inline int qt_regcap(const Geometry& g, int l) { return qt_n
 // host: K1 small-batch launch groups and their band tables (Geometry::pg) from the resize row tables
 bool pyr_plan(Geometry& g, const int2* yt, std::vector<int4>& bands);
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
-// K1b: GaussianBlur 7x7 of every level into ExtractBufs::blur (one launch); blur_plan sets the layout
-constexpr int kBlurRowsHost = 32, kBlurChunkHost = 256;
-void blur_plan(Geometry& g);
-void launch_blur(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
 void fast_groups(Geometry& g);   // host: FAST launch groups (cell ranges, LDS sizes)
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
 void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s);

@@ -174,7 +174,8 @@ __device__ __forceinline__ int pj_candidate(const PjWindow& w, const orbm_proj_p
 }
 
 // The first kTop candidates of a window in (distance, visiting position) order -- the order in which
-// the reference's sequential strict-< scan ranks them -- packed as dist:9 | bin:5 | octave:4 | idx:13.
+// the reference's sequential strict-< scan ranks them -- packed as dist:9 | bin:5 | octave:4 | idx:14
+// (frames of up to ORBM_MAX_FEATURES = 16384 features; a distance is at most 256, 9 bits).
 // A claim made later in the call only removes candidates, so the replay takes the first unclaimed
 // entries of this list and scans the window again only when more than kTop were taken.
 constexpr int kTop = 8;
@@ -185,21 +186,22 @@ struct TopK {
 
 __device__ __forceinline__ uint32_t top_entry(int dist, int bin, int oct, int idx)
 {
-    return (uint32_t)dist << 22 | (uint32_t)bin << 17 | (uint32_t)(oct & 15) << 13 | (uint32_t)idx;
+    return (uint32_t)dist << 23 | (uint32_t)bin << 18 | (uint32_t)(oct & 15) << 14 | (uint32_t)idx;
 }
-__device__ __forceinline__ int top_idx(uint32_t e) { return (int)(e & 0x1FFF); }
-__device__ __forceinline__ int top_oct(uint32_t e) { return (int)((e >> 13) & 15); }
-__device__ __forceinline__ int top_bin(uint32_t e) { return (int)((e >> 17) & 31); }
-__device__ __forceinline__ int top_dist(uint32_t e) { return (int)(e >> 22); }
+static_assert(ORBM_MAX_FEATURES <= (1 << 14), "top_entry packs a feature index in 14 bits");
+__device__ __forceinline__ int top_idx(uint32_t e) { return (int)(e & 0x3FFF); }
+__device__ __forceinline__ int top_oct(uint32_t e) { return (int)((e >> 14) & 15); }
+__device__ __forceinline__ int top_bin(uint32_t e) { return (int)((e >> 18) & 31); }
+__device__ __forceinline__ int top_dist(uint32_t e) { return (int)(e >> 23); }
 
 __device__ __forceinline__ void top_insert(TopK& t, uint32_t entry)
 {
-    const uint32_t dnew = entry >> 22;
+    const uint32_t dnew = entry >> 23;
     uint32_t carry = entry;
     bool shifting = false;   // stable: after the entries of equal distance, then everything moves down
 #pragma unroll
     for (int k = 0; k < kTop; ++k) {
-        const bool take = shifting || k >= t.n || (t.e[k] >> 22) > dnew;
+        const bool take = shifting || k >= t.n || (t.e[k] >> 23) > dnew;
         if (take) {
             const uint32_t x = t.e[k];
             t.e[k] = carry;
@@ -211,7 +213,7 @@ __device__ __forceinline__ void top_insert(TopK& t, uint32_t entry)
 }
 
 // J2 / P1 give a MapPoint kSub adjacent lanes: sub-lane s scans window positions lo + s, lo + s +
-// kSub, ...  Each keeps its own first kTop as 64-bit keys dist:9 | position:16 | entry low 22 bits
+// kSub, ...  Each keeps its own first kTop as 64-bit keys dist:9 | position:16 | entry low 23 bits
 // (bin, octave, index), i.e. in (distance, visiting position) order, and the group merges its
 // lists by kTop rounds of a min over the group's heads.  Same list as one sequential scan.
 constexpr int kSub = 4;
@@ -222,7 +224,7 @@ struct TopK64 {
 
 __device__ __forceinline__ unsigned long long top_key(uint32_t entry, int p)
 {
-    return (unsigned long long)(entry >> 22) << 38 | (unsigned long long)p << 22 | (entry & 0x3FFFFFu);
+    return (unsigned long long)(entry >> 23) << 39 | (unsigned long long)p << 23 | (entry & 0x7FFFFFu);
 }
 
 __device__ __forceinline__ void top64_insert(TopK64& t, unsigned long long key)
@@ -270,7 +272,7 @@ __device__ __forceinline__ TopK top_merge(TopK64& t)
             for (int k = 0; k + 1 < kTop; ++k) t.e[k] = t.e[k + 1];
             --have;
         }
-        out.e[r] = m == ~0ull ? 0u : (uint32_t)((m >> 38) << 22 | (m & 0x3FFFFFu));
+        out.e[r] = m == ~0ull ? 0u : (uint32_t)((m >> 39) << 23 | (m & 0x7FFFFFu));
     }
     return out;
 }

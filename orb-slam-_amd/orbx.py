@@ -36,7 +36,7 @@ TOP2, FULL_U16 = 0, 1
 EXPORTED = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_capacity", "orbx_extract", "orbx_get_level",
     "orbx_extract_batch_device", "orbx_extract_stage_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
-    "orbx_debug_pyramid", "orbx_debug_blurred", "orbx_debug_candidates", "orbx_debug_launches", "orbm_descriptor_distance", "orbm_allpairs_device", "orbm_allpairs",
+    "orbx_debug_pyramid", "orbx_debug_candidates", "orbx_debug_launches", "orbm_descriptor_distance", "orbm_allpairs_device", "orbm_allpairs",
     "orbm_search_init_batch_device", "orbm_search_for_initialization_device", "orbm_search_for_initialization",
     "orbx_compute_stereo_matches", "orbx_stereo_batch_device",
     "orbm_bow_search_device", "orbm_bow_search",
@@ -172,7 +172,6 @@ def _load():
     L.orbx_set_timing.argtypes = [vp, C.c_int]
     L.orbx_get_stage_times.argtypes = [vp, f32p, C.c_int]
     L.orbx_debug_pyramid.argtypes = [vp, C.c_int, u8p, C.c_size_t]
-    L.orbx_debug_blurred.argtypes = [vp, C.c_int, u8p, C.c_size_t]
     L.orbx_debug_candidates.argtypes = [vp, C.c_int, C.c_int, i32p, C.c_int, i32p]
     L.orbx_debug_launches.argtypes = [vp, C.c_int, C.c_int, C.c_int, i32p, C.c_int]
     L.orbm_descriptor_distance.argtypes = [u8p, u8p]
@@ -384,17 +383,6 @@ class ORBextractor:
         total = sum(w * h for w, h in sizes)
         buf = np.zeros(total, np.uint8)
         _check("orbx_debug_pyramid", lib.orbx_debug_pyramid(self._h, frame, _u8(buf), total))
-        out, o = [], 0
-        for w, h in sizes:
-            out.append(buf[o:o + w * h].reshape(h, w))
-            o += w * h
-        return out
-
-    def debug_blurred(self, frame, sizes):
-        """GaussianBlur 7x7 of every level of frame `frame` of the last batch (K1b output, rBRIEF's input)."""
-        total = sum(w * h for w, h in sizes)
-        buf = np.zeros(total, np.uint8)
-        _check("orbx_debug_blurred", lib.orbx_debug_blurred(self._h, frame, _u8(buf), total))
         out, o = [], 0
         for w, h in sizes:
             out.append(buf[o:o + w * h].reshape(h, w))

@@ -83,11 +83,6 @@ def test_extract_parity(orbref, cuda, name, W, H, nfeat, kind):
         for l, (a, b) in enumerate(zip(pyr, ref.pyramid)):
             bad = np.argwhere(a != b)
             assert bad.size == 0, "%s f%d pyramid level %d differs at %s" % (name, f, l, bad[:3])
-        # stage 1b: the blurred levels rBRIEF samples (GaussianBlur 7x7, reflect-101)
-        blr = ex.debug_blurred(f, sizes)
-        for l, (a, lv) in enumerate(zip(blr, ref.pyramid)):
-            bad = np.argwhere(a != orbref.gaussian_blur7(lv))
-            assert bad.size == 0, "%s f%d blurred level %d differs at %s" % (name, f, l, bad[:3])
         # stage 2: FAST candidates per level, reference order
         for l in range(8):
             want = orbref.level_candidates(ref.pyramid[l])
