@@ -2173,8 +2173,10 @@ void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts,
 constexpr int kRawP = 48;                             // LDS row pitch (bytes): the 43 columns + shift slack
 constexpr int kRawRows = 44;                          // 43 rows used (row 43 repeats row 42)
 constexpr int kRawSlots = kRawRows * kRawP / 4;
-// row-blurred, transposed: [col][row pairs], 22 dwords per column
-constexpr int kTCols = 40, kTP = 22;
+// row-blurred, transposed: [col][row pairs], 23 dwords per column (22 hold the 44 rows; the odd pitch spreads
+// the horizontal pass's column stores over the banks: 48 LDS-array cycles per keypoint against 68 at 22, and
+// 98 against 108 for the blur reads of tools/gen/brief_slots.py's slots)
+constexpr int kTCols = 40, kTP = 23;
 #ifndef ORBX_DESC_KPW
 #define ORBX_DESC_KPW 4
 #endif
@@ -2208,16 +2210,25 @@ __host__ __device__ constexpr uint32_t blur_wshift(int off, int d)
 constexpr int kPattern[1024] = {
 #include "orb_pattern.inc"
 };
+#include "orb_slots.inc"
 
 // Keypoint-independent lane state of k_describe, a function of the lane alone, built at compile time
 // (the kernel loads it instead of computing ~235 VALU instructions per wave).
 //   IC_Angle: lane 2i + h owns disc row v = i - 15 (i < 31), half h: u = -15..0 or 1..15, as 4
 //   realigned dwords of the raw row dotted (v_dot4_u32_u8) with per-lane weights that are zero
 //   outside |u| <= umax[|v|]: w1 = (u + 16) for m10 (minus 16 * sum I), w0 = 1 for sum I.
-//   rBRIEF: the lane's 8 pattern points (tests m = 64 wd + lane, wd = q >> 1; e = q & 1), as floats.
+//   rBRIEF: the pattern's 512 points hold 375 distinct ones.  Each is blurred once, in slot 64 q + lane (lane,
+//   round q < 6) of a u16 table; test m = 64 wd + lane (wd = q >> 1) reads its two samples (e = q & 1) from
+//   slot byte offsets rd[q].  Which point sits in which slot (orb_slots.inc, tools/gen/brief_slots.py) keeps
+//   each half-round's 32 points a compact cluster of the pattern, so their blur reads share LDS addresses
+//   and spread over the banks at any keypoint angle (98 LDS-array cycles per keypoint against 156 for the
+//   points in order of first use, 212 for the 512 points of round 4), and orders lanes inside each
+//   half-round for the table reads' banks.
+constexpr int kDescSlots = 6;   // distinct sample points per lane (384 slots >= 375)
 struct DescLane {
     uint32_t w1[4], w0[4];
-    float px[8], py[8];
+    float upx[kDescSlots], upy[kDescSlots];
+    uint32_t rd[8];
 };
 struct DescLaneTable {
     DescLane l[64];
@@ -2236,14 +2247,32 @@ constexpr DescLaneTable make_desc_lanes()
                     t.l[lane].w0[k] |= 1u << (8 * b);
                 }
             }
+    }
+    for (int lane = 0; lane < 64; ++lane) {
+        for (int q = 0; q < kDescSlots; ++q) {
+            const int i = kSlotPt[64 * q + lane];
+            t.l[lane].upx[q] = (float)kPattern[2 * i];
+            t.l[lane].upy[q] = (float)kPattern[2 * i + 1];
+        }
         for (int q = 0; q < 8; ++q) {
             const int m = (q >> 1) * 64 + lane, e = q & 1;
-            t.l[lane].px[q] = (float)kPattern[4 * m + 2 * e];
-            t.l[lane].py[q] = (float)kPattern[4 * m + 2 * e + 1];
+            t.l[lane].rd[q] = 2u * (uint32_t)kPtSlot[2 * m + e];
         }
     }
     return t;
 }
+// every pattern point's slot holds that point
+constexpr bool desc_slots_ok()
+{
+    for (int i = 0; i < 512; ++i) {
+        const int s = kPtSlot[i];
+        if (s < 0 || s >= 64 * kDescSlots) return false;
+        const int j = kSlotPt[s];
+        if (kPattern[2 * j] != kPattern[2 * i] || kPattern[2 * j + 1] != kPattern[2 * i + 1]) return false;
+    }
+    return true;
+}
+static_assert(desc_slots_ok(), "orb_slots.inc does not match orb_pattern.inc");
 __constant__ DescLaneTable c_desc_lanes = make_desc_lanes();
 
 __device__ __forceinline__ int reflect101(int p, int len)
@@ -2287,29 +2316,17 @@ __device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t b
     asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"(f), "v"(t));
     const __attribute__((address_space(3))) uint32_t* col = (const __attribute__((address_space(3))) uint32_t*)(uintptr_t)a;
     const uint32_t d0 = col[0], d1 = col[1], d2 = col[2], d3 = col[3];
-    // even y: rows y..y+6 = (d0.lo d0.hi d1.lo d1.hi d2.lo d2.hi d3.lo); odd y: (d0.hi .. d3.hi)
-    const bool odd = by & 1u;
-    const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
-    const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
-    const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
-    const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
-    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), w0, 1u << 15, false);
-    acc = __builtin_amdgcn_udot2(as_us2(d1), w1, acc, false);
-    acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
-    return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
-}
-// The vertical taps of a sample from its four dwords (even or odd row parity)
-__device__ __forceinline__ uint32_t blur_taps(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t by)
-{
-    const bool odd = by & 1u;
-    const ushort2_t w0 = odd ? ushort2_t{0, 18} : ushort2_t{18, 34};
-    const ushort2_t w1 = odd ? ushort2_t{34, 49} : ushort2_t{49, 55};
-    const ushort2_t w2 = odd ? ushort2_t{55, 49} : ushort2_t{49, 34};
-    const ushort2_t w3 = odd ? ushort2_t{34, 18} : ushort2_t{18, 0};
-    uint32_t acc = __builtin_amdgcn_udot2(as_us2(d0), w0, 1u << 15, false);
-    acc = __builtin_amdgcn_udot2(as_us2(d1), w1, acc, false);
-    acc = __builtin_amdgcn_udot2(as_us2(d2), w2, acc, false);
-    return __builtin_amdgcn_udot2(as_us2(d3), w3, acc, false);
+    // rows y..y+6 are (d0.lo d0.hi d1.lo d1.hi d2.lo d2.hi d3.lo) for even y and (d0.hi .. d3.hi) for odd y:
+    // shifting the dword chain right by 16 bits for odd y (v_alignbit uses its shift's low five bits, so
+    // by << 4 is that shift) leaves the same weights for both parities -- in SGPRs, where the per-lane
+    // selection of round 4 (four v_cndmask, a test) held both weight sets in VGPRs
+    const uint32_t sh = by << 4;
+    const uint32_t e0 = __builtin_amdgcn_alignbit(d1, d0, sh), e1 = __builtin_amdgcn_alignbit(d2, d1, sh);
+    const uint32_t e2 = __builtin_amdgcn_alignbit(d3, d2, sh), e3 = d3 >> (sh & 31u);
+    uint32_t acc = __builtin_amdgcn_udot2(as_us2(e0), ushort2_t{18, 34}, 1u << 15, false);
+    acc = __builtin_amdgcn_udot2(as_us2(e1), ushort2_t{49, 55}, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(e2), ushort2_t{49, 34}, acc, false);
+    return __builtin_amdgcn_udot2(as_us2(e3), ushort2_t{18, 0}, acc, false);
 }
 #ifndef ORBX_DESC_WPE
 #define ORBX_DESC_WPE 1
@@ -2337,17 +2354,20 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     const int vrow = icv - 15;
     const DescLane& DL = c_desc_lanes.l[lane];
     uint32_t W1[4], W0[4];
-    float ppx[8], ppy[8];
+    float ppx[kDescSlots], ppy[kDescSlots];
+    uint32_t rdo[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         W1[k] = DL.w1[k];
         W0[k] = DL.w0[k];
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        ppx[q] = DL.px[q];
-        ppy[q] = DL.py[q];
+    for (int q = 0; q < kDescSlots; ++q) {
+        ppx[q] = DL.upx[q];
+        ppy[q] = DL.upy[q];
     }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rdo[q] = DL.rd[q];
     const int ic_row = 21 + vrow, ic_col = ich ? 22 : 6;   // raw row, patch column of the first pixel
     int bitem[3];
 #pragma unroll
@@ -2582,20 +2602,32 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, kp_sin), jj));
         // GaussianBlur's u8 saturation: min(t0, 255) < min(t1, 255) iff t0 < min(t1, 255)
         const uint32_t cblur = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)rowT + kBlurByte0;
+        // the lane's distinct sample points blurred, two per packed coordinate evaluation, then written to
+        // the u16 sample table over rowT's first 768 bytes (one wave: its LDS reads and writes complete in
+        // issue order, so every sample's rowT reads precede the table writes)
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v va = {a, a}, vb = {b, b}, mg = {kRoundMagic, kRoundMagic};
+        uint32_t tv[kDescSlots];
+#pragma unroll
+        for (int q = 0; q < kDescSlots; q += 2) {
+            // (v_pk_mul / v_pk_fma / v_pk_add: the same roundings as the scalar statements, two samples per
+            // instruction)
+            const f2v PX = {ppx[q], ppx[q + 1]}, PY = {ppy[q], ppy[q + 1]};
+            const f2v BY = __builtin_elementwise_fma(PX, vb, PY * va) + mg;
+            const f2v BX = __builtin_elementwise_fma(PX, va, -(PY * vb)) + mg;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) tv[q + e] = blur_acc(cblur, __float_as_uint(BY[e]), __float_as_uint(BX[e]));
+        }
+        uint16_t* const stab = (uint16_t*)rowT;
+#pragma unroll
+        for (int q = 0; q < kDescSlots; ++q) stab[64 * q + lane] = (uint16_t)(tv[q] >> 16);
+        wave_lds_sync();
         unsigned long long words[4];
 #pragma unroll
         for (int wd = 0; wd < 4; ++wd) {
-            // the test's two samples as packed f32 pairs (v_pk_mul / v_pk_fma / v_pk_add: the same roundings
-            // as the scalar statements, two samples per instruction)
-            typedef float f2v __attribute__((ext_vector_type(2)));
-            const f2v PX = {ppx[2 * wd], ppx[2 * wd + 1]}, PY = {ppy[2 * wd], ppy[2 * wd + 1]};
-            const f2v va = {a, a}, vb = {b, b}, mg = {kRoundMagic, kRoundMagic};
-            const f2v BY = __builtin_elementwise_fma(PX, vb, PY * va) + mg;
-            const f2v BX = __builtin_elementwise_fma(PX, va, -(PY * vb)) + mg;
-            uint32_t t2[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) t2[e] = blur_acc(cblur, __float_as_uint(BY[e]), __float_as_uint(BX[e])) >> 16;
-            words[wd] = __ballot(t2[0] < (t2[1] < 255u ? t2[1] : 255u));
+            const uint32_t t0 = *(const uint16_t*)((const uint8_t*)stab + rdo[2 * wd]);
+            const uint32_t t1 = *(const uint16_t*)((const uint8_t*)stab + rdo[2 * wd + 1]);
+            words[wd] = __ballot(t0 < (t1 < 255u ? t1 : 255u));
         }
         {   // A/B knob: per-keypoint stores (round 2)
             const size_t o = (size_t)f * cap + oidx;
