@@ -749,6 +749,13 @@ __device__ unsigned long long g_fast_prof[8];
 #endif
 
 __device__ __forceinline__ unsigned long long ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// (a + b) << 1 in one v_add_lshl_u32
+__device__ __forceinline__ uint32_t add_lshl1(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_add_lshl_u32 %0, %1, %2, 1" : "=v"(r) : "v"(a), "s"(b));
+    return r;
+}
 __device__ __forceinline__ uint16_t* lds_u16(uint32_t a) { return (uint16_t*)(__attribute__((address_space(3))) uint16_t*)(uintptr_t)a; }
 // per lane: a if the lane's bit of the scalar mask m is set, else b -- one v_cndmask on the mask, with every
 // lane active (the compiler's form of the select is an exec-masked region)
@@ -914,7 +921,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             // LDS byte address of list[lcap - nb]: a back write is one v_lshl_add from it, and its update one
             // scalar subtract of twice the count
             const uint32_t bend = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)(list + lcap);
-            uint32_t bptr = bend;
+            uint32_t bptr = bend >> 1;   // in u16 entries: the count update is one scalar subtract
             const int rlane_b = rlane + rstep;
             const uint32_t fbeg = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)list;
             uint32_t fptr = fbeg;
@@ -927,22 +934,26 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
                 const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
                 const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
-                if (__builtin_amdgcn_inverse_ballot_w64(mfa)) list[nf + lanes_below(mfa)] = (uint16_t)t;
-                nf += __popcll(mfa);
-                if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
-                nf += __popcll(mfb);
+                // front entries are rare (about 2% of the pixels): one scalar test per trip skips both writes'
+                // exec save / restore and the count updates (s_or sets SCC)
+                if (mfa | mfb) {
+                    if (__builtin_amdgcn_inverse_ballot_w64(mfa)) list[nf + lanes_below(mfa)] = (uint16_t)t;
+                    nf += __popcll(mfa);
+                    if (__builtin_amdgcn_inverse_ballot_w64(mfb)) list[nf + lanes_below(mfb)] = (uint16_t)(t + rstep * TP);
+                    nf += __popcll(mfb);
+                }
                 // back entries (a quarter of the pixels: the mask is rarely empty) written by every lane, the
                 // lanes outside the mask into their own scratch dword: an address select instead of the exec
                 // save / branch / restore (FAST's time follows its scalar instruction count)
-                bptr -= 2u * (uint32_t)__popcll(mba);
-                *lds_select(mba, lds_u16(bptr + 2u * (uint32_t)lanes_below(mba)), bscratch) = (uint16_t)t;
-                bptr -= 2u * (uint32_t)__popcll(mbb);
-                *lds_select(mbb, lds_u16(bptr + 2u * (uint32_t)lanes_below(mbb)), bscratch) = (uint16_t)(t + rstep * TP);
+                bptr -= (uint32_t)__popcll(mba);
+                *lds_select(mba, lds_u16(add_lshl1((uint32_t)lanes_below(mba), bptr)), bscratch) = (uint16_t)t;
+                bptr -= (uint32_t)__popcll(mbb);
+                *lds_select(mbb, lds_u16(add_lshl1((uint32_t)lanes_below(mbb), bptr)), bscratch) = (uint16_t)(t + rstep * TP);
                 t += 2 * rstep * TP;
             };
             for (; rem >= 2 * rstep; rem -= 2 * rstep) trip(colmask, colmask);
             if (rem > 0) trip(colmask & ballot64(rlane < rem), colmask & ballot64(rlane_b < rem));
-            nb = (int)(bend - bptr) >> 1;
+            nb = (int)((bend >> 1) - bptr);
         };
         if constexpr (LD < 10) {   // (the 10-register prefetch kernels: 76 VGPRs, 6 waves per SIMD)
             if (dw <= 32) pass1(std::integral_constant<int, 5>{});
