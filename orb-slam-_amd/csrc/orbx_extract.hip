@@ -715,6 +715,41 @@ __device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneM
     }
 }
 
+// The first LD passes of a cell (u0 = 0) without per-pass address arithmetic: a pass is skipped when all its
+// rows lie below the ROI, and otherwise loads unclamped from a scalar row base plus the lane's fixed offset
+// (rows up to kRPP - 1 past the ROI's last: it ends >= 16 rows above its level's last row, kEdge - 3, so
+// they are inside the level) and stores at an immediate LDS offset (those rows land in the map, cleared
+// after the commit).  No VALU per pass; the general form below clamps every lane's row (3 VALU per pass).
+template <int TP, int LD>
+__device__ __forceinline__ void fast_issue0(const FastCellSrc& S, const FastLaneMap<TP>& M, FastPrefetch<LD>& F)
+{
+    constexpr int kRPP = FastLaneMap<TP>::kRPP;
+    static_assert(kRPP - 1 <= kEdge - 3, "a pass's rows past the ROI stay inside the level");
+    if (S.rh <= 0 || S.nd <= 0) return;   // wave-uniform
+    const uint32_t lo = __umul24((uint32_t)M.rl, (uint32_t)S.pitch) + 4u * (uint32_t)min(M.kl, S.nd - 1);
+    // a buffer descriptor over the ROI: the pass's row offset goes in the scalar offset (buffer_load ... offen
+    // with soffset), the lane's in the vector one
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.src, (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < LD; ++u)
+        if (u * kRPP < S.rh)   // wave-uniform
+            F.w[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo, u * kRPP * S.pitch, 0);
+}
+template <int TP, int LD>
+__device__ __forceinline__ void fast_commit0(const FastPrefetch<LD>& F, const FastCellSrc& S, const FastLaneMap<TP>& M,
+                                             uint8_t* tile)
+{
+    constexpr int kRPP = FastLaneMap<TP>::kRPP;
+    if (S.rh > 0 && S.nd > 0) {   // wave-uniform (empty cells store nothing)
+        const uint32_t a = __umul24((uint32_t)M.rl, (uint32_t)TP) + 4u * (uint32_t)min(M.kl, S.nd - 1) +
+                           (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)tile;
+#pragma unroll
+        for (int u = 0; u < LD; ++u)
+            if (u * kRPP < S.rh)   // wave-uniform; an immediate offset
+                *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)(a + (uint32_t)(u * kRPP * TP)) = F.w[u];
+    }
+}
+
 // 4 pixels of ROI row r from column 4 kl: the lane's dword and its neighbour's realigned by the row's
 // byte shift (v_alignbyte uses the shift's low two bits, so the shift of pass u is the lane's first one
 // plus a uniform step), one 4-byte LDS store at an immediate offset per pass
@@ -866,14 +901,14 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     FastCellSrc S = cell_src(C);
     const FastLaneMap<TP> M(lane);
     FastPrefetch<LD> F;
-    fast_issue(S, M, 0, F);
+    fast_issue0(S, M, F);
 
 #pragma unroll 1
     for (int c = c0; c < c1; ++c) {
         const int dw = C.roi_w - 6, dh = C.roi_h - 6;
         const Cell Cc = C;
         FP_STAMP(7);
-        fast_commit(F, S, M, 0, tile);
+        fast_commit0(F, S, M, tile);
         for (int u0 = LD; u0 * FastLaneMap<TP>::kRPP < S.rh; u0 += LD) {   // ROIs beyond LD passes
             FastPrefetch<LD> R;
             fast_issue(S, M, u0, R);
@@ -887,7 +922,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         if (c + 1 < c1) {   // prefetch the next cell (registers only; lands under the passes below)
             C = load_cell(c + 1);
             S = cell_src(C);
-            fast_issue(S, M, 0, F);
+            fast_issue0(S, M, F);
         }
         if (dw <= 0 || dh <= 0) {
             wave_lds_sync();
