@@ -595,8 +595,11 @@ __host__ __device__ inline int fast_list_cap(int rw, int rh) { return (rh - 6) *
 // Output buffer (packed candidates) of the wave's cells, written to HBM once after its last cell: a global
 // store inside the cell loop would make the next cell's wait for its prefetched ROI (vmcnt counts loads
 // and stores, completed in issue order) wait for the store's round trip as well.
-constexpr int kFastObCap = 128;
-constexpr int kFastScratch = 256;   // a dword per lane after obuf (pass 1's masked-off writes)
+#ifndef ORBX_FAST_OBCAP
+#define ORBX_FAST_OBCAP 128
+#endif
+constexpr int kFastObCap = ORBX_FAST_OBCAP;
+constexpr int kFastScratch = 128;   // a u16 per lane after obuf (the masked-off lanes' list and map writes)
 __host__ __device__ inline size_t fast_list_bytes(int rw, int rh) { return (2 * (size_t)fast_list_cap(rw, rh) + 3) & ~(size_t)3; }
 __host__ __device__ inline size_t fast_wave_bytes(int rw, int rh)
 {
@@ -847,7 +850,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     uint16_t* list = (uint16_t*)(map + fast_map_bytes(rw, rh));
     uint32_t* obuf = (uint32_t*)((uint8_t*)list + fast_list_bytes(rw, rh));
     const int lcap = fast_list_cap(rw, rh);
-    uint16_t* const bscratch = (uint16_t*)(obuf + kFastObCap + lane);
+    uint16_t* const bscratch = (uint16_t*)(obuf + kFastObCap) + lane;
     uint32_t* fslots = slots + (size_t)f * G->slots_per_frame;
     // lane i: the wave's cell c0 + i -- its candidate count, obuf offset (buffered cells) and the slot its
     // candidates start at.  The wave's cells (one level: the cell lists are padded to whole waves) are
@@ -1150,7 +1153,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
     if (obn > 0) {   // the buffered cells: one run from the wave's first cell's slot base (128-byte aligned)
         uint32_t* out = fslots + cells[c0].slot_base;
         if (lane < obn) out[lane] = obuf[lane];
-        if (lane + 64 < obn) out[lane + 64] = obuf[lane + 64];
+        if (kFastObCap > 64 && lane + 64 < obn) out[lane + 64] = obuf[lane + 64];
         static_assert(kFastObCap <= 128, "two stores per lane");
     }
     // a cell written straight to its own slots is flagged; the buffered ones' slots follow from the counts
