@@ -1422,9 +1422,9 @@ __host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap, int ixb = 2
         o += (bytes + 15) & ~(size_t)15;
         return r;
     };
-    int p2 = 1;
-    while (p2 < lcap) p2 <<= 1;
-    const int scan_n = (4 * lcap > cellcap ? 4 * lcap : cellcap) + 1;
+    // scans: the cells' counts (cellcap), a round's split ranks (<= lcap) and phase 2's non-split flags from
+    // lcap + 1 (scan2), so 2 lcap + 2 entries cover the rounds
+    const int scan_n = (2 * lcap + 2 > cellcap ? 2 * lcap + 2 : cellcap) + 1;
     L.scan = take(sizeof(uint32_t) * scan_n);
     L.rect = take(sizeof(int16_t) * 4 * 2 * lcap);   // [2 buffers][4 coords][lcap]
     L.cnt = take(sizeof(uint32_t) * 2 * lcap);
@@ -1436,8 +1436,10 @@ __host__ __device__ inline QtLayout qt_layout(int lcap, int cellcap, int ixb = 2
     L.cpos = take((size_t)ixb * 4 * lcap);
     L.vprev = take((size_t)ixb * lcap);
     L.vnew = take((size_t)ixb * lcap);
-    L.skey = take(sizeof(uint32_t) * (p2 + 4));   // + padding to whole 16-byte groups (rank sort)
-    L.best = take(sizeof(unsigned long long) * lcap);
+    L.skey = take(sizeof(uint32_t) * (lcap + 4));   // + padding to whole 16-byte groups (rank sort)
+    // the retain step's per-node best keys reuse the node rectangles (dead once the rounds end: 16 bytes per
+    // node against 8), which takes 8 bytes per node off the workgroup's LDS
+    L.best = L.rect;
     L.wsum = take(sizeof(uint32_t) * (QT_NW + 1));
     L.sh = take(sizeof(int) * 16);
     L.kpa = take(sizeof(uint32_t) * kpn);
@@ -1479,7 +1481,7 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 #define ORBX_QT1_WPE 4
 #endif
 #ifndef ORBX_QT2_WPE
-#define ORBX_QT2_WPE 5
+#define ORBX_QT2_WPE 6
 #endif
 // Minimum waves per SIMD (HIP's second __launch_bounds__ argument), i.e. a VGPR budget per template:
 //   <512,16> (level 0) 4: 128 VGPRs (7 dwords spilled) instead of the compiler's 172, so two workgroups
@@ -1490,6 +1492,10 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 // Round 3: levels 1 and 2-7 at 128 / 96 VGPRs (4 / 5 waves per SIMD, no spill): their occupancy is set by
 // LDS and workgroup waves anyway (2 and 5 workgroups per CU), quadtree 0.165 -> 0.164 ms.
 // FAST at 5 (94 VGPRs, no spill) measured slower (485 -> 495 us) and keeps the compiler's choice.
+// Round 5: <256,4> at 6 (80 VGPRs, 5 dwords spilled) once its LDS fits six workgroups per CU (the retain
+// step's keys over the node rectangles, the scan array at 2 lcap + 3 entries instead of 4 lcap + 1, the rank
+// sort's keys at lcap + 4 instead of the next power of two: 28.7 -> 23.0 KB at KITTI): 135 -> 120 us per
+// 1,024 frames; at 7 (72 VGPRs, 12 dwords spilled) 123 us.
 #define ORBX_QT_WPE(NT, KPT, G) ((G) ? 1                                          \
                                  : ((NT) == 512 && (KPT) == 16) ? ORBX_QT0_WPE  \
                                  : ((NT) == 512 && (KPT) == 8) ? ORBX_QT1_WPE   \
