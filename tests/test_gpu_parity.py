@@ -94,6 +94,23 @@ def test_extract_parity(orbref, cuda, name, W, H, nfeat, kind):
         assert_same_keypoints(klist[f], ref.keypoints, dlist[f], ref.descriptors, "%s f%d" % (name, f))
 
 
+@pytest.mark.parametrize("W,H", [(642, 480), (643, 481), (1243, 377)])
+@pytest.mark.parametrize("batch", [2, 10])
+def test_extract_parity_row_alignments(orbref, cuda, W, H, batch):
+    """Frames whose rows start at every byte alignment mod 4 (widths 642 / 643 / 1243 besides the suite's 640 and
+    1241): describe's per-row-shift horizontal pass, FAST's unaligned ROI loads and the level-1 pyramid's
+    unaligned source rows, for the small-batch (2 frames: one keypoint and one cell per wave, fused pyramid) and
+    the large-batch (10 frames: four keypoints and three cells per wave, one launch per level) kernels."""
+    frames = _frames("gen", W, H, batch, seed0=31)
+    ex = _extractor(1000)
+    p = orbref.make_params(1000, 1.2, 8, 20, 7)
+    _, _, _, _, klist, dlist = _run_batch(ex, frames, cuda)
+    for f in range(batch):
+        ref = orbref.extract(frames[f], p)
+        assert len(ref.keypoints) >= 500
+        assert_same_keypoints(klist[f], ref.keypoints, dlist[f], ref.descriptors, "%dx%d b%d f%d" % (W, H, batch, f))
+
+
 def test_host_api_matches_batch(orbref, cuda):
     import orbx_synth
     img = orbx_synth.gen_image(11, 640, 480)
