@@ -2564,6 +2564,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
 #pragma unroll
             for (int k = 0; k < 5; ++k) q[ji][k] = src[k];
         }
+        int pv[kIcGroup][2];   // the lane's partial moments of the group's keypoints: (m10, m01)
 #pragma unroll
         for (int ji = 0; ji < kIcGroup; ++ji) {
             uint32_t s1 = 0u, s0 = 0u;
@@ -2573,11 +2574,46 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                 s1 = __builtin_amdgcn_udot4(w, W1[k], s1, false);
                 s0 = __builtin_amdgcn_udot4(w, W0[k], s0, false);
             }
-            const int x10 = wave_sum((int)s1 - 16 * (int)s0);
-            const int x01 = wave_sum(vrow * (int)s0);
-            if (lane == j0 + ji) {
-                ic_m10 = x10;
-                ic_m01 = x01;
+            pv[ji][0] = (int)s1 - 16 * (int)s0;
+            pv[ji][1] = vrow * (int)s0;
+        }
+        if constexpr (kIcGroup == 4) {
+            // the eight wave sums as one reduce-scatter: v_permlane32_swap and v_permlane16_swap exchange half /
+            // quarter waves, so each swap-and-add halves the lanes of two sums at once and packs them into one
+            // register; the last 16-lane step is the DPP butterfly of wave_sum.  28 VALU for the group instead of
+            // eight wave_sum (64).  Quarters of Q0: (m10 k0, m10 k1, m01 k0, m01 k1); of Q1 the same for k2, k3.
+            auto swap_add = [](int a, int b, bool sixteen) {
+                const auto r = sixteen ? __builtin_amdgcn_permlane16_swap(a, b, false, false)
+                                       : __builtin_amdgcn_permlane32_swap(a, b, false, false);
+                return (int)r[0] + (int)r[1];
+            };
+            auto row_sum = [](int v) {
+                v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+                v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
+                v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true);   // row_half_mirror
+                return v + __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true);   // row_mirror
+            };
+            const int r0 = swap_add(pv[0][0], pv[0][1], false), r1 = swap_add(pv[1][0], pv[1][1], false);
+            const int r2 = swap_add(pv[2][0], pv[2][1], false), r3 = swap_add(pv[3][0], pv[3][1], false);
+            const int q0 = row_sum(swap_add(r0, r1, true)), q1 = row_sum(swap_add(r2, r3, true));
+            const int m10[4] = {__builtin_amdgcn_readlane(q0, 0), __builtin_amdgcn_readlane(q0, 16),
+                                __builtin_amdgcn_readlane(q1, 0), __builtin_amdgcn_readlane(q1, 16)};
+            const int m01[4] = {__builtin_amdgcn_readlane(q0, 32), __builtin_amdgcn_readlane(q0, 48),
+                                __builtin_amdgcn_readlane(q1, 32), __builtin_amdgcn_readlane(q1, 48)};
+#pragma unroll
+            for (int ji = 0; ji < 4; ++ji)
+                if (lane == j0 + ji) {
+                    ic_m10 = m10[ji];
+                    ic_m01 = m01[ji];
+                }
+        } else {
+#pragma unroll
+            for (int ji = 0; ji < kIcGroup; ++ji) {
+                const int x10 = wave_sum(pv[ji][0]), x01 = wave_sum(pv[ji][1]);
+                if (lane == j0 + ji) {
+                    ic_m10 = x10;
+                    ic_m01 = x01;
+                }
             }
         }
     }
@@ -2677,7 +2713,11 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         // the u16 sample table over rowT's first 768 bytes (one wave: its LDS reads and writes complete in
         // issue order, so every sample's rowT reads precede the table writes)
         typedef float f2v __attribute__((ext_vector_type(2)));
-        const f2v va = {a, a}, vb = {b, b}, mg = {kRoundMagic, kRoundMagic};
+        // (the magic pair through an opaque scalar move: as a literal the compiler splits BX's packed add into two
+        // v_add_f32, VOP3P having no literal operand)
+        float mgs = kRoundMagic;
+        asm("" : "+s"(mgs));
+        const f2v va = {a, a}, vb = {b, b}, mg = {mgs, mgs};
         uint32_t tv[kDescSlots];
 #pragma unroll
         for (int q = 0; q < kDescSlots; q += 2) {
