@@ -1084,63 +1084,66 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const int xr0 = Cc.roi_x0 + 3 - kMinBorder, yr0 = Cc.roi_y0 + 3 - kMinBorder;
             const int ci = c - c0;
             const bool buffered = !direct && obn + kept_n <= kFastObCap;   // wave-uniform
-            uint32_t* dst;
+            const int rounds = (nf2 + nbk + 63) >> 6;
+            // (one copy of the emission per destination, so that each store's address space is known: a pointer
+            // that may be either compiles to flat stores, which wait on both counters)
+            auto emit = [&](uint32_t* dst) {
+                if (nbk == 0) {
+                    int idx = 0;
+                    for (int r = 0; r < rounds; ++r) {
+                        const bool keep = (keepm[r >> 6] >> (r & 63)) & 1ull;
+                        const unsigned long long km = ballot64(keep);
+                        if (km == 0ull) continue;   // wave-uniform
+                        if (keep) {
+                            const int m = list[lane + (r << 6)];   // window (i, j) at m = i * TP + j
+                            const int wi = m / TP, wj = m - wi * TP;
+                            const int sc = map[m + TP + 1];
+                            dst[idx + lanes_below(km)] = pack_kp((uint32_t)(xr0 + wj), (uint32_t)(yr0 + wi), (uint32_t)(sc - 1));
+                        }
+                        idx += __popcll(km);
+                    }
+                } else {
+                    for (int i = lane; i < dh; i += 64) kept[i] = 0ull;
+                    wave_lds_sync();
+                    for (int r = 0; r < rounds; ++r) {
+                        if (!((keepm[r >> 6] >> (r & 63)) & 1ull)) continue;
+                        const int j = lane + (r << 6);
+                        const int m = list[j < nf2 ? j : lcap - 1 - (j - nf2)];
+                        const int wi = m / TP;
+                        atomicOr(&kept[wi], 1ull << (m - wi * TP));
+                    }
+                    wave_lds_sync();
+                    // lane i emits window row i (rows <= 60): prefix sum of the row counts gives its first slot
+                    const unsigned long long rowbits = lane < dh ? kept[lane] : 0ull;
+                    const int cnt = __popcll(rowbits);
+                    int base = 0;
+                    {
+                        int v = cnt;
+                        // inclusive wave scan of the counts
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const int u = __shfl_up(v, o);
+                            if (lane >= o) v += u;
+                        }
+                        base = v - cnt;
+                    }
+                    unsigned long long bits = rowbits;
+                    int idx = base;
+                    while (bits) {
+                        const int jj = __builtin_ctzll(bits);
+                        bits &= bits - 1;
+                        const int sc = map[(lane + 1) * TP + jj + 1];
+                        dst[idx++] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + lane), (uint32_t)(sc - 1));
+                    }
+                }
+            };
             if (buffered) {
                 if (lane == ci) c_off = obn;
-                dst = obuf + obn;
+                emit(obuf + obn);
                 obn += kept_n;
             } else {   // rare: more than obuf holds
                 direct = true;
-                dst = fslots + Cc.slot_base;
-            }
-            const int rounds = (nf2 + nbk + 63) >> 6;
-            if (nbk == 0) {
-                int idx = 0;
-                for (int r = 0; r < rounds; ++r) {
-                    const bool keep = (keepm[r >> 6] >> (r & 63)) & 1ull;
-                    const unsigned long long km = ballot64(keep);
-                    if (km == 0ull) continue;   // wave-uniform
-                    if (keep) {
-                        const int m = list[lane + (r << 6)];   // window (i, j) at m = i * TP + j
-                        const int wi = m / TP, wj = m - wi * TP;
-                        const int sc = map[m + TP + 1];
-                        dst[idx + lanes_below(km)] = pack_kp((uint32_t)(xr0 + wj), (uint32_t)(yr0 + wi), (uint32_t)(sc - 1));
-                    }
-                    idx += __popcll(km);
-                }
-            } else {
-                for (int i = lane; i < dh; i += 64) kept[i] = 0ull;
-                wave_lds_sync();
-                for (int r = 0; r < rounds; ++r) {
-                    if (!((keepm[r >> 6] >> (r & 63)) & 1ull)) continue;
-                    const int j = lane + (r << 6);
-                    const int m = list[j < nf2 ? j : lcap - 1 - (j - nf2)];
-                    const int wi = m / TP;
-                    atomicOr(&kept[wi], 1ull << (m - wi * TP));
-                }
-                wave_lds_sync();
-                // lane i emits window row i (rows <= 60): prefix sum of the row counts gives its first slot
-                const unsigned long long rowbits = lane < dh ? kept[lane] : 0ull;
-                const int cnt = __popcll(rowbits);
-                int base = 0;
-                {
-                    int v = cnt;
-                    // inclusive wave scan of the counts
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const int u = __shfl_up(v, o);
-                        if (lane >= o) v += u;
-                    }
-                    base = v - cnt;
-                }
-                unsigned long long bits = rowbits;
-                int idx = base;
-                while (bits) {
-                    const int jj = __builtin_ctzll(bits);
-                    bits &= bits - 1;
-                    const int sc = map[(lane + 1) * TP + jj + 1];
-                    dst[idx++] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + lane), (uint32_t)(sc - 1));
-                }
+                emit(fslots + Cc.slot_base);
             }
         }
         if (lane == c - c0) cnt_all = kept_n;
