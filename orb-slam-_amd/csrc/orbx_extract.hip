@@ -2562,7 +2562,10 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             int pitch;
             const uint8_t* img = level_base(P, G, f, l, pitch);
             const uintptr_t a = (uintptr_t)(img + (size_t)(cy + vrow) * pitch + (cx - 15 + 16 * ich));
-            const uint32_t* src = (const uint32_t*)(a & ~(uintptr_t)3);
+            // (as a global pointer: an integer cast loses the address space, and flat loads count against both
+            // wait counters)
+            const __attribute__((address_space(1))) uint32_t* src =
+                (const __attribute__((address_space(1))) uint32_t*)(a & ~(uintptr_t)3);
             qs[ji] = (uint32_t)(a & 3);
 #pragma unroll
             for (int k = 0; k < 5; ++k) q[ji][k] = src[k];
