@@ -85,6 +85,47 @@ __device__ __forceinline__ int ham_u4(const uint4& a0, const uint4& a1, const ui
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+// A view with its arrays as global pointers: the struct's pointers are loaded from memory, where the compiler no
+// longer knows they are global, and reads through them would be flat loads (which wait on both counters).
+#define ORBX_G1 __attribute__((address_space(1)))
+struct GView {
+    const ORBX_G1 orbx_keypoint* kps;
+    const ORBX_G1 uint8_t* desc;
+    const ORBX_G1 uint8_t* has_mp;
+    const ORBX_G1 float* u_right;
+    const ORBX_G1 int32_t* fv_node;
+    const ORBX_G1 int32_t* fv_ptr;
+    const ORBX_G1 int32_t* fv_idx;
+    int32_t n, fv_nnodes;
+};
+__device__ __forceinline__ orbx_keypoint kp_at(const ORBX_G1 orbx_keypoint* k, int i)
+{
+    const ORBX_G1 orbx_keypoint& q = k[i];
+    orbx_keypoint r;
+    r.x = q.x;
+    r.y = q.y;
+    r.size = q.size;
+    r.angle = q.angle;
+    r.response = q.response;
+    r.octave = q.octave;
+    r.class_id = q.class_id;
+    return r;
+}
+// descriptor i's 32 bytes as two uint4
+__device__ __forceinline__ void desc_at(const ORBX_G1 uint8_t* d, int i, uint4& a, uint4& b)
+{
+    const ORBX_G1 uint32_t* q = (const ORBX_G1 uint32_t*)(d + (size_t)i * 32);
+    a = make_uint4(q[0], q[1], q[2], q[3]);
+    b = make_uint4(q[4], q[5], q[6], q[7]);
+}
+__device__ __forceinline__ GView gview(const orbm_bow_view& v)
+{
+    return GView{(const ORBX_G1 orbx_keypoint*)v.kps, (const ORBX_G1 uint8_t*)v.desc,
+                 (const ORBX_G1 uint8_t*)v.has_mp, (const ORBX_G1 float*)v.u_right,
+                 (const ORBX_G1 int32_t*)v.fv_node, (const ORBX_G1 int32_t*)v.fv_ptr,
+                 (const ORBX_G1 int32_t*)v.fv_idx, v.n, v.fv_nnodes};
+}
+
 __global__ __launch_bounds__(256) void k_bow_nodes(int mode, const orbm_bow_view* __restrict__ V1,
                                                    const orbm_bow_view* __restrict__ V2,
                                                    const orbm_triang_params* __restrict__ TP, float nnratio,
@@ -94,7 +135,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(int mode, const orbm_bow_view
     __shared__ uint32_t s_done[4][kBowWords];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // uniform
     const int p = blockIdx.y;
-    const orbm_bow_view A = V1[p], B = V2[p];
+    const GView A = gview(V1[p]), B = gview(V2[p]);
     const int k = blockIdx.x * 4 + wave;
     if (k >= A.fv_nnodes) return;   // wave-uniform; no block barriers below
     const int node = A.fv_node[k];
@@ -126,12 +167,10 @@ __global__ __launch_bounds__(256) void k_bow_nodes(int mode, const orbm_bow_view
     if (lane < nb) {
         c_idx2 = B.fv_idx[b0 + lane];
         c_mp2 = B.has_mp ? B.has_mp[c_idx2] != 0 : false;
-        const uint4* d2 = reinterpret_cast<const uint4*>(B.desc + (size_t)c_idx2 * 32);
-        c_e0 = d2[0];
-        c_e1 = d2[1];
+        desc_at(B.desc, c_idx2, c_e0, c_e1);
         if (tri) {
             c_st2 = B.u_right ? B.u_right[c_idx2] >= 0 : false;
-            c_kp2 = B.kps[c_idx2];
+            c_kp2 = kp_at(B.kps, c_idx2);
         }
     }
     const int n1 = a1 - a0;
@@ -144,10 +183,8 @@ __global__ __launch_bounds__(256) void k_bow_nodes(int mode, const orbm_bow_view
             const bool mp = A.has_mp ? A.has_mp[l_idx1] != 0 : false;
             const bool st = tri && A.u_right ? A.u_right[l_idx1] >= 0 : false;
             l_flags = (mp ? 1 : 0) | (st ? 2 : 0);
-            const uint4* d1 = reinterpret_cast<const uint4*>(A.desc + (size_t)l_idx1 * 32);
-            l_q0 = d1[0];
-            l_q1 = d1[1];
-            const orbx_keypoint kp = A.kps[l_idx1];
+            desc_at(A.desc, l_idx1, l_q0, l_q1);
+            const orbx_keypoint kp = kp_at(A.kps, l_idx1);
             l_x = kp.x;
             l_y = kp.y;
             l_ang = kp.angle;
@@ -181,9 +218,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(int mode, const orbm_bow_view
                 if (c > 0) {
                     idx2 = B.fv_idx[b0 + pos];
                     mp2 = B.has_mp ? B.has_mp[idx2] != 0 : false;
-                    const uint4* d2 = reinterpret_cast<const uint4*>(B.desc + (size_t)idx2 * 32);
-                    e0 = d2[0];
-                    e1 = d2[1];
+                    desc_at(B.desc, idx2, e0, e1);
                 }
                 bool ok;
                 if (tri) {
@@ -198,7 +233,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(int mode, const orbm_bow_view
                     const bool stereo2 = c > 0 ? (B.u_right ? B.u_right[idx2] >= 0 : false) : c_st2;
                     if (T.only_stereo && !stereo2) continue;
                     if (dist > kTH_LOW) continue;
-                    const orbx_keypoint kp2 = c > 0 ? B.kps[idx2] : c_kp2;
+                    const orbx_keypoint kp2 = c > 0 ? kp_at(B.kps, idx2) : c_kp2;
                     if (!stereo1 && !stereo2) {   // :800-806
                         const float distex = T.ex - kp2.x, distey = T.ey - kp2.y;
                         if (__builtin_fmaf(distex, distex, distey * distey) < 100 * T.scale2[kp2.octave]) continue;

@@ -41,10 +41,14 @@ __device__ __forceinline__ void ig_taps(const uint8_t* __restrict__ row, int sx,
         const int sh = (int)(a - a4) * 8;
         unsigned long long v;
         if (kWords == 2) {
-            const uint2 w = *reinterpret_cast<const uint2*>(a4);
+            // (through a global pointer: an integer cast loses the address space, and flat loads count against both
+            // wait counters)
+            const __attribute__((address_space(1))) uint32_t* q = (const __attribute__((address_space(1))) uint32_t*)a4;
+            const uint2 w = make_uint2(q[0], q[1]);
             v = ((unsigned long long)w.y << 32 | w.x) >> sh;
         } else {
-            const uint3 w = *reinterpret_cast<const uint3*>(a4);
+            const __attribute__((address_space(1))) uint32_t* q = (const __attribute__((address_space(1))) uint32_t*)a4;
+            const uint3 w = make_uint3(q[0], q[1], q[2]);
             const unsigned long long lo = (unsigned long long)w.y << 32 | w.x;
             v = sh ? (lo >> sh) | ((unsigned long long)w.z << (64 - sh)) : lo;
         }

@@ -471,9 +471,12 @@ __global__ __launch_bounds__(SI_BUILD_NT) void k_si_build(const orbx_keypoint* _
         }
         __syncthreads();
     }
-    const uint32_t* keys = staged ? (const uint32_t*)skeys : gkeys + (size_t)fb * cap;
-    const float2* xy = staged ? (const float2*)sxy : gxy + (size_t)fb * cap;
-    si_colstart(keys, ng, colstart, tid, SI_BUILD_NT);
+    // global and LDS sources kept apart (a pointer that may be either compiles to flat loads, which wait on both
+    // counters)
+    const uint32_t* keys = gkeys + (size_t)fb * cap;
+    const float2* xy = gxy + (size_t)fb * cap;
+    if (staged) si_colstart((const uint32_t*)skeys, ng, colstart, tid, SI_BUILD_NT);
+    else si_colstart(keys, ng, colstart, tid, SI_BUILD_NT);
     __syncthreads();
     const orbx_keypoint* k1 = kps + (size_t)fa * cap;
     const uint8_t* d1 = desc + (size_t)fa * cap * 32;
