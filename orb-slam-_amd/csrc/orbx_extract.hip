@@ -23,6 +23,19 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The dynamic LDS of a kernel without static LDS, as the constant address 0.  An extern __shared__ array's
+// address is a symbol the compiler adds to every LDS address it forms from a runtime offset (one v_add of 0
+// each, and registers to hold the sums: k_quadtree<256,4> and <512,16> spilled 16 and 8 bytes per lane to
+// scratch with it).  The backend lowers __builtin_amdgcn_groupstaticsize (the static LDS size) to a
+// constant, so base plus offset folds into the instructions; the check below costs one scalar compare of
+// two constants per wave.
+__device__ __forceinline__ uint8_t* dyn_lds()
+{
+    const uint32_t base = __builtin_amdgcn_groupstaticsize();
+    if (base != 0u) __builtin_trap();   // a kernel with static LDS would need the rounded offset and a larger launch size
+    return (uint8_t*)(__attribute__((address_space(3))) uint8_t*)(uintptr_t)base;
+}
+
 __device__ __forceinline__ int lanes_below(unsigned long long mask)
 {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -838,14 +851,13 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                                                    int cpw)
 {
     // cells [cb, ce); LDS sized from the group's largest cell ROI (rw x rh)
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_fast[];
     const int lane = threadIdx.x;
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x;
     const int c0 = cb + (lb - f * gridDim.x) * cpw;
     const int c1 = min(c0 + cpw, ce);
     if (c0 >= c1) return;   // wave-uniform; no block barriers below
-    uint8_t* tile = s_fast;
+    uint8_t* tile = dyn_lds();
     uint8_t* map = tile + (size_t)rh * TP;
     uint16_t* list = (uint16_t*)(map + fast_map_bytes(rw, rh));
     uint32_t* obuf = (uint32_t*)((uint8_t*)list + fast_list_bytes(rw, rh));
@@ -950,19 +962,12 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const int rstep = 64 >> cw_shift;
             const int rlane = lane >> cw_shift;
             const unsigned long long colmask = ballot64(col < dw);
-            // lanes of the first k rows of a row step (whole rows of cw lanes): scalar arithmetic, no compare
-            // (branch-free: a branch here splits the loop body, and the byte loads above it get re-masked)
-            auto rows_below = [&](int k) -> unsigned long long {
-                return ballot64(rlane < k);
-            };
             int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
-            // LDS byte address of list[lcap - nb]: a back write is one v_lshl_add from it, and its update one
-            // scalar subtract of twice the count
+            // LDS address of list[lcap - nb] in u16 entries: a back write's byte address is one v_add_lshl from
+            // it, and its update one scalar subtract of the count
             const uint32_t bend = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)(list + lcap);
-            uint32_t bptr = bend >> 1;   // in u16 entries: the count update is one scalar subtract
+            uint32_t bptr = bend >> 1;
             const int rlane_b = rlane + rstep;
-            const uint32_t fbeg = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)list;
-            uint32_t fptr = fbeg;
             // full trips (both row steps inside the window) take the column mask alone; the last, partial
             // trip its row masks, once (the loop body is a lambda of the two masks, inlined twice)
             int rem = dh;
@@ -1523,7 +1528,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     using Ix = typename std::conditional<kG, uint32_t, uint16_t>::type;
     constexpr Ix kNoneI = (Ix)~(Ix)0;
     constexpr uint32_t kPosMask = kG ? 0xFFFFFFFFu : 0xFFFFu;   // node position bits of a keypoint's node word
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* const smem = dyn_lds();   // the dynamic LDS (no static LDS in this kernel)
     const int tid = threadIdx.x;
 #ifdef ORBX_QT_PROF
     const long long qt_t0 = clock64();
