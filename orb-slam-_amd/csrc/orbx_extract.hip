@@ -931,7 +931,11 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         }
         const int mapn = (dh + 2) * TP;
         FP_STAMP(0);
-        for (int i = lane; i < (mapn + 3) >> 2; i += 64) ((uint32_t*)map)[i] = 0u;
+        if constexpr (TP % 8 == 0) {   // the map (at rh * TP) and mapn are whole 8-byte words: half the stores
+            for (int i = lane; i < mapn >> 3; i += 64) ((uint2*)map)[i] = make_uint2(0u, 0u);
+        } else {
+            for (int i = lane; i < (mapn + 3) >> 2; i += 64) ((uint32_t*)map)[i] = 0u;
+        }
         wave_lds_sync();
         FP_STAMP(1);
         if (c + 1 < c1) {   // prefetch the next cell (registers only; lands under the passes below)
@@ -994,7 +998,14 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                 *lds_select(mbb, lds_u16(add_lshl1((uint32_t)lanes_below(mbb), bptr)), bscratch) = (uint16_t)(t + rstep * TP);
                 t += 2 * rstep * TP;
             };
-            for (; rem >= 2 * rstep; rem -= 2 * rstep) trip(colmask, colmask);
+            // a bottom-tested count of full trips: one scalar decrement, compare and branch per trip
+            const int nfull = rem / (2 * rstep);
+            if (nfull > 0) {
+                int k = nfull;
+                do trip(colmask, colmask);
+                while (--k > 0);
+            }
+            rem -= nfull * 2 * rstep;
             if (rem > 0) trip(colmask & ballot64(rlane < rem), colmask & ballot64(rlane_b < rem));
             nb = (int)((bend >> 1) - bptr);
         };
@@ -1503,7 +1514,9 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 // Round 5: <256,4> at 6 (80 VGPRs, 5 dwords spilled) once its LDS fits six workgroups per CU (the retain
 // step's keys over the node rectangles, the scan array at 2 lcap + 3 entries instead of 4 lcap + 1, the rank
 // sort's keys at lcap + 4 instead of the next power of two: 28.7 -> 23.0 KB at KITTI): 135 -> 120 us per
-// 1,024 frames; at 7 (72 VGPRs, 12 dwords spilled) 123 us.
+// 1,024 frames; at 7 (72 VGPRs, 12 dwords spilled) 123 us.  With the dynamic LDS at a constant base (dyn_lds)
+// none of the three spills at these budgets; <256,4> at 7 then spills 5 dwords (112 against 117 us, the
+// pipelined rate unchanged).
 #define ORBX_QT_WPE(NT, KPT, G) ((G) ? 1                                          \
                                  : ((NT) == 512 && (KPT) == 16) ? ORBX_QT0_WPE  \
                                  : ((NT) == 512 && (KPT) == 8) ? ORBX_QT1_WPE   \
