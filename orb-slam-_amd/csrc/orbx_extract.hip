@@ -731,25 +731,24 @@ __device__ __forceinline__ void fast_issue(const FastCellSrc& S, const FastLaneM
     }
 }
 
-// The first LD passes of a cell (u0 = 0) without per-pass address arithmetic: a pass is skipped when all its
-// rows lie below the ROI, and otherwise loads unclamped from a scalar row base plus the lane's fixed offset
-// (rows up to kRPP - 1 past the ROI's last: it ends >= 16 rows above its level's last row, kEdge - 3, so
-// they are inside the level) and stores at an immediate LDS offset (those rows land in the map, cleared
-// after the commit).  No VALU per pass; the general form below clamps every lane's row (3 VALU per pass).
+// The first LD passes of a cell (u0 = 0) without per-pass address arithmetic or tests: every pass loads, from
+// a scalar row offset plus the lane's fixed one, through a buffer descriptor whose size ends at the ROI's last
+// byte, so the rows past the ROI read zeros (gfx950's range check covers soffset too,
+// tools/probes/buffer_oob.hip) instead of each pass taking a scalar compare and branch.  The commit stores the
+// passes holding ROI rows at immediate LDS offsets (a partial pass's rows past the ROI land in the map,
+// cleared after the commit).  No VALU per pass; the general form below clamps every lane's row (3 VALU per pass).
 template <int TP, int LD>
 __device__ __forceinline__ void fast_issue0(const FastCellSrc& S, const FastLaneMap<TP>& M, FastPrefetch<LD>& F)
 {
     constexpr int kRPP = FastLaneMap<TP>::kRPP;
-    static_assert(kRPP - 1 <= kEdge - 3, "a pass's rows past the ROI stay inside the level");
     if (S.rh <= 0 || S.nd <= 0) return;   // wave-uniform
     const uint32_t lo = __umul24((uint32_t)M.rl, (uint32_t)S.pitch) + 4u * (uint32_t)min(M.kl, S.nd - 1);
-    // a buffer descriptor over the ROI: the pass's row offset goes in the scalar offset (buffer_load ... offen
-    // with soffset), the lane's in the vector one
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.src, (short)0, 0x7FFFFFFF, 0x00020000);
+    // the pass's row offset goes in the scalar offset (buffer_load ... offen with soffset), the lane's in the
+    // vector one
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)S.src, (short)0,
+                                                                         (S.rh - 1) * S.pitch + 4 * S.nd, 0x00020000);
 #pragma unroll
-    for (int u = 0; u < LD; ++u)
-        if (u * kRPP < S.rh)   // wave-uniform
-            F.w[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo, u * kRPP * S.pitch, 0);
+    for (int u = 0; u < LD; ++u) F.w[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, lo, u * kRPP * S.pitch, 0);
 }
 template <int TP, int LD>
 __device__ __forceinline__ void fast_commit0(const FastPrefetch<LD>& F, const FastCellSrc& S, const FastLaneMap<TP>& M,
