@@ -964,22 +964,26 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const int col = lane & ((1 << cw_shift) - 1);
             const int rstep = 64 >> cw_shift;
             const int rlane = lane >> cw_shift;
-            const unsigned long long colmask = ballot64(col < dw);
             int t = rlane * TP + col;   // the lane's window index m in the trip's first row step
             // LDS address of list[lcap - nb] in u16 entries: a back write's byte address is one v_add_lshl from
             // it, and its update one scalar subtract of the count
             const uint32_t bend = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)(list + lcap);
             uint32_t bptr = bend >> 1;
             const int rlane_b = rlane + rstep;
-            // full trips (both row steps inside the window) take the column mask alone; the last, partial
-            // trip its row masks, once (the loop body is a lambda of the two masks, inlined twice)
+            // Thresholds per lane: +inf in the lanes past the window's columns, so a full trip's compares need no
+            // column mask (two scalar ANDs per row step fewer).  The last, partial trip also takes its row masks
+            // (the loop body is a lambda of the two masks, inlined twice).
+            const _Float16 inf16 = __builtin_bit_cast(_Float16, (uint16_t)0x7C00);
+            const _Float16 th_hi = col < dw ? f_hi : inf16, th_lo = col < dw ? f_lo : inf16;
             int rem = dh;
-            auto trip = [&](const unsigned long long va, const unsigned long long vb) {
+            auto trip = [&](auto full_tag, const unsigned long long va, const unsigned long long vb) {
+                constexpr bool kFull = decltype(full_tag)::value;
                 const _Float16 qa = fast_compass_q<TP>(tile + t + (3 * TP + 3));
                 const _Float16 qb = fast_compass_q<TP>(tile + t + (rstep * TP + 3 * TP + 3));
-                const unsigned long long hqa = ballot64(qa > f_hi), hqb = ballot64(qb > f_hi);
-                const unsigned long long mfa = hqa & va, mba = ballot64(qa > f_lo) & ~hqa & va;
-                const unsigned long long mfb = hqb & vb, mbb = ballot64(qb > f_lo) & ~hqb & vb;
+                const unsigned long long hqa = ballot64(qa > th_hi), hqb = ballot64(qb > th_hi);
+                const unsigned long long lqa = ballot64(qa > th_lo) & ~hqa, lqb = ballot64(qb > th_lo) & ~hqb;
+                const unsigned long long mfa = kFull ? hqa : hqa & va, mba = kFull ? lqa : lqa & va;
+                const unsigned long long mfb = kFull ? hqb : hqb & vb, mbb = kFull ? lqb : lqb & vb;
                 // front entries are rare (about 2% of the pixels): one scalar test per trip skips both writes'
                 // exec save / restore and the count updates (s_or sets SCC)
                 if (mfa | mfb) {
@@ -1001,11 +1005,11 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const int nfull = rem / (2 * rstep);
             if (nfull > 0) {
                 int k = nfull;
-                do trip(colmask, colmask);
+                do trip(std::true_type{}, 0ull, 0ull);
                 while (--k > 0);
             }
             rem -= nfull * 2 * rstep;
-            if (rem > 0) trip(colmask & ballot64(rlane < rem), colmask & ballot64(rlane_b < rem));
+            if (rem > 0) trip(std::false_type{}, ballot64(rlane < rem), ballot64(rlane_b < rem));
             nb = (int)((bend >> 1) - bptr);
         };
         if constexpr (LD < 10) {   // (the 10-register prefetch kernels: 76 VGPRs, 6 waves per SIMD)
