@@ -1073,15 +1073,19 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             const int rounds = (nfr + nbk + 63) >> 6;
             int kept_n = 0;
             keepm[0] = keepm[1] = 0;
-            for (int r = 0; r < rounds; ++r) {
+            auto round = [&](int r, unsigned long long& km) {
                 const int j = lane + (r << 6);
                 // branch-free: lanes past the entries re-test the last one, masked out of the ballot
                 const int jc = min(j, nfr + nbk - 1);
                 const int k = list[jc < nfr ? jc : lcap - 1 - (jc - nfr)];
                 const bool keep = (j < nfr + nbk) & nms_keep<TP>(map + k + (TP + 1), (uint32_t)max(th, 1));
-                keepm[r >> 6] |= (unsigned long long)keep << (r & 63);
+                km |= (unsigned long long)keep << (r & 63);
                 kept_n += __popcll(ballot64(keep));
-            }
+            };
+            // one loop per mask word, so that the word is not selected by the round at run time
+            const int r1 = min(rounds, 64);
+            for (int r = 0; r < r1; ++r) round(r, keepm[0]);
+            for (int r = 64; r < rounds; ++r) round(r, keepm[1]);
             return kept_n;
         };
         unsigned long long keepm[2];
@@ -1109,10 +1113,10 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
             auto emit = [&](uint32_t* dst) {
                 if (nbk == 0) {
                     int idx = 0;
-                    for (int r = 0; r < rounds; ++r) {
-                        const bool keep = (keepm[r >> 6] >> (r & 63)) & 1ull;
+                    auto round = [&](int r, unsigned long long kw) {
+                        const bool keep = (kw >> (r & 63)) & 1ull;
                         const unsigned long long km = ballot64(keep);
-                        if (km == 0ull) continue;   // wave-uniform
+                        if (km == 0ull) return;   // wave-uniform
                         if (keep) {
                             const int m = list[lane + (r << 6)];   // window (i, j) at m = i * TP + j
                             const int wi = m / TP, wj = m - wi * TP;
@@ -1120,17 +1124,21 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                             dst[idx + lanes_below(km)] = pack_kp((uint32_t)(xr0 + wj), (uint32_t)(yr0 + wi), (uint32_t)(sc - 1));
                         }
                         idx += __popcll(km);
-                    }
+                    };
+                    for (int r = 0; r < min(rounds, 64); ++r) round(r, keepm[0]);
+                    for (int r = 64; r < rounds; ++r) round(r, keepm[1]);
                 } else {
                     for (int i = lane; i < dh; i += 64) kept[i] = 0ull;
                     wave_lds_sync();
-                    for (int r = 0; r < rounds; ++r) {
-                        if (!((keepm[r >> 6] >> (r & 63)) & 1ull)) continue;
+                    auto mark = [&](int r, unsigned long long kw) {
+                        if (!((kw >> (r & 63)) & 1ull)) return;
                         const int j = lane + (r << 6);
                         const int m = list[j < nf2 ? j : lcap - 1 - (j - nf2)];
                         const int wi = m / TP;
                         atomicOr(&kept[wi], 1ull << (m - wi * TP));
-                    }
+                    };
+                    for (int r = 0; r < min(rounds, 64); ++r) mark(r, keepm[0]);
+                    for (int r = 64; r < rounds; ++r) mark(r, keepm[1]);
                     wave_lds_sync();
                     // lane i emits window row i (rows <= 60): prefix sum of the row counts gives its first slot
                     const unsigned long long rowbits = lane < dh ? kept[lane] : 0ull;
