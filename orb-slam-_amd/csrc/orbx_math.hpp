@@ -5,7 +5,7 @@
 //   * glibc 2.35 cosf/sinf (sysdeps/ieee754/flt-32 sincosf.h; double
 //     evaluation, table of the x86-64 libm — constants read back from the
 //     host libm, algorithm verified equal to libm on every float in
-//     [0, 2*pi] by tests/test_sincos.py)                          SURVEY.md A.5 / F7
+//     [0, 2*pi] by tests/test_host_math.py)                          SURVEY.md A.5 / F7
 // The library is compiled with -ffp-contract=off; the FMAs below are the ones
 // glibc's x86-64 FMA variant forms and are written out explicitly.
 #pragma once

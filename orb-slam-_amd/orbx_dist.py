@@ -50,14 +50,24 @@ class Gatherer:
 
     Uses point-to-point sends to rank 0: each peer pushes over its own xGMI
     link, which is what a rank-0 collection needs on a point-to-point fabric
-    (a ring all-gather would push (G-1)x the bytes through every link)."""
+    (a ring all-gather would push (G-1)x the bytes through every link).
 
-    def __init__(self, payload: Payload, world: int, rank: int):
+    host_stage: the process group's backend cannot move device tensors (gloo between ranks that share
+    one GPU, the -m gpu test of the sharded replay): a peer copies its device payload into a pinned host
+    buffer (ordered after the work queued on the current stream) and sends that; rank 0 receives into
+    host buffers."""
+
+    def __init__(self, payload: Payload, world: int, rank: int, host_stage: bool = False):
         self.world, self.rank = world, rank
         self.payload = payload
+        self.host_stage = bool(host_stage) and payload.buf.is_cuda
         self.recv = None
+        self.stage = None
+        if world > 1 and self.host_stage and rank != 0:
+            self.stage = torch.empty(payload.nbytes, dtype=torch.uint8, pin_memory=True)
         if rank == 0 and world > 1:
-            self.recv = [torch.empty_like(payload.buf) for _ in range(world - 1)]
+            dev = torch.device("cpu") if self.host_stage else payload.buf.device
+            self.recv = [torch.empty(payload.nbytes, dtype=torch.uint8, device=dev) for _ in range(world - 1)]
 
     def gather_async(self):
         """Queue the hand-back and return its work handles without waiting.  The sends read the
@@ -68,7 +78,11 @@ class Gatherer:
         if self.rank == 0:
             ops = [dist.P2POp(dist.irecv, self.recv[r - 1], r) for r in range(1, self.world)]
         else:
-            ops = [dist.P2POp(dist.isend, self.payload.buf, 0)]
+            src = self.payload.buf
+            if self.stage is not None:
+                self.stage.copy_(src)   # waits for the current stream's work, then the D2H copy
+                src = self.stage
+            ops = [dist.P2POp(dist.isend, src, 0)]
         return list(dist.batch_isend_irecv(ops))
 
     @staticmethod
@@ -90,9 +104,9 @@ class HandBack:
     wait, not a host wait) only when the slot is about to overwrite it, so the hand-back of batch k
     overlaps the extraction of batch k + 1 on the same stream instead of sitting in its way."""
 
-    def __init__(self, batch: int, cap: int, device, world: int, rank: int, depth: int = 2):
+    def __init__(self, batch: int, cap: int, device, world: int, rank: int, depth: int = 2, host_stage: bool = False):
         self.payloads = [Payload(batch, cap, device) for _ in range(depth)]
-        self.gatherers = [Gatherer(p, world, rank) for p in self.payloads]
+        self.gatherers = [Gatherer(p, world, rank, host_stage) for p in self.payloads]
         self.pending = [[] for _ in range(depth)]
         self.k = 0
 

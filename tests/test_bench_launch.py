@@ -71,10 +71,23 @@ def test_spawn_relays_json_line_and_status(capfd):
 
 
 def test_gpus_n_refused_without_that_many_gpus():
-    # with fewer GPUs than --gpus the launcher refuses instead of starting ranks that would fail
-    import pytest
-    import torch
-    if torch.cuda.device_count() >= 2:
-        pytest.skip("this host has 2 GPUs")
-    r = _run(["--gpus", "2"])
+    # with fewer GPUs than --gpus the launcher refuses instead of starting ranks that would fail; the count
+    # comes from sysfs and the *_VISIBLE_DEVICES lists, never from a HIP call
+    r = _run(["--gpus", "2"], ROCR_VISIBLE_DEVICES="0")
     assert r.returncode == 2 and "GPU(s) visible" in r.stderr
+
+
+def test_visible_gpu_count_from_sysfs(tmp_path):
+    src = open(BENCH).read().split('\nif __name__ == "__main__":\n')[0]
+    ns = {"__file__": BENCH, "__name__": "bench_launch"}
+    exec(compile(src, BENCH, "exec"), ns)
+    count = ns["visible_gpu_count"]
+    nodes = tmp_path / "nodes"
+    for i, gfx in enumerate([0, 90500, 90500, 90500]):      # node 0: the CPU
+        (nodes / str(i)).mkdir(parents=True)
+        (nodes / str(i) / "properties").write_text("cpu_cores_count 4\ngfx_target_version %d\n" % gfx)
+    assert count({}, str(nodes)) == 3
+    assert count({"HIP_VISIBLE_DEVICES": "1"}, str(nodes)) == 1
+    assert count({"ROCR_VISIBLE_DEVICES": "0,1,2,3,4"}, str(nodes)) == 3
+    assert count({}, str(tmp_path / "absent")) is None
+    assert count({"CUDA_VISIBLE_DEVICES": "0,1"}, str(tmp_path / "absent")) == 2

@@ -59,3 +59,23 @@ def test_level0_at_the_4096_px_side(orbref, cuda):
     frames = np.stack([orbx_synth.gen_image(62 + f, 4096, 320) for f in range(9)])
     ref = _check(orbref, img, 4000, 1.2, 8, 20, 7, "4096 wide", frames, cuda)
     assert ref.keypoints["x"].max() > 4000
+
+
+def test_buffer_range_check_covers_soffset(cuda):
+    """k_fast_cells' first staging passes (fast_issue0) load a partial last pass's rows past the cell ROI through
+    a buffer descriptor sized to end at the ROI's last byte, with the pass's row offset in the scalar offset.
+    That is memory-safe only if gfx950's range check tests voffset + soffset against num_records, so that those
+    loads return zeros without touching memory.  tools/probes/buffer_oob.hip pins it: a 64-byte descriptor over
+    nonzero data, loads at soffset 0 / 64 / 256."""
+    import ctypes
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "tools", "probes", "liboob_probe.so")
+    assert os.path.exists(path), "liboob_probe.so missing: run __graft_entry__.build()"
+    lib = ctypes.CDLL(path)
+    r = (ctypes.c_uint32 * (3 * 64))()
+    assert lib.oob_probe_run(r) == 0
+    v = np.frombuffer(r, dtype=np.uint32).reshape(3, 64)
+    want0 = np.where(np.arange(64) < 16, 0x1000 + np.arange(64), 0).astype(np.uint32)
+    assert np.array_equal(v[0], want0), v[0]                   # the descriptor's 16 dwords, zeros past them
+    assert not v[1].any() and not v[2].any(), (v[1], v[2])     # soffset moves every lane past num_records
