@@ -312,9 +312,17 @@ def cpu_topology():
                 info[k.strip()] = v.strip()
     except Exception:
         pass
-    # one CPU per physical core first, then the SMT siblings
+    # the job's CPU quota (cgroup v2 cpu.max "quota period"): the box shares the host by time, not by mask
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    # one CPU per physical core first, then the SMT siblings; and the cores that have both siblings allowed,
+    # as sibling pairs (for the SMT gain)
     order = [cs[0] for cs in cores.values()] + [c for cs in cores.values() for c in cs[1:]]
-    return info, order
+    pairs = [c for cs in cores.values() if len(cs) >= 2 for c in cs[:2]]
+    return info, order, pairs
 
 
 def cpu_baseline_all_cores(frames: np.ndarray, budget_s: float, threads: int = 16, pin=None):
@@ -363,7 +371,7 @@ def cpu_scaling(frames: np.ndarray, budget_s: float, max_threads: int):
     physical core, then onto SMT siblings), and the all-core figure it grounds: the per-core rate at the
     widest one-thread-per-core point x the host's physical cores x the measured SMT gain (1.0 when the
     share holds no sibling pairs).  Still an extrapolation past the share, labelled as one."""
-    info, order = cpu_topology()
+    info, order, pairs = cpu_topology()
     ncore = info["allowed_physical_cores"]
     pts = sorted({t for t in (1, 2, 4, 8, 16, ncore, len(order), max_threads) if 1 <= t <= min(max_threads, len(order))})
     curve = []
@@ -374,9 +382,16 @@ def cpu_scaling(frames: np.ndarray, budget_s: float, max_threads: int):
     by_t = {c["threads"]: c["frames_per_s"] for c in curve}
     p_core = max(t for t in by_t if t <= ncore)
     per_core = by_t[p_core] / p_core
+    # SMT gain inside the job's quota: max_threads threads on max_threads / 2 cores' sibling pairs against
+    # max_threads / 2 threads on those cores alone
     smt = None
-    if 2 * p_core in by_t and 2 * p_core <= len(order) and p_core == ncore:
-        smt = by_t[2 * p_core] / by_t[p_core]
+    h = max_threads // 2
+    if h >= 1 and len(pairs) >= 2 * h:
+        r_pair = cpu_baseline_all_cores(frames, budget_s, 2 * h, pin=pairs[:2 * h])["value"]
+        r_one = by_t[h] if h in by_t else cpu_baseline_all_cores(frames, budget_s, h, pin=pairs[0:2 * h:2])["value"]
+        smt = r_pair / r_one
+        curve.append({"threads": 2 * h, "frames_per_s": round(r_pair, 2), "physical_cores_used": h,
+                      "smt_siblings": True})
     eff = by_t[p_core] / (p_core * by_t[1])
     host_cores = info["host_physical_cores"]
     grounded = per_core * host_cores * (smt if smt else 1.0)
@@ -387,8 +402,9 @@ def cpu_scaling(frames: np.ndarray, budget_s: float, max_threads: int):
                 "sample": "per-core rate at %d pinned threads (%.2f frames/s/core, parallel efficiency %.2f vs 1 thread) "
                           "x %d physical cores x SMT gain %s: NOT MEASURED on the whole host (the box gives one "
                           "GPU's job a %d-CPU share)" % (p_core, per_core, eff, host_cores,
-                                                         ("%.2f (measured)" % smt) if smt else "1.0 (no sibling "
-                                                         "pairs in the share)", info["allowed_cpus"])}}
+                                                         ("%.2f (measured on %d sibling pairs)" % (smt, h)) if smt else
+                                                         "1.0 (no sibling pairs allowed)",
+                                                         info.get("cgroup_cpu_quota") or info["allowed_cpus"])}}
 
 
 def main():
@@ -846,7 +862,7 @@ def main():
             # (os.cpu_count() shows the whole host): the thread-scaling curve is measured on the share, pinned
             # one thread per physical core before SMT siblings, and the whole-host figure is grounded on it
             sc = cpu_scaling(seq, args.cpu_seconds / 3, args.cpu_threads)
-            top = sc["curve"][-1]
+            top = max((c for c in sc["curve"] if not c.get("smt_siblings")), key=lambda c: c["threads"])
             out["cpu_baseline_all_cores"] = {
                 "value": top["frames_per_s"], "unit": "frames/s", "cores": top["threads"], "kind": "port",
                 "sample": "oracle/orbref (%s), %d pinned threads each on its own block of the config-2 sequence, "
