@@ -69,6 +69,22 @@ orbx_status orbx_get_tables(const orbx_handle* h, int* nlevels, float* scale_fac
                             float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
                             int* features_per_level);
 
+/* OpenCV build the extractor reproduces.  The reference links whatever OpenCV 2.4 / 3.x
+ * its user has (CMakeLists.txt:31-37), and the builds differ in the last bit of two primitives it calls:
+ *   resize  cv::resize INTER_LINEAR's vertical pass in ComputePyramid (src/ORBextractor.cc:1361):
+ *           ORBX_RESIZE_SCALAR  the generic FixedPtCast (h0 b0 + h1 b1 + 2^21) >> 22 (cv::setUseOptimized(false));
+ *           ORBX_RESIZE_SSE2    x86 VResizeLinearVec_32s8u on all but a 0..4-px row tail (a stock x86 build).
+ *   blur    GaussianBlur(7x7, 2) before computeDescriptors (src/ORBextractor.cc:1300-1306):
+ *           ORBX_BLUR_SCALAR    OpenCV <= 3.4.1 integer column pass, kernel [18 34 49 55 49 34 18] / 2^8;
+ *           ORBX_BLUR_SSE2      OpenCV <= 3.4.1 x86 SymmColumnVec_32s8u: the same sums rounded half to even on
+ *                               every column but the row's width % 4 tail;
+ *           ORBX_BLUR_BITEXACT  OpenCV >= 3.4.6 / 4.x fixed-point GaussianBlur, kernel [18 34 48 56 48 34 18] / 2^8.
+ * The default is SCALAR / SCALAR, the path the CPU oracle pins.  DESIGN.md section 3 tabulates how far each mode
+ * moves the output.  Takes effect from the next extract on the handle. */
+enum { ORBX_RESIZE_SCALAR = 0, ORBX_RESIZE_SSE2 = 1 };
+enum { ORBX_BLUR_SCALAR = 0, ORBX_BLUR_SSE2 = 1, ORBX_BLUR_BITEXACT = 2 };
+orbx_status orbx_set_cv_modes(orbx_handle* h, int resize_mode, int blur_mode);
+
 /* Per-frame keypoint capacity the extractor may need (nfeatures + slack per level).
  * -1 (and ORBX_EINVAL from the extract calls) for a geometry the kernels do not run:
  *   - a level narrower or shorter than one 30-px FAST cell inside its border (the

@@ -83,11 +83,35 @@ void orbref_level_size(const orbref_tables* t, int level, int cols, int rows, in
 }
 
 /* ---- a3: cv::resize INTER_LINEAR, u8, generic fixed-point path ---------- */
-void orbref_resize_linear(const uint8_t* src, int sw, int sh, size_t sstep,
-                          uint8_t* dst, int dw, int dh, size_t dstep)
+/* SURVEY A.2 alternative: how far OpenCV 3.x's x86 build takes VResizeLinearVec_32s8u (SSE2) over a dst row of
+ * `width` bytes before the scalar VResizeLinear loop finishes it: 16 at a time while x <= width - 16, then 4 at a
+ * time while x < width - 4 (imgproc/src/resize.cpp), leaving a 0..4-byte scalar tail. */
+int orbref_resize_simd_end(int width)
+{
+    int x = 0;
+    while (x <= width - 16) x += 16;
+    while (x < width - 4) x += 4;
+    return x;
+}
+
+/* Vertical pass of one dst pixel: mode 0 the generic FixedPtCast<int, uchar, 22>
+ * (h0 b0 + h1 b1 + 2^21) >> 22; mode 1 the SSE2 VResizeLinearVec_32s8u form
+ * ((mulhi16(h0 >> 4, b0) + mulhi16(h1 >> 4, b1) + 2) >> 2) (_mm_srai_epi32 by 4, _mm_packs_epi32, _mm_mulhi_epi16,
+ * _mm_adds_epi16, _mm_srai_epi16 by 2, _mm_packus_epi16). */
+static inline uint8_t resize_vpass(int h0, int h1, int b0, int b1, int simd)
+{
+    if (!simd) return sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);
+    const int x0 = clampi(h0 >> 4, SHRT_MIN, SHRT_MAX), x1 = clampi(h1 >> 4, SHRT_MIN, SHRT_MAX);
+    const int m = clampi(((x0 * (short)b0) >> 16) + ((x1 * (short)b1) >> 16), SHRT_MIN, SHRT_MAX);
+    return sat_u8(clampi(m + 2, SHRT_MIN, SHRT_MAX) >> 2);
+}
+
+void orbref_resize_linear_mode(const uint8_t* src, int sw, int sh, size_t sstep,
+                               uint8_t* dst, int dw, int dh, size_t dstep, int mode)
 {
     const double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
     const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    const int xs = mode == ORBREF_RESIZE_SSE2 ? orbref_resize_simd_end(dw) : 0;
     int* xofs = (int*)malloc(sizeof(int) * (size_t)dw);
     short* alpha = (short*)malloc(sizeof(short) * 2 * (size_t)dw);
     for (int dx = 0; dx < dw; dx++) {
@@ -114,11 +138,17 @@ void orbref_resize_linear(const uint8_t* src, int sw, int sh, size_t sstep,
             const int a0 = alpha[2 * dx], a1 = alpha[2 * dx + 1];
             const int h0 = r0[x0] * a0 + r0[x1] * a1;
             const int h1 = r1[x0] * a0 + r1[x1] * a1;
-            d[dx] = sat_u8((h0 * b0 + h1 * b1 + (1 << 21)) >> 22);
+            d[dx] = resize_vpass(h0, h1, b0, b1, dx < xs);
         }
     }
     free(xofs);
     free(alpha);
+}
+
+void orbref_resize_linear(const uint8_t* src, int sw, int sh, size_t sstep,
+                          uint8_t* dst, int dw, int dh, size_t dstep)
+{
+    orbref_resize_linear_mode(src, sw, sh, sstep, dst, dw, dh, dstep, ORBREF_RESIZE_SCALAR);
 }
 
 /* ---- a5: cv::FAST TYPE_9_16 with NMS (FAST_t<16> + cornerScore<16>) ----- */
@@ -578,10 +608,69 @@ static inline int reflect101(int p, int len)
     return p;
 }
 
-void orbref_gaussian_blur7(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, size_t dstep)
+/* The 7 integer taps of GaussianBlur(7x7, sigma 2) on u8, per OpenCV build:
+ *  ORBREF_BLUR_SCALAR / _SSE2: OpenCV <= 3.4.1 (and 2.4).  createSeparableLinearFilter converts the CV_32F
+ *    getGaussianKernel(7, 2) to CV_32S at x256 (convertTo, cvRound): [18 34 49 55 49 34 18], sum 257.
+ *  ORBREF_BLUR_BITEXACT: OpenCV >= 3.4.6 / 4.1 GaussianBlur 8U fixed point (smooth.cpp
+ *    getGaussianKernelBitExact + getGaussianKernelFixedPoint_ED): the side taps are rounded at 8 fraction
+ *    bits with the rounding error carried inwards, and the centre closes the sum to exactly 256. */
+void orbref_blur_kernel(int mode, int k[7])
 {
-    /* getGaussianKernel(7, 2, CV_32F) scaled by 256 and rounded */
-    static const int k[7] = {18, 34, 49, 55, 49, 34, 18};
+    if (mode != ORBREF_BLUR_BITEXACT) {
+        static const int k0[7] = {18, 34, 49, 55, 49, 34, 18};
+        memcpy(k, k0, sizeof(k0));
+        return;
+    }
+    /* sigmaX = 2; scale2X = -0.125 / sigma^2; values[i] = exp(x*x*scale2X) for x = 1-n, 3-n, .. (step 2) */
+    const int n = 7, n2 = 3;
+    const double scale2X = -0.125 / (2.0 * 2.0);
+    double values[3], sum = 0.0;
+    for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
+        values[i] = exp((double)(x * x) * scale2X);
+        sum += values[i];
+    }
+    sum *= 2.0;
+    sum += 1.0;
+    const double mul1 = 1.0 / sum;
+    double err = 0.0;
+    int side = 0;
+    for (int i = 0; i < n2; i++) {
+        const double adj = values[i] * mul1 * 256.0 + err;
+        const int v0 = (int)lrint(adj);
+        err = adj - (double)v0;
+        k[i] = k[n - 1 - i] = v0;
+        side += v0;
+    }
+    k[n2] = 256 - 2 * side;
+}
+
+/* The column pass of one pixel from its 7-tap sum T (in 2^-16 units of the output):
+ *  scalar: FixedPtCastEx<int, uchar>(16): (T + 2^15) >> 16, saturated.
+ *  SSE2 (SymmColumnVec_32s8u, OpenCV <= 3.4.1 x86, every column but the row's width % 4 tail): the taps as
+ *    float k/2^16, s = S0*k0 + 0; s += (S+j + S-j)*kj, j = 1..3 (mul then add, no FMA), _mm_cvtps_epi32
+ *    (round half to even), _mm_packs_epi32, _mm_packus_epi16. */
+static inline uint8_t blur_col(const int* S /* rows y-3 .. y+3 */, const int* k, int simd)
+{
+    if (!simd) {
+        int acc = 0;
+        for (int j = 0; j < 7; j++) acc += k[j] * S[j];
+        return sat_u8((acc + (1 << 15)) >> 16);
+    }
+    const float f0 = (float)k[3] * (1.0f / 65536.0f), f1 = (float)k[4] * (1.0f / 65536.0f),
+                f2 = (float)k[5] * (1.0f / 65536.0f), f3 = (float)k[6] * (1.0f / 65536.0f);
+    float s = (float)S[3] * f0 + 0.0f;
+    s = s + (float)(S[4] + S[2]) * f1;
+    s = s + (float)(S[5] + S[1]) * f2;
+    s = s + (float)(S[6] + S[0]) * f3;
+    const long v = lrintf(s);
+    return sat_u8(v > SHRT_MAX ? SHRT_MAX : (v < SHRT_MIN ? SHRT_MIN : (int)v));
+}
+
+void orbref_gaussian_blur7_mode(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, size_t dstep, int mode)
+{
+    int k[7];
+    orbref_blur_kernel(mode, k);
+    const int xs = mode == ORBREF_BLUR_SSE2 ? (w & ~3) : 0;   /* SymmColumnVec_32s8u: i <= width - 4, by 16 then 4 */
     int* rows = (int*)malloc(sizeof(int) * (size_t)w * (size_t)h);
     for (int y = 0; y < h; y++) {
         const uint8_t* s = src + (size_t)y * sstep;
@@ -594,20 +683,31 @@ void orbref_gaussian_blur7(const uint8_t* src, int w, int h, size_t sstep, uint8
     for (int y = 0; y < h; y++) {
         uint8_t* d = dst + (size_t)y * dstep;
         for (int x = 0; x < w; x++) {
-            int acc = 0;
-            for (int j = 0; j < 7; j++) acc += k[j] * rows[(size_t)reflect101(y + j - 3, h) * w + x];
-            d[x] = sat_u8((acc + (1 << 15)) >> 16);
+            int S[7];
+            for (int j = 0; j < 7; j++) S[j] = rows[(size_t)reflect101(y + j - 3, h) * w + x];
+            d[x] = blur_col(S, k, x < xs);
         }
     }
     free(rows);
 }
 
+void orbref_gaussian_blur7(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, size_t dstep)
+{
+    orbref_gaussian_blur7_mode(src, w, h, sstep, dst, dstep, ORBREF_BLUR_SCALAR);
+}
+
 /* ---- a9: computeOrbDescriptor, src/ORBextractor.cc:141-192 --------------- */
-void orbref_brief(const uint8_t* blur, size_t step, float kx, float ky, float angle_deg, uint8_t desc[32])
+/* cos/sin of the BRIEF angle.  ORBREF_TRIG_GLIBC is the host libm's cosf / sinf (glibc 2.35, the
+ * reference's own, < 1 ulp but not correctly rounded); ORBREF_TRIG_CR rounds the x87 80-bit cosl / sinl of the
+ * same float once to float (correct rounding except where the long double result sits within 2^-64 relative of
+ * a float midpoint; tests/test_cv_modes.py checks it against the double evaluation on every angle it meets). */
+void orbref_brief_mode(const uint8_t* blur, size_t step, float kx, float ky, float angle_deg, uint8_t desc[32],
+                       int trig_mode)
 {
     const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
     const float angle = angle_deg * factorPI;
-    const float a = cosf(angle), b = sinf(angle);
+    const float a = trig_mode == ORBREF_TRIG_CR ? (float)cosl((long double)angle) : cosf(angle);
+    const float b = trig_mode == ORBREF_TRIG_CR ? (float)sinl((long double)angle) : sinf(angle);
     const uint8_t* center = blur + (ptrdiff_t)cv_round_f(ky) * (ptrdiff_t)step + cv_round_f(kx);
     const int s = (int)step;
     for (int i = 0; i < 32; ++i) {
@@ -627,11 +727,18 @@ void orbref_brief(const uint8_t* blur, size_t step, float kx, float ky, float an
     }
 }
 
-/* ---- a2: ORBextractor::operator(), src/ORBextractor.cc:1248-1334 --------- */
-int orbref_extract(const orbref_params* p, const uint8_t* img, int rows, int cols, size_t step,
-                   orbref_keypoint* kps, int cap, uint8_t* desc, int* n_out,
-                   uint8_t* pyramid, int* level_counts, int* cand_counts)
+void orbref_brief(const uint8_t* blur, size_t step, float kx, float ky, float angle_deg, uint8_t desc[32])
 {
+    orbref_brief_mode(blur, step, kx, ky, angle_deg, desc, ORBREF_TRIG_GLIBC);
+}
+
+/* ---- a2: ORBextractor::operator(), src/ORBextractor.cc:1248-1334 --------- */
+int orbref_extract_mode(const orbref_params* p, const orbref_cv_modes* m, const uint8_t* img, int rows, int cols,
+                        size_t step, orbref_keypoint* kps, int cap, uint8_t* desc, int* n_out,
+                        uint8_t* pyramid, int* level_counts, int* cand_counts)
+{
+    static const orbref_cv_modes canonical = {ORBREF_RESIZE_SCALAR, ORBREF_BLUR_SCALAR, ORBREF_TRIG_GLIBC};
+    if (!m) m = &canonical;
     if (!p || !n_out) return -22;
     if (!img || rows <= 0 || cols <= 0) return 1; /* :1252 empty image: no-op */
     orbref_tables t;
@@ -648,7 +755,8 @@ int orbref_extract(const orbref_params* p, const uint8_t* img, int rows, int col
         if (l == 0) {
             for (int y = 0; y < rows; y++) memcpy(lev[0] + (size_t)y * cols, img + (size_t)y * step, (size_t)cols);
         } else {
-            orbref_resize_linear(lev[l - 1], lw[l - 1], lh[l - 1], (size_t)lw[l - 1], lev[l], lw[l], lh[l], (size_t)lw[l]);
+            orbref_resize_linear_mode(lev[l - 1], lw[l - 1], lh[l - 1], (size_t)lw[l - 1], lev[l], lw[l], lh[l],
+                                      (size_t)lw[l], m->resize);
         }
     }
 
@@ -694,11 +802,12 @@ int orbref_extract(const orbref_params* p, const uint8_t* img, int rows, int col
             if (nl == 0) continue;
             const float size = (float)(int)(PATCH_SIZE * t.scale[l]);   /* :1013 */
             uint8_t* blur = (uint8_t*)malloc((size_t)lw[l] * lh[l]);
-            orbref_gaussian_blur7(lev[l], lw[l], lh[l], (size_t)lw[l], blur, (size_t)lw[l]);   /* :1300-1306 */
+            orbref_gaussian_blur7_mode(lev[l], lw[l], lh[l], (size_t)lw[l], blur, (size_t)lw[l], m->blur);   /* :1300-1306 */
             for (int i = 0; i < nl; i++) {
                 orbref_keypoint* k = &kps[off + i];
                 const float ang = orbref_ic_angle(lev[l], (size_t)lw[l], lvl_kx[l][i], lvl_ky[l][i], t.umax);  /* :1030-1033 */
-                orbref_brief(blur, (size_t)lw[l], (float)lvl_kx[l][i], (float)lvl_ky[l][i], ang, desc + 32 * (size_t)(off + i));
+                orbref_brief_mode(blur, (size_t)lw[l], (float)lvl_kx[l][i], (float)lvl_ky[l][i], ang,
+                                  desc + 32 * (size_t)(off + i), m->trig);
                 float x = (float)lvl_kx[l][i], y = (float)lvl_ky[l][i];
                 if (l != 0) { x *= t.scale[l]; y *= t.scale[l]; }   /* :1322-1329 */
                 k->x = x; k->y = y; k->size = size; k->angle = ang;
@@ -716,6 +825,14 @@ int orbref_extract(const orbref_params* p, const uint8_t* img, int rows, int col
     }
     for (int l = 0; l < L; l++) { free(lev[l]); free(lvl_kx[l]); free(lvl_ky[l]); free(lvl_sc[l]); }
     return status;
+}
+
+int orbref_extract(const orbref_params* p, const uint8_t* img, int rows, int cols, size_t step,
+                   orbref_keypoint* kps, int cap, uint8_t* desc, int* n_out,
+                   uint8_t* pyramid, int* level_counts, int* cand_counts)
+{
+    return orbref_extract_mode(p, NULL, img, rows, cols, step, kps, cap, desc, n_out, pyramid, level_counts,
+                               cand_counts);
 }
 
 /* ---- a11: DescriptorDistance, src/ORBmatcher.cc:1728-1744 ---------------- */

@@ -76,6 +76,28 @@ void orbref_level_size(const orbref_tables* t, int level, int cols, int rows, in
 void orbref_resize_linear(const uint8_t* src, int sw, int sh, size_t sstep,
                           uint8_t* dst, int dw, int dh, size_t dstep);
 
+/* SURVEY Appendix A's alternative OpenCV builds.  The reference links whatever OpenCV 2.4 / 3.x the user has
+ * (CMakeLists.txt:31-37); the canonical modes (all 0) are OpenCV 3.x's generic scalar paths, what
+ * cv::setUseOptimized(false) runs.  The others are restated from OpenCV's published source, not run here
+ * (OpenCV is absent): PARITY UNPINNED like the canonical ones.
+ *   resize  0 scalar VResizeLinear;  1 SSE2 VResizeLinearVec_32s8u on all but a 0..4-px row tail (A.2)
+ *   blur    0 <= 3.4.1 scalar column pass;  1 <= 3.4.1 SSE2 float column pass SymmColumnVec_32s8u (A.3);
+ *           2 >= 3.4.6 / 4.1 bit-exact fixed point, error-diffused kernel [18 34 48 56 48 34 18] (A.3)
+ *   trig    0 glibc cosf / sinf;  1 correctly rounded (A.5) */
+enum { ORBREF_RESIZE_SCALAR = 0, ORBREF_RESIZE_SSE2 = 1 };
+enum { ORBREF_BLUR_SCALAR = 0, ORBREF_BLUR_SSE2 = 1, ORBREF_BLUR_BITEXACT = 2 };
+enum { ORBREF_TRIG_GLIBC = 0, ORBREF_TRIG_CR = 1 };
+typedef struct {
+    int resize, blur, trig;
+} orbref_cv_modes;
+int orbref_resize_simd_end(int width);
+void orbref_resize_linear_mode(const uint8_t* src, int sw, int sh, size_t sstep,
+                               uint8_t* dst, int dw, int dh, size_t dstep, int mode);
+void orbref_blur_kernel(int mode, int k[7]);
+void orbref_gaussian_blur7_mode(const uint8_t* src, int w, int h, size_t sstep, uint8_t* dst, size_t dstep, int mode);
+void orbref_brief_mode(const uint8_t* blur, size_t step, float kx, float ky, float angle_deg, uint8_t desc[32],
+                       int trig_mode);
+
 /* OpenCV FAST_t<16> with non-max suppression on a ROI.
  * Writes (x, y, score) triples in OpenCV emission order; returns the count,
  * or -1 if more than cap keypoints. */
@@ -117,6 +139,10 @@ void orbref_brief(const uint8_t* blur, size_t step, float kx, float ky, float an
 int orbref_extract(const orbref_params* p, const uint8_t* img, int rows, int cols, size_t step,
                    orbref_keypoint* kps, int cap, uint8_t* desc, int* n_out,
                    uint8_t* pyramid, int* level_counts, int* cand_counts);
+/* The same under the OpenCV build modes m (NULL = canonical). */
+int orbref_extract_mode(const orbref_params* p, const orbref_cv_modes* m, const uint8_t* img, int rows, int cols,
+                        size_t step, orbref_keypoint* kps, int cap, uint8_t* desc, int* n_out,
+                        uint8_t* pyramid, int* level_counts, int* cand_counts);
 
 /* a11: ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:1728-1744). */
 int orbref_descriptor_distance(const uint8_t* a, const uint8_t* b);

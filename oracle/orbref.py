@@ -36,6 +36,16 @@ class Tables(C.Structure):
                 ("nfeat_level", C.c_int * MAX_LEVELS), ("umax", C.c_int * 16)]
 
 
+class CvModes(C.Structure):
+    """SURVEY Appendix A's OpenCV build modes (orbref.h orbref_cv_modes)."""
+    _fields_ = [("resize", C.c_int), ("blur", C.c_int), ("trig", C.c_int)]
+
+
+RESIZE_SCALAR, RESIZE_SSE2 = 0, 1
+BLUR_SCALAR, BLUR_SSE2, BLUR_BITEXACT = 0, 1, 2
+TRIG_GLIBC, TRIG_CR = 0, 1
+
+
 class ProjPoint(C.Structure):
     _fields_ = [("proj_x", C.c_float), ("proj_y", C.c_float), ("proj_xr", C.c_float), ("view_cos", C.c_float),
                 ("level", C.c_int32), ("flags", C.c_int32)]
@@ -99,6 +109,15 @@ def lib():
         L.orbref_brief.argtypes = [u8p, C.c_size_t, C.c_float, C.c_float, C.c_float, u8p]
         L.orbref_extract.argtypes = [P(Params), u8p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_int,
                                      u8p, i32p, u8p, i32p, i32p]
+        L.orbref_extract_mode.argtypes = [P(Params), P(CvModes), u8p, C.c_int, C.c_int, C.c_size_t, C.c_void_p,
+                                          C.c_int, u8p, i32p, u8p, i32p, i32p]
+        L.orbref_resize_simd_end.argtypes = [C.c_int]
+        L.orbref_resize_linear_mode.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_int, C.c_int, C.c_size_t,
+                                                C.c_int]
+        L.orbref_blur_kernel.argtypes = [C.c_int, i32p]
+        L.orbref_blur_kernel.restype = None
+        L.orbref_gaussian_blur7_mode.argtypes = [u8p, C.c_int, C.c_int, C.c_size_t, u8p, C.c_size_t, C.c_int]
+        L.orbref_brief_mode.argtypes = [u8p, C.c_size_t, C.c_float, C.c_float, C.c_float, u8p, C.c_int]
         L.orbref_descriptor_distance.argtypes = [u8p, u8p]
         L.orbref_search_for_initialization.argtypes = [C.c_void_p, u8p, C.c_int, C.c_void_p, u8p, C.c_int,
                                                        C.c_float, C.c_float, C.c_float, C.c_float, f32p, i32p,
@@ -172,11 +191,21 @@ def level_sizes(p: Params, cols: int, rows: int):
     return out
 
 
-def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+def resize_linear(src: np.ndarray, dw: int, dh: int, mode: int = RESIZE_SCALAR) -> np.ndarray:
     src = np.ascontiguousarray(src, dtype=np.uint8)
     dst = np.empty((dh, dw), np.uint8)
-    lib().orbref_resize_linear(_u8(src), src.shape[1], src.shape[0], src.strides[0], _u8(dst), dw, dh, dw)
+    lib().orbref_resize_linear_mode(_u8(src), src.shape[1], src.shape[0], src.strides[0], _u8(dst), dw, dh, dw, mode)
     return dst
+
+
+def resize_simd_end(width: int) -> int:
+    return lib().orbref_resize_simd_end(width)
+
+
+def blur_kernel(mode: int = BLUR_SCALAR) -> np.ndarray:
+    k = np.zeros(7, np.int32)
+    lib().orbref_blur_kernel(mode, _i32(k))
+    return k
 
 
 def fast(roi: np.ndarray, threshold: int) -> np.ndarray:
@@ -244,17 +273,18 @@ def ic_angle(img: np.ndarray, cx: int, cy: int, umax) -> float:
     return lib().orbref_ic_angle(_u8(img), img.strides[0], cx, cy, _i32(um))
 
 
-def gaussian_blur7(img: np.ndarray) -> np.ndarray:
+def gaussian_blur7(img: np.ndarray, mode: int = BLUR_SCALAR) -> np.ndarray:
     img = np.ascontiguousarray(img, dtype=np.uint8)
     dst = np.empty_like(img)
-    lib().orbref_gaussian_blur7(_u8(img), img.shape[1], img.shape[0], img.strides[0], _u8(dst), dst.strides[0])
+    lib().orbref_gaussian_blur7_mode(_u8(img), img.shape[1], img.shape[0], img.strides[0], _u8(dst), dst.strides[0],
+                                     mode)
     return dst
 
 
-def brief(blur: np.ndarray, x: float, y: float, angle: float) -> np.ndarray:
+def brief(blur: np.ndarray, x: float, y: float, angle: float, trig: int = TRIG_GLIBC) -> np.ndarray:
     blur = np.ascontiguousarray(blur, dtype=np.uint8)
     d = np.zeros(32, np.uint8)
-    lib().orbref_brief(_u8(blur), blur.strides[0], x, y, angle, _u8(d))
+    lib().orbref_brief_mode(_u8(blur), blur.strides[0], x, y, angle, _u8(d), trig)
     return d
 
 
@@ -267,7 +297,8 @@ class ExtractResult:
         self.cand_counts = cand_counts
 
 
-def extract(img: np.ndarray, p: Params, want_pyramid: bool = True) -> ExtractResult:
+def extract(img: np.ndarray, p: Params, want_pyramid: bool = True, modes=None) -> ExtractResult:
+    """ORBextractor::operator() restated; modes = (resize, blur, trig) OpenCV build modes (None: canonical)."""
     img = np.ascontiguousarray(img, dtype=np.uint8)
     rows, cols = img.shape
     sizes = level_sizes(p, cols, rows)
@@ -278,8 +309,9 @@ def extract(img: np.ndarray, p: Params, want_pyramid: bool = True) -> ExtractRes
     pyr = np.zeros(sum(w * h for w, h in sizes), np.uint8) if want_pyramid else None
     lc = np.zeros(MAX_LEVELS, np.int32)
     cc = np.zeros(MAX_LEVELS, np.int32)
-    rc = lib().orbref_extract(C.byref(p), _u8(img), rows, cols, img.strides[0], kps.ctypes.data, cap,
-                              _u8(desc), C.byref(n), _u8(pyr) if pyr is not None else None, _i32(lc), _i32(cc))
+    m = None if modes is None else C.byref(CvModes(*modes))
+    rc = lib().orbref_extract_mode(C.byref(p), m, _u8(img), rows, cols, img.strides[0], kps.ctypes.data, cap,
+                                   _u8(desc), C.byref(n), _u8(pyr) if pyr is not None else None, _i32(lc), _i32(cc))
     if rc != 0:
         raise RuntimeError("orbref_extract failed: %d" % rc)
     levels = None

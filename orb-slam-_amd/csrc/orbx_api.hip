@@ -111,6 +111,8 @@ struct orbx_handle {
     hipStream_t stream = nullptr;
     orbx_params params{};
     Tables tab;
+    int resize_mode = ORBX_RESIZE_SCALAR;   // orbx_set_cv_modes
+    int blur_mode = ORBX_BLUR_SCALAR;
 
     // geometry (per rows x cols): the current size's host copy and device tables
     bool geom_ok = false;
@@ -300,6 +302,7 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
             L.xtab_off = (int)xt.size();
             L.ytab_off = (int)yt.size();
             resize_tables(prev_w, prev_h, L.w, L.h, xt, yt);
+            L.rz_simd_end = rz_simd_end(L.w);
             L.pyr_win = 1;
             for (int g0 = 0; g0 < L.w; g0 += 4) {   // k_pyramid_level's byte window per 4-column group
                 const int first = xt[L.xtab_off + g0].x & 0xFFFF;
@@ -473,6 +476,8 @@ ExtractBufs bufs(orbx_handle* h)
     b.qt_out = h->d_qt_out;
     b.qt_cnt = h->d_qt_cnt;
     b.status = h->d_status;
+    b.resize_mode = h->resize_mode;
+    b.blur_mode = h->blur_mode;
     return b;
 }
 
@@ -624,6 +629,17 @@ void orbx_destroy(orbx_handle* h)
     delete h;
 }
 
+orbx_status orbx_set_cv_modes(orbx_handle* h, int resize_mode, int blur_mode)
+{
+    if (!h || (resize_mode != ORBX_RESIZE_SCALAR && resize_mode != ORBX_RESIZE_SSE2) ||
+        (blur_mode != ORBX_BLUR_SCALAR && blur_mode != ORBX_BLUR_SSE2 && blur_mode != ORBX_BLUR_BITEXACT))
+        return ORBX_EINVAL;
+    h->resize_mode = resize_mode;
+    h->blur_mode = blur_mode;
+    std::fill(h->level_cached.begin(), h->level_cached.end(), false);
+    return ORBX_OK;
+}
+
 orbx_status orbx_get_tables(const orbx_handle* h, int* nlevels, float* scale_factor, float* scale, float* inv_scale,
                             float* sigma2, float* inv_sigma2, int* features_per_level)
 {
@@ -764,7 +780,8 @@ orbx_status orbx_extract(orbx_handle* h, const uint8_t* img, int rows, int cols,
     const std::vector<const void*> key = {(const void*)h->h_pin, h->d_img, h->d_out, h->d_pyr, h->d_slots, h->d_cell_counts, h->d_spill,
                                           h->d_spill_node, h->d_qt_nodes, h->d_qt_out, h->d_qt_cnt, h->d_status, h->d_geom,
                                           h->d_cells, h->d_xtab, h->d_ytab, h->d_pyrbt, (const void*)(uintptr_t)rows,
-                                          (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap};
+                                          (const void*)(uintptr_t)cols, (const void*)(uintptr_t)ocap,
+                                          (const void*)(uintptr_t)h->resize_mode, (const void*)(uintptr_t)h->blur_mode};
     bool launched = false;
     if (!ev && !h->graph_failed && !getenv("ORBX_NO_GRAPH")) {
         if (h->host_graph && h->graph_key != key) {

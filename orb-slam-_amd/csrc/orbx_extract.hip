@@ -78,9 +78,20 @@ __device__ __forceinline__ ushort2_t as_us2(uint32_t v)
 constexpr int kPyrRows = ORBX_PYR_ROWS;
 constexpr int kPyrNT = ORBX_PYR_NT;   // threads per pyramid workgroup
 
+// SURVEY.md A.2's SSE2 vertical pass (ORBX_RESIZE_SSE2): VResizeLinearVec_32s8u's
+// ((mulhi16(h0 >> 4, b0) + mulhi16(h1 >> 4, b1) + 2) >> 2) of the horizontal sums h0, h1 (h >> 4 <= 32640 and
+// b <= 2048 are non-negative: mulhi16 is the plain (x * b) >> 16, every product a 24 x 24-bit multiply)
+__device__ __forceinline__ uint32_t rz_sse2(uint32_t h0, uint32_t h1, uint32_t b0, uint32_t b1)
+{
+    const uint32_t v = ((__umul24(h0 >> 4, b0) >> 16) + (__umul24(h1 >> 4, b1) >> 16) + 2u) >> 2;
+    return min(v, 255u);
+}
+
 // kA: every staged source row starts 4-byte aligned in LDS (source pitch and base multiples of 4, always
-// so for levels >= 1), so a lane's realignment shift is the same on every row
-template <bool kWin, bool kA>
+// so for levels >= 1), so a lane's realignment shift is the same on every row.  kRM: ORBX_RESIZE_* (columns
+// [0, rz_simd_end) of an ORBX_RESIZE_SSE2 level take rz_sse2; rz_simd_end is a multiple of 4, so a 4-column
+// group takes one form)
+template <bool kWin, bool kA, int kRM>
 __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __restrict__ G, FramePtrs P, int l,
                                                        const int2* __restrict__ xtab,
                                                        const int2* __restrict__ ytab, int lp)
@@ -211,8 +222,15 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
                     asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(t) : "v"(h0[k]), "s"(b0), "v"(1u << 23));
                     asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(acc[k]) : "v"(h1[k]), "s"(b1), "v"(t));
                 }
-                const uint32_t packed = __builtin_amdgcn_perm(acc[1], acc[0], 0x0C0C0703u) |
-                                        __builtin_amdgcn_perm(acc[3], acc[2], 0x07030C0Cu);
+                uint32_t packed = __builtin_amdgcn_perm(acc[1], acc[0], 0x0C0C0703u) |
+                                  __builtin_amdgcn_perm(acc[3], acc[2], 0x07030C0Cu);
+                if constexpr (kRM == 1) {
+                    if (dx0 < D.rz_simd_end) {
+                        packed = 0u;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) packed |= rz_sse2(h0[k], h1[k], b0 >> 2, b1 >> 2) << (8 * k);
+                    }
+                }
                 *reinterpret_cast<uint32_t*>(drow0 + (size_t)rr * D.pitch + dx0) = packed;
                 cr = hi;
 #pragma unroll
@@ -230,7 +248,8 @@ __global__ __launch_bounds__(kPyrNT) void k_pyramid_level(const Geometry* __rest
             for (int k = 0; k < 4; ++k) {
                 const uint32_t h0 = __umul24(r0[x0[k]], a0[k]) + __umul24(r0[x1[k]], a1[k]);
                 const uint32_t h1 = __umul24(r1[x0[k]], a0[k]) + __umul24(r1[x1[k]], a1[k]);
-                const uint32_t v = (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
+                const uint32_t v = (kRM == 1 && dx0 < D.rz_simd_end) ? rz_sse2(h0, h1, b0, b1)
+                                                                    : (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
                 packed |= min(v, 255u) << (8 * k);
             }
             // columns past the level width land in the row's pitch padding (pitch = align64(w))
@@ -255,11 +274,12 @@ constexpr int kPyrChunk = 8;   // output rows per work item (unrolled; their row
 __device__ __forceinline__ void pyr_rows(const LevelGeom& Dg, const int2* __restrict__ xtab,
                                          const int2* __restrict__ ytab, const uint8_t* S, int slp, int sfirst,
                                          uint32_t ssh0, uint32_t ssp, uint8_t* dst, int dlp, int4 e, bool last,
-                                         uint8_t* gimg, int nt, int split, int wave, int lane)
+                                         uint8_t* gimg, int nt, int split, int wave, int lane, int rm)
 {
     // the level's fields in registers: the stores below could alias the geometry as far as the compiler
     // knows, which would reload them after every store
     const int w = Dg.w, pitch = Dg.pitch, xoff = Dg.xtab_off, yoff = Dg.ytab_off, win = Dg.pyr_win;
+    const int xs = rm == 1 ? Dg.rz_simd_end : 0;   // ORBX_RESIZE_SSE2 columns (a multiple of 4)
     auto rowb = [&](int r) -> uint32_t {
         const int k = r - sfirst;
         return (uint32_t)(k * slp) + ((ssh0 + (uint32_t)k * ssp) & 15u);
@@ -349,8 +369,14 @@ __device__ __forceinline__ void pyr_rows(const LevelGeom& Dg, const int2* __rest
                 uint32_t acc[4];
 #pragma unroll
                 for (int t = 0; t < 4; ++t) acc[t] = __umul24(h1[t], b1) + (__umul24(h0[t], b0) + (1u << 23));
-                put(r0 + k, __builtin_amdgcn_perm(acc[1], acc[0], 0x0C0C0703u) |
-                                __builtin_amdgcn_perm(acc[3], acc[2], 0x07030C0Cu));
+                uint32_t packed = __builtin_amdgcn_perm(acc[1], acc[0], 0x0C0C0703u) |
+                                  __builtin_amdgcn_perm(acc[3], acc[2], 0x07030C0Cu);
+                if (dx0 < xs) {
+                    packed = 0u;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) packed |= rz_sse2(h0[t], h1[t], b0 >> 2, b1 >> 2) << (8 * t);
+                }
+                put(r0 + k, packed);
                 cr = hi;
 #pragma unroll
                 for (int t = 0; t < 4; ++t) hc[t] = h1[t];
@@ -367,7 +393,7 @@ __device__ __forceinline__ void pyr_rows(const LevelGeom& Dg, const int2* __rest
                 for (int t = 0; t < 4; ++t) {
                     const uint32_t h0 = __umul24(p0[x0[t]], a0[t]) + __umul24(p0[x1[t]], a1[t]);
                     const uint32_t h1 = __umul24(p1[x0[t]], a0[t]) + __umul24(p1[x1[t]], a1[t]);
-                    const uint32_t v = (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
+                    const uint32_t v = dx0 < xs ? rz_sse2(h0, h1, b0, b1) : (__umul24(h0, b0) + __umul24(h1, b1) + (1u << 21)) >> 22;
                     packed |= min(v, 255u) << (8 * t);
                 }
                 put(r0 + k, packed);
@@ -387,7 +413,7 @@ __device__ __forceinline__ void pyr_rows(const LevelGeom& Dg, const int2* __rest
 // (about one per level at each band edge) instead of synchronising.
 __global__ __launch_bounds__(kPyrMaxNT) void k_pyramid_fused(const Geometry* __restrict__ G, FramePtrs P, int gi,
                                                     const int2* __restrict__ xtab, const int2* __restrict__ ytab,
-                                                    const int4* __restrict__ bands)
+                                                    const int4* __restrict__ bands, int rm)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
     const PyrGroup& PG = G->pg[gi];
@@ -433,7 +459,7 @@ __global__ __launch_bounds__(kPyrMaxNT) void k_pyramid_fused(const Geometry* __r
         uint8_t* dst = (i & 1) ? Y : X;
         const int dlp = ((D.w + 15) >> 4) << 4;
         uint8_t* gimg = P.pyr + (size_t)f * P.pyr_fstride + D.pyr_off;
-        pyr_rows(D, xtab, ytab, S, slp, sfirst, ssh0, ssp, dst, dlp, e, last, gimg, nt, PG.split, wave, lane);
+        pyr_rows(D, xtab, ytab, S, slp, sfirst, ssh0, ssp, dst, dlp, e, last, gimg, nt, PG.split, wave, lane, rm);
         if (last) break;
         __syncthreads();   // level s+i is whole in LDS; the buffer it was made from is free
         S = dst;
@@ -529,7 +555,7 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
             if (smem > 64 * 1024)
                 hipFuncSetAttribute((const void*)k_pyramid_fused, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
             hipLaunchKernelGGL(k_pyramid_fused, dim3(1, P.nbands, batch), dim3(P.nt), smem, s, b.geom, p, i, b.xtab,
-                               b.ytab, b.pyr_bands);
+                               b.ytab, b.pyr_bands, b.resize_mode);
         }
         return;
     }
@@ -546,12 +572,20 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         const int q = (g.lv[l].w + 3) >> 2;
         const int nt = std::min(kPyrNT, (q + 63) & ~63);
         const bool al = l >= 2 || (((uintptr_t)p.in | (uintptr_t)p.in_pitch | (uintptr_t)p.in_fstride) & 3) == 0;
-        if (g.lv[l].pyr_win && al)
-            hipLaunchKernelGGL((k_pyramid_level<true, true>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
-        else if (g.lv[l].pyr_win)
-            hipLaunchKernelGGL((k_pyramid_level<true, false>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
-        else
-            hipLaunchKernelGGL((k_pyramid_level<false, false>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
+        auto go = [&](auto rm_tag) {
+            constexpr int RM = decltype(rm_tag)::value;
+            if (g.lv[l].pyr_win && al)
+                hipLaunchKernelGGL((k_pyramid_level<true, true, RM>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab,
+                                   lp);
+            else if (g.lv[l].pyr_win)
+                hipLaunchKernelGGL((k_pyramid_level<true, false, RM>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab,
+                                   b.ytab, lp);
+            else
+                hipLaunchKernelGGL((k_pyramid_level<false, false, RM>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab,
+                                   b.ytab, lp);
+        };
+        if (b.resize_mode == ORBX_RESIZE_SSE2) go(std::integral_constant<int, 1>{});
+        else go(std::integral_constant<int, 0>{});
     }
 }
 
@@ -2299,14 +2333,21 @@ constexpr int kDescWaves = ORBX_DESC_WAVES;
 // load read neighbouring raw dwords (distinct LDS banks).
 __constant__ uint16_t c_blur_items[192] = {2,3,4,5,6,257,258,259,260,261,262,263,513,514,515,516,517,518,519,768,769,770,771,772,773,774,775,776,1024,1025,1026,1027,1028,1029,1030,1031,1032,1280,1281,1282,1283,1284,1285,1286,1287,1288,1536,1537,1538,1539,1540,1541,1542,1543,1544,1545,1792,1793,1794,1795,1796,1797,1798,1799,1800,1801,2048,2049,2050,2051,2052,2053,2054,2055,2056,2057,2304,2305,2306,2307,2308,2309,2310,2311,2312,2313,2560,2561,2562,2563,2564,2565,2566,2567,2568,2569,2816,2817,2818,2819,2820,2821,2822,2823,2824,2825,3072,3073,3074,3075,3076,3077,3078,3079,3080,3081,3328,3329,3330,3331,3332,3333,3334,3335,3336,3337,3584,3585,3586,3587,3588,3589,3590,3591,3592,3593,3840,3841,3842,3843,3844,3845,3846,3847,3848,3849,4096,4097,4098,4099,4100,4101,4102,4103,4104,4352,4353,4354,4355,4356,4357,4358,4359,4360,4609,4610,4611,4612,4613,4614,4615,4616,4865,4866,4867,4868,4869,4870,4871,5122,5123,5124,5125,5126,5127,5379,5380,5381,5382,65535,65535,65535};
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-// GaussianBlur's 7 taps starting at byte `off` of four consecutive raw dwords: the weight bytes of dword d
-__host__ __device__ constexpr uint32_t blur_wshift(int off, int d)
+// GaussianBlur(7x7, sigma 2)'s integer taps per ORBX_BLUR_* mode: OpenCV <= 3.4.1 (scalar and
+// SSE2 column passes) converts getGaussianKernel's floats at x256, [18 34 49 55 49 34 18] (sum 257); 3.4.6+ / 4.x's
+// bit-exact GaussianBlur carries the rounding error inwards and closes the sum at 256, [18 34 48 56 48 34 18]
+__host__ __device__ constexpr uint32_t blur_tap(int bm, int t)
 {
-    constexpr uint32_t k[7] = {18, 34, 49, 55, 49, 34, 18};
+    return t == 2 || t == 4 ? (bm == ORBX_BLUR_BITEXACT ? 48u : 49u)
+                            : t == 3 ? (bm == ORBX_BLUR_BITEXACT ? 56u : 55u) : (t == 1 || t == 5 ? 34u : 18u);
+}
+// GaussianBlur's 7 taps starting at byte `off` of four consecutive raw dwords: the weight bytes of dword d
+__host__ __device__ constexpr uint32_t blur_wshift(int off, int d, int bm = ORBX_BLUR_SCALAR)
+{
     uint32_t w = 0;
     for (int b = 0; b < 4; ++b) {
         const int t = 4 * d + b - off;
-        if (t >= 0 && t < 7) w |= k[t] << (8 * b);
+        if (t >= 0 && t < 7) w |= blur_tap(bm, t) << (8 * b);
     }
     return w;
 }
@@ -2411,6 +2452,7 @@ constexpr uint32_t kRoundBits = 0x4B400000u;
 // mad24(bx, 4 kTP, C) with C = rowT + 4 (9 - 0x200000 + (18 - 0x400000) kTP) (mod 2^32); the compiler's
 // form of (by >> 1) + bx * kTP + rowT took five.
 constexpr uint32_t kBlurByte0 = 4u * (9u - 0x200000u + (18u - 0x400000u) * (uint32_t)kTP);
+template <int kBM>
 __device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t bx)
 {
     const uint32_t t = __umul24(bx, 4u * (uint32_t)kTP) + C, f = __builtin_amdgcn_ubfe(by, 1, 23);
@@ -2426,14 +2468,18 @@ __device__ __forceinline__ uint32_t blur_acc(uint32_t C, uint32_t by, uint32_t b
     const uint32_t sh = by << 4;
     const uint32_t e0 = __builtin_amdgcn_alignbit(d1, d0, sh), e1 = __builtin_amdgcn_alignbit(d2, d1, sh);
     const uint32_t e2 = __builtin_amdgcn_alignbit(d3, d2, sh), e3 = d3 >> (sh & 31u);
+    constexpr unsigned short k1 = (unsigned short)blur_tap(kBM, 2), k3 = (unsigned short)blur_tap(kBM, 3);
     uint32_t acc = __builtin_amdgcn_udot2(as_us2(e0), ushort2_t{18, 34}, 1u << 15, false);
-    acc = __builtin_amdgcn_udot2(as_us2(e1), ushort2_t{49, 55}, acc, false);
-    acc = __builtin_amdgcn_udot2(as_us2(e2), ushort2_t{49, 34}, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(e1), ushort2_t{k1, k3}, acc, false);
+    acc = __builtin_amdgcn_udot2(as_us2(e2), ushort2_t{k1, 34}, acc, false);
     return __builtin_amdgcn_udot2(as_us2(e3), ushort2_t{18, 0}, acc, false);
 }
 #ifndef ORBX_DESC_WPE
 #define ORBX_DESC_WPE 1
 #endif
+// kBM: ORBX_BLUR_* (the kernel taps; ORBX_BLUR_SSE2 also rounds the column pass half to even on the level's
+// columns below w & ~3, as SymmColumnVec_32s8u does)
+template <int kBM>
 __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(const Geometry* __restrict__ G, FramePtrs P,
                                                const uint32_t* __restrict__ qt_out,
                                                const int* __restrict__ qt_cnt,
@@ -2678,11 +2724,15 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         // Output column j of the realigned bytes R0 | R1 | R2 is sum_t w[t] * byte[j + t]: a dot4 of each
         // dword with the kernel shifted by j (zero outside the 7 taps), 10 dot4 per row instead of 8
         // byte-realignments and 8 dot4.
+        // (kW[j][d] = blur_wshift(j, d): for the default kernel {18 | 34 << 8 | 49 << 16 | 55 << 24, 49 | 34 << 8 |
+        // 18 << 16, 0} for j = 0, and so on)
         constexpr uint32_t kW[4][3] = {
-            {18u | 34u << 8 | 49u << 16 | 55u << 24, 49u | 34u << 8 | 18u << 16, 0u},
-            {18u << 8 | 34u << 16 | 49u << 24, 55u | 49u << 8 | 34u << 16 | 18u << 24, 0u},
-            {18u << 16 | 34u << 24, 49u | 55u << 8 | 49u << 16 | 34u << 24, 18u},
-            {18u << 24, 34u | 49u << 8 | 55u << 16 | 49u << 24, 34u | 18u << 8}};
+            {blur_wshift(0, 0, kBM), blur_wshift(0, 1, kBM), blur_wshift(0, 2, kBM)},
+            {blur_wshift(1, 0, kBM), blur_wshift(1, 1, kBM), blur_wshift(1, 2, kBM)},
+            {blur_wshift(2, 0, kBM), blur_wshift(2, 1, kBM), blur_wshift(2, 2, kBM)},
+            {blur_wshift(3, 0, kBM), blur_wshift(3, 1, kBM), blur_wshift(3, 2, kBM)}};
+        static_assert(kBM != ORBX_BLUR_SCALAR || (kW[0][0] == (18u | 34u << 8 | 49u << 16 | 55u << 24) &&
+                                                  kW[3][2] == (34u | 18u << 8)), "row-pass weights");
         // Rows that all start at the same byte shift S (csp == 0: the level pitch is a multiple of 4, or the
         // reflect-101 byte path) skip the realignment: output column j is a dot4 of each raw dword with the
         // kernel shifted by S + j bytes, still 10 dot4 per row (2 or 3 per column) and no alignbyte.
@@ -2716,7 +2766,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                             uint32_t acc = 0u;
 #pragma unroll
                             for (int d = 0; d < 4; ++d) {
-                                const uint32_t w = blur_wshift(S + j, d);   // folds to a constant
+                                const uint32_t w = blur_wshift(S + j, d, kBM);   // folds to a constant
                                 if (w) acc = __builtin_amdgcn_udot4(W[d], w, acc, false);
                             }
                             o[e][j] = acc;
@@ -2762,7 +2812,17 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             const f2v BY = __builtin_elementwise_fma(PX, vb, PY * va) + mg;
             const f2v BX = __builtin_elementwise_fma(PX, va, -(PY * vb)) + mg;
 #pragma unroll
-            for (int e = 0; e < 2; ++e) tv[q + e] = blur_acc(cblur, __float_as_uint(BY[e]), __float_as_uint(BX[e]));
+            for (int e = 0; e < 2; ++e) {
+                uint32_t t = blur_acc<kBM>(cblur, __float_as_uint(BY[e]), __float_as_uint(BX[e]));
+                if constexpr (kBM == ORBX_BLUR_SSE2) {
+                    // SymmColumnVec_32s8u: _mm_cvtps_epi32 of the exact sum T / 2^16 rounds half to even, so a
+                    // tie (T % 2^16 == 2^15, here t = T + 2^15 with t % 2^16 == 0) above an even T >> 16 (t's bit
+                    // 16 set) rounds down, on every level column below w & ~3
+                    const int xl = cx + (int)(__float_as_uint(BX[e]) - kRoundBits);
+                    if ((t & 0x1FFFFu) == 0x10000u && xl < (LG.w & ~3)) t -= 0x10000u;
+                }
+                tv[q + e] = t;
+            }
         }
         uint16_t* const stab = (uint16_t*)rowT;
 #pragma unroll
@@ -2805,8 +2865,15 @@ void launch_describe(const Geometry& g, const ExtractBufs& b, const FramePtrs& p
     // small batches (the per-frame host path) are latency-bound: one keypoint per wave
     const int kpw = batch <= kLatencyMaxBatch ? 1 : kDescPerWave;
     dim3 grid((g.out_per_frame + kDescWaves * kpw - 1) / (kDescWaves * kpw), batch);
-    hipLaunchKernelGGL(k_describe, grid, dim3(64 * kDescWaves), 0, s, b.geom, p, b.qt_out, b.qt_cnt, kps, desc, cap,
-                       b.status, kpw);
+    if (b.blur_mode == ORBX_BLUR_SSE2)
+        hipLaunchKernelGGL(k_describe<ORBX_BLUR_SSE2>, grid, dim3(64 * kDescWaves), 0, s, b.geom, p, b.qt_out, b.qt_cnt,
+                           kps, desc, cap, b.status, kpw);
+    else if (b.blur_mode == ORBX_BLUR_BITEXACT)
+        hipLaunchKernelGGL(k_describe<ORBX_BLUR_BITEXACT>, grid, dim3(64 * kDescWaves), 0, s, b.geom, p, b.qt_out,
+                           b.qt_cnt, kps, desc, cap, b.status, kpw);
+    else
+        hipLaunchKernelGGL(k_describe<ORBX_BLUR_SCALAR>, grid, dim3(64 * kDescWaves), 0, s, b.geom, p, b.qt_out,
+                           b.qt_cnt, kps, desc, cap, b.status, kpw);
 }
 
 }  // namespace orbx

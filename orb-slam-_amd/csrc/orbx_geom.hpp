@@ -42,6 +42,7 @@ struct LevelGeom {
     float patch_size;         // (float)(int)(PATCH_SIZE * scale)
     int roi_mw, roi_mh;       // largest FAST cell ROI of this level
     int pyr_win;              // 1: every 4-column group's taps lie in 8 bytes from its first tap (K1 window path)
+    int rz_simd_end;          // ORBX_RESIZE_SSE2: columns [0, rz_simd_end) take VResizeLinearVec_32s8u's vertical pass
     // K3 node arrays: in LDS (qt_glob 0), or, for budgets whose node list outgrows a workgroup's LDS,
     // in a per-(frame, level) global region of qtg_bytes at qtg_off inside the frame's node block
     int qt_glob;

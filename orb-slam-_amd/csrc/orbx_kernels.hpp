@@ -33,7 +33,20 @@ struct ExtractBufs {
     uint32_t* qt_out;           // [B][out_per_frame] retained keypoints (level coords)
     int* qt_cnt;                // [B][nlevels]
     int* status;                // device error word (bit flags)
+    int resize_mode;            // ORBX_RESIZE_* (orbx_set_cv_modes): K1's vertical pass
+    int blur_mode;              // ORBX_BLUR_*: K4's GaussianBlur column pass and kernel
 };
+
+// OpenCV x86 builds run cv::resize INTER_LINEAR's vertical pass as VResizeLinearVec_32s8u (SSE2) over a dst row's
+// first rz_simd_end(w) bytes: 16 at a time while x <= w - 16, then 4 at a time while x < w - 4; the scalar loop
+// finishes the 0..4-byte tail (imgproc/src/resize.cpp)
+inline int rz_simd_end(int w)
+{
+    int x = 0;
+    while (x <= w - 16) x += 16;
+    while (x < w - 4) x += 4;
+    return x;
+}
 
 // XCD-aware workgroup order.  The dispatcher hands flat workgroup id b to XCD b % 8;
 // each XCD has its own 4 MiB L2.  xcd_block maps b to a logical id so that every

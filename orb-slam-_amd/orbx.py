@@ -32,9 +32,11 @@ OK, EMPTY, EINVAL, ENOMEM, EDEVICE, ENOSPC = 0, 1, -22, -12, -5, -28
 ORBM_MAX_FEATURES = 16384   # include/orbx.h: keypoints per frame of the matcher searches
 ORBV_MAX_FEATURES = 65536   # include/orbx.h: descriptors per frame of the vocabulary transform
 TOP2, FULL_U16 = 0, 1
+RESIZE_SCALAR, RESIZE_SSE2 = 0, 1              # orbx_set_cv_modes (include/orbx.h)
+BLUR_SCALAR, BLUR_SSE2, BLUR_BITEXACT = 0, 1, 2
 
 EXPORTED = [
-    "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_capacity", "orbx_extract", "orbx_get_level",
+    "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_capacity", "orbx_set_cv_modes", "orbx_extract", "orbx_get_level",
     "orbx_extract_batch_device", "orbx_extract_stage_device", "orbx_sync", "orbx_set_timing", "orbx_get_stage_times",
     "orbx_debug_pyramid", "orbx_debug_candidates", "orbx_debug_launches", "orbm_descriptor_distance", "orbm_allpairs_device", "orbm_allpairs",
     "orbm_search_init_batch_device", "orbm_search_for_initialization_device", "orbm_search_for_initialization",
@@ -162,6 +164,7 @@ def _load():
     L.orbx_destroy.restype = None
     L.orbx_get_tables.argtypes = [vp, i32p, f32p, f32p, f32p, f32p, f32p, i32p]
     L.orbx_capacity.argtypes = [vp, C.c_int, C.c_int]
+    L.orbx_set_cv_modes.argtypes = [vp, C.c_int, C.c_int]
     L.orbx_extract.argtypes = [vp, u8p, C.c_int, C.c_int, C.c_size_t, vp, C.c_int, u8p, i32p]
     L.orbx_get_level.argtypes = [vp, C.c_int, P(u8p), i32p, i32p, P(C.c_size_t)]
     L.orbx_extract_batch_device.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_size_t, vp, vp,
@@ -262,6 +265,7 @@ class ORBextractor:
         _check("orbx_get_tables", lib.orbx_get_tables(h, None, None, f32(self._scale), f32(self._inv), f32(self._s2),
                                                       f32(self._is2), self._nfl.ctypes.data_as(C.POINTER(C.c_int))))
         self._last_shape = None
+        self._modes = (RESIZE_SCALAR, BLUR_SCALAR)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -295,6 +299,12 @@ class ORBextractor:
 
     def features_per_level(self):
         return self._nfl.copy()
+
+    def set_cv_modes(self, resize=None, blur=None):
+        """The OpenCV build the extractor reproduces (include/orbx.h orbx_set_cv_modes):
+        resize RESIZE_SCALAR / RESIZE_SSE2, blur BLUR_SCALAR / BLUR_SSE2 / BLUR_BITEXACT (None: keep)."""
+        self._modes = (self._modes[0] if resize is None else int(resize), self._modes[1] if blur is None else int(blur))
+        _check("orbx_set_cv_modes", lib.orbx_set_cv_modes(self._h, self._modes[0], self._modes[1]))
 
     def capacity(self, rows, cols):
         c = lib.orbx_capacity(self._h, rows, cols)
