@@ -91,7 +91,9 @@ orbx_status orbx_set_cv_modes(orbx_handle* h, int resize_mode, int blur_mode);
  *     reference divides by zero there, src/ORBextractor.cc:941-949);
  *   - a level whose quadtree region is less than half as wide as it is tall (nIni = 0,
  *     :650);
- *   - an image side above 4096 pixels (12-bit packed keypoint coordinates).
+ *   - an image whose sides' bit widths sum to more than 24 (keypoint coordinates are packed in 24 bits,
+ *     split between x and y by the image's shape: up to 4096 x 4096, 8192 x 2048, 16384 x 1024, ...);
+ *   - a level whose resize source rows outgrow a workgroup's 160 KiB of LDS (sides above ~9,700 px).
  * Any keypoint budget runs: a level whose quadtree node list outgrows a workgroup's LDS
  * (about 1,700 keypoints, e.g. Tracking's 2 * nFeatures initialisation extractor at 4,000
  * features, src/Tracking.cc:133) keeps its node arrays in device memory instead. */

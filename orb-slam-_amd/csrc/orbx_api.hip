@@ -271,7 +271,10 @@ bool dalloc_exact(T*& p, size_t count)
 orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
 {
     if (h->geom_ok && h->grows == rows && h->gcols == cols) return ORBX_OK;
-    if (rows <= 0 || cols <= 0 || rows > kMaxDim || cols > kMaxDim) return ORBX_EINVAL;
+    // packed keypoint coordinates (pack_kp): x and y share 24 bits, 12 / 12 up to 4096 x 4096
+    auto bits = [](int v) { int b = 0; while ((1 << b) < v) ++b; return b; };
+    if (rows <= 0 || cols <= 0 || bits(cols) + bits(rows) > kKpCoordBits) return ORBX_EINVAL;
+    const int kp_xbits = std::max(bits(cols), std::min(12, kKpCoordBits - bits(rows)));
     for (const auto& b : h->geom_blocks)
         if (b.rows == rows && b.cols == cols) {
             select_geometry(h, b);
@@ -282,6 +285,7 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
     g.rows = rows;
     g.cols = cols;
     g.nlevels = t.nlevels;
+    g.kp_xbits = kp_xbits;
     g.ini_th = std::min(std::max(h->params.ini_th_fast, 0), 255);
     g.min_th = std::min(std::max(h->params.min_th_fast, 0), 255);
     std::memcpy(g.umax, t.umax, sizeof(g.umax));
@@ -388,6 +392,8 @@ orbx_status ensure_geometry(orbx_handle* h, int rows, int cols)
         L.patch_size = (float)(int)(31 * t.scale[l]);   // :1013
     }
     g.ncells = (int)cells.size();
+    for (int l = 1; l < t.nlevels; ++l)   // a per-level pyramid launch stages its source rows in one workgroup's LDS
+        if (pyr_level_lds(g, l) > 160 * 1024) return ORBX_EINVAL;
     std::vector<int4> pyrbt;
     if (!pyr_plan(g, yt.data(), pyrbt)) return ORBX_EINVAL;
     fast_groups(g);
@@ -1024,8 +1030,8 @@ orbx_status orbx_debug_candidates(orbx_handle* h, int frame, int level, int* xys
         for (int i = 0; i < n; ++i) {
             const uint32_t v = sl[a + i];
             if (k < cap && xys) {
-                xys[3 * k] = (int)(v & 0xFFF);
-                xys[3 * k + 1] = (int)((v >> 12) & 0xFFF);
+                xys[3 * k] = (int)kp_x(v, (uint32_t)g.kp_xbits);
+                xys[3 * k + 1] = (int)kp_y(v, (uint32_t)g.kp_xbits);
                 xys[3 * k + 2] = (int)(v >> 24);
             }
             ++k;

@@ -546,6 +546,16 @@ bool pyr_plan(Geometry& g, const int2* yt, std::vector<int4>& bands)
     return true;
 }
 
+size_t pyr_level_lds(const Geometry& g, int l)
+{
+    // source rows per block: kPyrRows * (src/dst scale) + 2, bounded by the level ratio; an LDS row is the
+    // 16-byte chunks spanning a source row at any start alignment; + 16 bytes: the window path's third dword
+    // of a group at the end of the last row
+    const int srows = (kPyrRows * g.lv[l - 1].h + g.lv[l].h - 1) / g.lv[l].h + 2;
+    const int lp = ((g.lv[l - 1].w + 15 + 15) >> 4) << 4;
+    return (size_t)srows * lp + 16;
+}
+
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s)
 {
     if (batch <= kLatencyMaxBatch && g.pyr_ngroups > 0) {
@@ -572,17 +582,18 @@ void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p,
         const int q = (g.lv[l].w + 3) >> 2;
         const int nt = std::min(kPyrNT, (q + 63) & ~63);
         const bool al = l >= 2 || (((uintptr_t)p.in | (uintptr_t)p.in_pitch | (uintptr_t)p.in_fstride) & 3) == 0;
+        // (levels of images wider than about 4,000 px stage more than the default 64 KiB; ensure_geometry
+        // rejects any above the workgroup's 160 KiB, pyr_level_lds)
+        auto launch = [&](auto kern) {
+            if (smem > 64 * 1024)
+                hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+            hipLaunchKernelGGL(kern, grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab, lp);
+        };
         auto go = [&](auto rm_tag) {
             constexpr int RM = decltype(rm_tag)::value;
-            if (g.lv[l].pyr_win && al)
-                hipLaunchKernelGGL((k_pyramid_level<true, true, RM>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab, b.ytab,
-                                   lp);
-            else if (g.lv[l].pyr_win)
-                hipLaunchKernelGGL((k_pyramid_level<true, false, RM>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab,
-                                   b.ytab, lp);
-            else
-                hipLaunchKernelGGL((k_pyramid_level<false, false, RM>), grid, dim3(nt), smem, s, b.geom, p, l, b.xtab,
-                                   b.ytab, lp);
+            if (g.lv[l].pyr_win && al) launch(k_pyramid_level<true, true, RM>);
+            else if (g.lv[l].pyr_win) launch(k_pyramid_level<true, false, RM>);
+            else launch(k_pyramid_level<false, false, RM>);
         };
         if (b.resize_mode == ORBX_RESIZE_SSE2) go(std::integral_constant<int, 1>{});
         else go(std::integral_constant<int, 0>{});
@@ -1139,6 +1150,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
         // now): one bit per kept pixel, then lane i emits window row i.
         if (kept_n > 0) {
             const int xr0 = Cc.roi_x0 + 3 - kMinBorder, yr0 = Cc.roi_y0 + 3 - kMinBorder;
+            const uint32_t kxb = (uint32_t)G->kp_xbits;   // packed keypoint x width (pack_kp)
             const int ci = c - c0;
             const bool buffered = !direct && obn + kept_n <= kFastObCap;   // wave-uniform
             const int rounds = (nf2 + nbk + 63) >> 6;
@@ -1155,7 +1167,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                             const int m = list[lane + (r << 6)];   // window (i, j) at m = i * TP + j
                             const int wi = m / TP, wj = m - wi * TP;
                             const int sc = map[m + TP + 1];
-                            dst[idx + lanes_below(km)] = pack_kp((uint32_t)(xr0 + wj), (uint32_t)(yr0 + wi), (uint32_t)(sc - 1));
+                            dst[idx + lanes_below(km)] = pack_kp((uint32_t)(xr0 + wj), (uint32_t)(yr0 + wi), (uint32_t)(sc - 1), kxb);
                         }
                         idx += __popcll(km);
                     };
@@ -1194,7 +1206,7 @@ __global__ __launch_bounds__(64, LD >= 10 ? ORBX_FAST_WPE10 : ORBX_FAST_WPE) voi
                         const int jj = __builtin_ctzll(bits);
                         bits &= bits - 1;
                         const int sc = map[(lane + 1) * TP + jj + 1];
-                        dst[idx++] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + lane), (uint32_t)(sc - 1));
+                        dst[idx++] = pack_kp((uint32_t)(xr0 + jj), (uint32_t)(yr0 + lane), (uint32_t)(sc - 1), kxb);
                     }
                 }
             };
@@ -1593,6 +1605,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     unsigned long long qt_acc[16] = {};
 #endif
     const LevelGeom& LG = G->lv[l];
+    const uint32_t xb = (uint32_t)__builtin_amdgcn_readfirstlane(G->kp_xbits);   // packed keypoint x width
     // lcap / cellcap: node-list and cell capacity of this launch's levels (qt_launch)
     constexpr bool kKpL = qt_kpn(QT_NT, QT_KPT, kG) > 0;
     const QtLayout Ly = qt_layout(lcap, cellcap, (int)sizeof(Ix), qt_kpn(QT_NT, QT_KPT, kG));
@@ -1782,7 +1795,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     for (int i = tid; i < nIni; i += QT_NT) ccnt[i] = 0;
     __syncthreads();
     auto root_of = [&](uint32_t k) {
-        int r = (int)((float)(int)(k & 0xFFF) / hX);
+        int r = (int)((float)(int)kp_x(k, xb) / hX);
         return r >= nIni ? nIni - 1 : r;
     };
     const int wave_i0 = tid - (tid & 63);   // this wave's first candidate index in register slot 0
@@ -1868,7 +1881,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
             snode[s] = (Ix)p;
             const int hx = (int)ceilf((float)(cx1[p] - cx0[p]) / 2);
             const int hy = (int)ceilf((float)(cy1[p] - cy0[p]) / 2);
-            sinfo[p] = 0x80000000u | (uint32_t)(cx0[p] + hx) | ((uint32_t)(cy0[p] + hy) << 12);
+            sinfo[p] = 0x80000000u | (uint32_t)(cx0[p] + hx) | ((uint32_t)(cy0[p] + hy) << xb);
             ccnt[4 * p] = ccnt[4 * p + 1] = ccnt[4 * p + 2] = ccnt[4 * p + 3] = 0;
         };
 
@@ -1944,8 +1957,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
             const uint32_t p = d & kPosMask;
             const uint32_t w = sinfo[p];
             if (!(w & 0x80000000u)) return -1;
-            const uint32_t x = k & 0xFFFu, y = (k >> 12) & 0xFFFu;
-            return (int)(4 * p + (x >= (w & 0xFFFu) ? 1u : 0u) + (y >= ((w >> 12) & 0xFFFu) ? 2u : 0u));
+            return (int)(4 * p + (kp_x(k, xb) >= kp_x(w, xb) ? 1u : 0u) + (kp_y(k, xb) >= kp_y(w, xb) ? 2u : 0u));
         };
         if constexpr (!kG) {
             // keys first, branch-free (every slot's node and keypoint LDS reads in flight together; a slot
@@ -1961,8 +1973,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
                 const int i = tid + r * QT_NT;
                 const uint32_t w = wv[r], k = kv[r];
                 const bool cand = i < n && (w & 0x80000000u);
-                const uint32_t qd = ((k & 0xFFFu) >= (w & 0xFFFu) ? 1u : 0u) +
-                                    (((k >> 12) & 0xFFFu) >= ((w >> 12) & 0xFFFu) ? 2u : 0u);
+                const uint32_t qd = (kp_x(k, xb) >= kp_x(w, xb) ? 1u : 0u) + (kp_y(k, xb) >= kp_y(w, xb) ? 2u : 0u);
                 nd[r] = (nd[r] & 0xFFFFu) | (cand ? 0x40000u | (qd << 16) : 0u);
             }
 #pragma unroll
@@ -2041,7 +2052,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
             const int pos0 = Ctot - (int)(ps & 0xFFFFu) - cs;   // later splits are pushed in front
             int e = (int)(ps >> 16);
             const uint32_t w = sinfo[p];
-            const int mx = (int)(w & 0xFFFu), my = (int)((w >> 12) & 0xFFFu);
+            const int mx = (int)kp_x(w, xb), my = (int)kp_y(w, xb);
             const int x0 = cx0[p], x1 = cx1[p], y0 = cy0[p], y1 = cy1[p];
             int np = pos0 + cs;   // n1 lands last (it was pushed first)
 #pragma unroll
@@ -2139,9 +2150,9 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     uint32_t* out = qt_out + (size_t)f * G->out_per_frame + LG.out_off;
     for (int p = tid; p < outn; p += QT_NT) {
         const unsigned long long key = best[p];
-        const uint32_t x = (uint32_t)(key & 0xFFF) + kMinBorder;
-        const uint32_t y = (uint32_t)((key >> 12) & 0xFFF) + kMinBorder;
-        out[p] = pack_kp(x, y, (uint32_t)(key >> 56));
+        const uint32_t x = kp_x((uint32_t)key, xb) + kMinBorder;
+        const uint32_t y = kp_y((uint32_t)key, xb) + kMinBorder;
+        out[p] = pack_kp(x, y, (uint32_t)(key >> 56), xb);
     }
     if (tid == 0) {
         qt_cnt[(size_t)f * G->nlevels + l] = outn;
@@ -2492,6 +2503,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     const int lb = xcd_block(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
     const int f = lb / gridDim.x, bx = lb - f * gridDim.x;
     const int L = G->nlevels;
+    const uint32_t kxb = (uint32_t)__builtin_amdgcn_readfirstlane(G->kp_xbits);   // packed keypoint x width
     const int* cnts = qt_cnt + (size_t)f * L;
     uint32_t* raw32 = s_raw[wave];
     uint8_t* raw = (uint8_t*)raw32;
@@ -2559,7 +2571,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
     // the compiler wait for the DMA (a write-after-read on a VMEM source register) before BRIEF
     uint32_t dma_va[3] = {0u, 0u, 0u};
     auto fill = [&](int l, uint32_t pk, int& sb, int& sp) {
-        const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF);
+        const int cx = (int)kp_x(pk, kxb), cy = (int)kp_y(pk, kxb);
         const int w = G->lv[l].w, h = G->lv[l].h;
         int pitch;
         const uint8_t* img = level_base(P, G, f, l, pitch);
@@ -2633,7 +2645,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
             const int jc = jj < nkp ? jj : nkp - 1;   // wave-uniform
             const int l = __builtin_amdgcn_readlane(my_l, jc);
             const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)my_pk, jc);
-            const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF);
+            const int cx = (int)kp_x(pk, kxb), cy = (int)kp_y(pk, kxb);
             int pitch;
             const uint8_t* img = level_base(P, G, f, l, pitch);
             const uintptr_t a = (uintptr_t)(img + (size_t)(cy + vrow) * pitch + (cx - 15 + 16 * ich));
@@ -2708,7 +2720,7 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         const uint32_t pk = npk;
         const int csb = sb, csp = sp;
         const LevelGeom& LG = G->lv[l];
-        const int cx = (int)(pk & 0xFFF), cy = (int)((pk >> 12) & 0xFFF), score = (int)(pk >> 24);
+        const int cx = (int)kp_x(pk, kxb), cy = (int)kp_y(pk, kxb), score = (int)(pk >> 24);
         // this keypoint's DMA has landed.  vmcnt counts loads and stores and retires them in issue order, and
         // the previous keypoint's three output stores (desc dwordx2, cv::KeyPoint dwordx4 + dwordx3) were issued
         // after this DMA: waiting down to 3 leaves their round trip in flight

@@ -15,7 +15,7 @@ namespace orbx {
 constexpr int kMaxLevels = 16;
 constexpr int kEdge = 19;                 // EDGE_THRESHOLD, src/ORBextractor.cc:74
 constexpr int kMinBorder = kEdge - 3;     // minBorderX/Y, src/ORBextractor.cc:932
-constexpr int kMaxDim = 4096;             // 12-bit packed keypoint coordinates
+constexpr int kKpCoordBits = 24;          // packed keypoint: x (kp_xbits) | y (24 - kp_xbits) | score (8)
 
 // One FAST cell ROI (src/ORBextractor.cc:952-976), level coordinates.
 struct Cell {
@@ -76,6 +76,7 @@ struct Geometry {
     int fast_cb[3], fast_rw[2], fast_rh[2];
     int lcap;                 // quadtree list capacity (max level cap + slack)
     int qt_kpt0;              // level-0 quadtree keypoints per thread (16, or 24 for large frames)
+    int kp_xbits;             // packed keypoint x width (pack_kp): 12, or more for images wider than 4096 px
     long long pyr_bytes;      // bytes per frame for levels 1..L-1
     long long qtg_per_frame;  // K3 global node block per frame (0: every level's node list fits LDS)
     int pyr_ngroups;          // K1 small-batch launches (0: per-level launches for every batch)
@@ -84,10 +85,14 @@ struct Geometry {
     LevelGeom lv[kMaxLevels];
 };
 
-// Packed candidate / retained keypoint: x (12 bits) | y (12 bits) << 12 | score << 24
-ORBX_HD uint32_t pack_kp(uint32_t x, uint32_t y, uint32_t s)
+// Packed candidate / retained keypoint: x (xb bits) | y (24 - xb bits) << xb | score << 24.  xb =
+// Geometry::kp_xbits: 12 up to 4096 x 4096, wider images trade y bits for x bits (any image whose sides' bit
+// widths sum to 24 or less, e.g. 8192 x 2048)
+ORBX_HD uint32_t pack_kp(uint32_t x, uint32_t y, uint32_t s, uint32_t xb)
 {
-    return x | (y << 12) | (s << 24);
+    return x | (y << xb) | (s << 24);
 }
+ORBX_HD uint32_t kp_x(uint32_t k, uint32_t xb) { return k & ((1u << xb) - 1u); }
+ORBX_HD uint32_t kp_y(uint32_t k, uint32_t xb) { return (k >> xb) & ((1u << (kKpCoordBits - xb)) - 1u); }
 
 }  // namespace orbx

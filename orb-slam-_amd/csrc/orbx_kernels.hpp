@@ -116,6 +116,7 @@ __host__ __device__ inline int qt_regcap(const Geometry& g, int l) { return qt_n
 // host: K1 small-batch launch groups and their band tables (Geometry::pg) from the resize row tables
 bool pyr_plan(Geometry& g, const int2* yt, std::vector<int4>& bands);
 void launch_pyramid(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
+size_t pyr_level_lds(const Geometry& g, int l);   // k_pyramid_level's dynamic LDS for level l (>= 1)
 void fast_groups(Geometry& g);   // host: FAST launch groups (cell ranges, LDS sizes)
 void launch_fast(const Geometry& g, const ExtractBufs& b, const FramePtrs& p, int batch, hipStream_t s);
 void launch_quadtree(const Geometry& g, const ExtractBufs& b, int* frame_counts, int batch, hipStream_t s);

@@ -1,7 +1,8 @@
 """The two capability limits this library has and the reference does not (INTEGRATION.md "Deviations"):
 
-- image sides up to 4096 pixels (keypoint coordinates packed in 12 bits on the device; the reference's
-  ORBextractor::operator(), src/ORBextractor.cc:1248-1334, takes any size);
+- image sizes whose sides' bit widths sum to 24 or less, e.g. up to 4096 x 4096 or 8192 x 2048 (keypoint
+  coordinates packed in 24 bits on the device, split between x and y by the image's shape; the reference's
+  ORBextractor::operator(), src/ORBextractor.cc:1248-1334, takes any size; round 5 capped both sides at 4096);
 - at most ORBM_MAX_FEATURES (16384) keypoints per frame for the SearchByBoW / SearchForTriangulation
   searches and the projection searches, and ORBV_MAX_FEATURES (65536) for the vocabulary transform (per-frame
   state in a workgroup's LDS, or past 8192 features in global memory; src/ORBmatcher.cc:45-129, 159-288 and
@@ -16,30 +17,50 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_image_side_limit(orbref, cuda):
+def _check_extract(orbref, ex, img, nfeat, cuda, batch_frames=None):
+    from test_gpu_parity import _run_batch, assert_same_keypoints
+    p = orbref.make_params(nfeat, 1.2, 8, 20, 7)
+    ref = orbref.extract(img, p, want_pyramid=False)
+    kps, desc = ex(img)
+    assert len(ref.keypoints) > 500
+    assert_same_keypoints(kps, ref.keypoints, desc, ref.descriptors, "%dx%d host" % (img.shape[1], img.shape[0]))
+    if batch_frames is not None:
+        _, _, _, _, klist, dlist = _run_batch(ex, batch_frames, cuda)
+        for f in range(len(batch_frames)):
+            r = orbref.extract(batch_frames[f], p, want_pyramid=False)
+            assert_same_keypoints(klist[f], r.keypoints, dlist[f], r.descriptors, "batch frame %d" % f)
+    return ref
+
+
+def test_image_size_limit(orbref, cuda):
+    """sizes past the old 4096-px side run bit-exact (4097 x 600 and 8192 x 512, through the
+    host call and a 10-frame batch: the large-batch kernels); the packed coordinates' 24 bits bound the size."""
+    import ctypes
     import orbx
     import orbx_synth
-    ex = orbx.ORBextractor(1000, 1.2, 8, 20, 7)
+    ex = orbx.ORBextractor(2000, 1.2, 8, 20, 7)
     # (a level taller than wide gives nIni = 0, where the reference divides by zero: -1 for any size)
     cap = lambda r, c: orbx.lib.orbx_capacity(ex._h, r, c)   # the raw C value (-1 = refused)
-    assert cap(376, 4096) > 0 and cap(4096, 4096) > 0
-    assert cap(376, 4097) == -1 and cap(4097, 4097) == -1
-    img = orbx_synth.gen_image(17, 4096, 300)
-    kps, desc = ex(img)
-    ref = orbref.extract(img, orbref.make_params(1000, 1.2, 8, 20, 7), want_pyramid=False)
-    assert len(kps) == len(ref.keypoints) > 500
-    for f in ("x", "y", "size", "response", "octave"):
-        assert np.array_equal(kps[f], ref.keypoints[f]), f
-    assert np.array_equal(desc, ref.descriptors)
-    import ctypes
-    wide = np.zeros((300, 4097), np.uint8)
+    assert cap(376, 4096) > 0 and cap(4096, 4096) > 0 and cap(376, 4097) > 0 and cap(2048, 8192) > 0
+    assert cap(4097, 4097) == -1 and cap(2049, 8192) == -1 and cap(600, 16385) == -1
+    for (w, h, seed) in ((4097, 600, 17), (8192, 512, 18)):
+        img = orbx_synth.gen_image(seed, w, h)
+        frames = np.stack([orbx_synth.gen_image(seed * 10 + f, w, h) for f in range(10)])
+        ref = _check_extract(orbref, ex, img, 2000, cuda, frames)
+        assert ref.keypoints["x"].max() > 0.97 * w   # keypoints reach past x = 4096 - 19
+    tall = np.zeros((300, 4097), np.uint8)   # empty but valid: 0 keypoints
     kbuf = np.zeros((64, 7), np.int32)
     dbuf = np.zeros((64, 32), np.uint8)
     n = ctypes.c_int(-1)
-    rc = orbx.lib.orbx_extract(ex._h, wide.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 300, 4097, 4097,
+    big = np.zeros((4097, 4097), np.uint8)
+    rc = orbx.lib.orbx_extract(ex._h, big.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 4097, 4097, 4097,
                                kbuf.ctypes.data_as(ctypes.c_void_p), 64,
                                dbuf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(n))
     assert rc == orbx.EINVAL and n.value == -1
+    rc = orbx.lib.orbx_extract(ex._h, tall.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), 300, 4097, 4097,
+                               kbuf.ctypes.data_as(ctypes.c_void_p), 64,
+                               dbuf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(n))
+    assert rc == orbx.OK and n.value == 0
 
 
 def _tiny_vocabulary():

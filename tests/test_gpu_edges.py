@@ -52,8 +52,9 @@ def test_scale_factor_two(orbref, cuda):
 
 
 def test_level0_at_the_4096_px_side(orbref, cuda):
-    """4096 x 320: level 0's keypoint x reaches 4096 - 19, the largest the 12-bit packed coordinate holds
-    (orbx_geom.hpp kMaxDim), on every level and through both the host call and a batch."""
+    """4096 x 320: level 0's keypoint x reaches 4096 - 19, the largest a 12-bit packed x holds (the split
+    the geometry picks up to 4096 x 4096, orbx_geom.hpp pack_kp), on every level and through both the host call
+    and a batch."""
     import orbx_synth
     img = orbx_synth.gen_image(61, 4096, 320)
     frames = np.stack([orbx_synth.gen_image(62 + f, 4096, 320) for f in range(9)])
