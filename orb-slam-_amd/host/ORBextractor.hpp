@@ -85,6 +85,16 @@ public:
         pyramid_valid_ = false;
     }
 
+    // Which OpenCV build's resize / GaussianBlur arithmetic to reproduce (orbx_set_cv_modes, SURVEY.md
+    // Appendix A): ORBX_RESIZE_SCALAR / _SSE2 and ORBX_BLUR_SCALAR / _SSE2 / _BITEXACT.  Not in the reference's
+    // interface: the reference gets whatever its linked OpenCV does.
+    void SetOpenCVModes(int resize_mode, int blur_mode)
+    {
+        int rc = orbx_set_cv_modes(h_, resize_mode, blur_mode);
+        if (rc != ORBX_OK) throw OrbxError("orbx_set_cv_modes", rc);
+        pyramid_valid_ = false;
+    }
+
     int GetLevels() const { return nlevels_; }
     float GetScaleFactor() const { return scaleFactor_; }
     std::vector<float> GetScaleFactors() const { return mvScaleFactor; }

@@ -28,6 +28,8 @@ int snippets(orbx_handle* h, orbx_handle* hl, orbx_handle* hr, orbx_vocabulary* 
     std::vector<float> sf(8), isf(8), s2(8), is2(8);
     std::vector<int> fpl(8);
     orbx_get_tables(h, nullptr, nullptr, sf.data(), isf.data(), s2.data(), is2.data(), fpl.data());
+    orbx_set_cv_modes(h, ORBX_RESIZE_SSE2, ORBX_BLUR_SSE2);
+    orbx_set_cv_modes(h, ORBX_RESIZE_SSE2, ORBX_BLUR_BITEXACT);
     int rows = 376, cols = 1241, cap = orbx_capacity(h, rows, cols), n = 0;
     std::vector<uint8_t> image((size_t)rows * cols), desc((size_t)cap * 32);
     std::vector<KeyPoint> kps(cap);
