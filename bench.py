@@ -36,7 +36,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "orb-slam-_amd"))
 
-DEFAULT_BATCH = 1024   # frames per GPU per step (tools/pmc_summary.py and tools/sq_summary.py read it from here)
+DEFAULT_BATCH = 2048   # frames per GPU per step (tools/pmc_summary.py and tools/sq_summary.py read it from here)
 
 
 def _free_port() -> int:
@@ -414,11 +414,11 @@ def main():
     ap.add_argument("--dry-run", action="store_true", help="print the launch plan and exit")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="frames per GPU per step (round 4, K = 20: 384 -> "
-                    "249k, 512 -> 257k, 768 -> 261-263k, 1024 -> 263-266k, 1280 -> 265-267k frames/s: the pipeline's fill and drain "
-                    "weigh less; round 2, K = 100: "
-                    "128 -> 149.9k, 192 -> 152.6k, 256 -> 154.6k, 384 -> 156.4k)")
-    ap.add_argument("--pool", type=int, default=4, help="distinct batches resident per GPU (4 x 1024 frames = 1.9 GB > the 256 MB Infinity Cache)")
+    ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="frames per GPU per step (round 6, K = 20, one box: "
+                    "768 -> 279.0k, 1024 -> 281.1-283.0k, 1536 -> 283.5k, 2048 -> 285.3-286.1k, 3072 -> 287.8k, 4096 -> "
+                    "285.5k frames/s: the pipeline's fill and drain and the fixed per-launch costs weigh less; "
+                    "tools/diag/batch_stream_sweep.sh)")
+    ap.add_argument("--pool", type=int, default=4, help="distinct batches resident per GPU (4 x 2048 frames = 3.8 GB > the 256 MB Infinity Cache)")
     ap.add_argument("--streams", type=int, default=3, help="pipeline depth (batches in flight per GPU); "
                     "GPU_MAX_HW_QUEUES=4 leaves 3 besides the default stream")
     ap.add_argument("--iso-steps", type=int, default=3, help="untimed one-stream steps for roofline_isolated")
