@@ -1584,7 +1584,9 @@ __device__ __forceinline__ void wave_run_add(uint32_t* ctr, int key)
 // node indices, for budgets whose node list outgrows a workgroup's LDS (e.g. Tracking's
 // 2 * nFeatures initialisation extractor, src/Tracking.cc:133, at 4000 features).  The algorithm and its
 // order of operations are the same; only the wave totals and the shared scalars stay in LDS.
-template <int QT_NT, int QT_KPT, bool kG>
+// kWide: images wider or taller than 4096 px, whose packed keypoints split x / y at Geometry::kp_xbits; the
+// standard form keeps the 12-bit split as a constant (a runtime split costs <256,4> a spilled register)
+template <int QT_NT, int QT_KPT, bool kG, bool kWide>
 __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometry* __restrict__ G,
                                          const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
                                          const int* __restrict__ cell_counts,
@@ -1605,7 +1607,7 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     unsigned long long qt_acc[16] = {};
 #endif
     const LevelGeom& LG = G->lv[l];
-    const uint32_t xb = (uint32_t)__builtin_amdgcn_readfirstlane(G->kp_xbits);   // packed keypoint x width
+    const uint32_t xb = kWide ? (uint32_t)__builtin_amdgcn_readfirstlane(G->kp_xbits) : 12u;   // packed keypoint x width
     // lcap / cellcap: node-list and cell capacity of this launch's levels (qt_launch)
     constexpr bool kKpL = qt_kpn(QT_NT, QT_KPT, kG) > 0;
     const QtLayout Ly = qt_layout(lcap, cellcap, (int)sizeof(Ix), qt_kpn(QT_NT, QT_KPT, kG));
@@ -2168,14 +2170,14 @@ __device__ __forceinline__ void qt_nodes(const int l, const int f, const Geometr
     }
 }
 
-template <int QT_NT, int QT_KPT, bool kG>
+template <int QT_NT, int QT_KPT, bool kG, bool kWide>
 __global__ __launch_bounds__(QT_NT, ORBX_QT_WPE(QT_NT, QT_KPT, kG)) void k_quadtree(
     int level0, const Geometry* __restrict__ G, const Cell* __restrict__ cells, const uint32_t* __restrict__ slots,
     const int* __restrict__ cell_counts, uint32_t* __restrict__ spill,
     uint32_t* __restrict__ spill_node, uint8_t* __restrict__ gnodes, uint32_t* __restrict__ qt_out,
     int* __restrict__ qt_cnt, int* __restrict__ frame_counts, int* __restrict__ status, int lcap, int cellcap)
 {
-    qt_nodes<QT_NT, QT_KPT, kG>(level0 + blockIdx.x, blockIdx.y, G, cells, slots, cell_counts, spill,
+    qt_nodes<QT_NT, QT_KPT, kG, kWide>(level0 + blockIdx.x, blockIdx.y, G, cells, slots, cell_counts, spill,
                                 spill_node, gnodes, qt_out, qt_cnt, frame_counts, status, lcap, cellcap);
 }
 
@@ -2184,10 +2186,14 @@ static void qt_launch(const Geometry& g, const ExtractBufs& b, int* frame_counts
                       hipStream_t s)
 {
     const size_t smem = kG ? kQtGlobSmem : qt_layout(q.lcap, q.cellcap, 2, qt_kpn(NT, KPT, 0)).total;
-    hipFuncSetAttribute((const void*)k_quadtree<NT, KPT, kG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipLaunchKernelGGL((k_quadtree<NT, KPT, kG>), dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells,
-                       b.slots, b.cell_counts, b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt,
-                       frame_counts, b.status, q.lcap, q.cellcap);
+    auto launch = [&](auto kern) {
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        hipLaunchKernelGGL(kern, dim3(q.nl, batch), dim3(NT), smem, s, q.l0, b.geom, b.cells, b.slots, b.cell_counts,
+                           b.spill, b.spill_node, b.qt_nodes, b.qt_out, b.qt_cnt, frame_counts, b.status, q.lcap,
+                           q.cellcap);
+    };
+    if (g.kp_xbits == 12) launch(k_quadtree<NT, KPT, kG, false>);
+    else launch(k_quadtree<NT, KPT, kG, true>);
 }
 
 // Launch groups.  A group's node capacity is the largest cap + 4 of its levels: a level's list never holds
