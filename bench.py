@@ -625,7 +625,7 @@ def main():
     # stream uploads batch k into pipeline slot k % P's input buffer while the other slots extract;
     # slot j's buffer is overwritten only after its previous extraction has finished reading it.
     host_fed = None
-    if args.host_steps > 0:
+    if args.host_steps > 0 and world == 1:   # per-GPU PCIe figure; N > 1 ranks would each pin a 3.8 GB copy
         hseq = torch.from_numpy(seq).pin_memory()
         # input ring deeper than the pipeline: an upload may run two batches ahead of the oldest extraction
         # still reading its buffer (a slot's extraction lasts about P step times while it shares the chip)
