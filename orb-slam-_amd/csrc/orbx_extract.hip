@@ -2607,10 +2607,34 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                     dma_va[t] = o;
                 }
             }
+        } else if (l > 0) {
+            // Border keypoints of levels >= 1 (about 5% of KITTI's keypoints, 12% at level 7): the same DMA,
+            // through a buffer descriptor over the level's rows (pitch x h bytes of the handle's pyramid block),
+            // so that the patch bytes outside the level read as zeros instead of touching memory (the range check
+            // covers the whole offset: tests/test_gpu_edges.py test_buffer_range_check_covers_soffset); the
+            // reflect-101 bytes are copied in from inside the patch at the loop top (desc_border_fixup).  Offsets
+            // of rows above the level wrap to large unsigned values, also out of range.
+            const long long s0 = (long long)(cy - 21) * pitch + (cx - 21);
+            const uint32_t a0 = (uint32_t)(s0 & ~3ll);
+            sb = (int)(s0 & 3);
+            sp = pitch & 3;   // 0: pitch = align64(w)
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)img, (short)0, pitch * h, 0x00020000);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int c = 64 * t + lane, row = c / 3, k = c - 3 * row;
+                if (t < 2 || lane < 4) {
+                    const uint32_t o = a0 + (uint32_t)((sb + min(row, 42) * pitch) & ~3) + 16u * (uint32_t)k;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(raw32 + 256 * t), 16,
+                                                         o, 0, 0, 0);
+                    dma_va[t] = o;
+                }
+            }
         } else {
             sb = 0;
             sp = 0;
-            // reflect-101 bytes, lane = column (43 of the 48 per row), the column reflection once per lane,
+            // level-0 border keypoints (the caller's image: no room around it to read past), reflect-101 bytes,
+            // lane = column (43 of the 48 per row), the column reflection once per lane,
             // the row's per row (wave-uniform), and 11 rows' loads in flight before their LDS stores
             static_assert(kRawRows >= 44, "rows 0..43 filled");
             const uint8_t* col = img + reflect101(cx - 21 + min(lane, 42), w);
@@ -2737,6 +2761,38 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         __builtin_amdgcn_s_waitcnt(0x0F73);   // vmcnt(3)
         asm volatile("" ::"v"(dma_va[0]), "v"(dma_va[1]), "v"(dma_va[2]));
         wave_lds_sync();
+        // a level >= 1 border keypoint's patch: reflect-101 (copyMakeBorder's BORDER_REFLECT_101, which
+        // GaussianBlur applies at the level's edges) from the bytes inside it, columns first (lane = row), then
+        // whole rows (lane = column), so the corners reflect in both directions.  The patch spans level columns
+        // cx - 21 .. cx + 21 and rows cy - 21 .. cy + 21 (patch row 43 repeats row 42), and a keypoint lies >= 19 px
+        // inside its level, so one reflection reaches every byte.
+        if (l > 0 && !(cx >= 21 && cy >= 21 && cy + 21 < LG.h && (cx + 31 <= LG.w || (cx + 21 < LG.w && cy + 22 < LG.h)))) {
+            const int w = LG.w, h = LG.h, x0 = cx - 21, y0 = cy - 21;
+            auto at = [&](int r, int c) { return raw + r * kRawP + ((csb + r * csp) & 3) + c; };
+            if (x0 < 0 || x0 + 42 >= w) {   // wave-uniform
+                if (lane < kRawRows) {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        if (x0 + c < 0) *at(lane, c) = *at(lane, -(x0 + c) - x0);
+#pragma unroll
+                    for (int c = 40; c <= 42; ++c)
+                        if (x0 + c >= w) *at(lane, c) = *at(lane, 2 * w - 2 - (x0 + c) - x0);
+                }
+                wave_lds_sync();
+            }
+            if (y0 < 0 || y0 + 42 >= h) {   // wave-uniform
+                // (cy in [19, h - 20]: only patch rows 0, 1 (above) and 41, 42, 43 (below) can leave the level)
+                constexpr int kEdgeRows[5] = {0, 1, 41, 42, 43};
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    const int r = kEdgeRows[i], Y = y0 + min(r, 42);
+                    if (Y >= 0 && Y < h) continue;   // wave-uniform
+                    const int rr = (Y < 0 ? -Y : 2 * h - 2 - Y) - y0;
+                    if (lane <= 42) *at(r, lane) = *at(rr, lane);
+                }
+                wave_lds_sync();
+            }
+        }
 
         // horizontal 7-tap pass: lane item = (row pair rp, column group cg) -> 2 rows x 4 columns.
         // Output column j of the realigned bytes R0 | R1 | R2 is sum_t w[t] * byte[j + t]: a dot4 of each
