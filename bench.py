@@ -36,7 +36,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "orb-slam-_amd"))
 
-DEFAULT_BATCH = 2048   # frames per GPU per step (tools/pmc_summary.py and tools/sq_summary.py read it from here)
+DEFAULT_BATCH = 4096   # frames per GPU per step (tools/pmc_summary.py and tools/sq_summary.py read it from here)
 
 
 def _free_port() -> int:
@@ -414,13 +414,15 @@ def main():
     ap.add_argument("--dry-run", action="store_true", help="print the launch plan and exit")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="frames per GPU per step (round 6, K = 20, one box: "
-                    "768 -> 279.0k, 1024 -> 281.1-283.0k, 1536 -> 283.5k, 2048 -> 285.3-286.1k, 3072 -> 287.8k, 4096 -> "
-                    "285.5k frames/s: the pipeline's fill and drain and the fixed per-launch costs weigh less; "
-                    "tools/diag/batch_stream_sweep.sh)")
-    ap.add_argument("--pool", type=int, default=4, help="distinct batches resident per GPU (4 x 2048 frames = 3.8 GB > the 256 MB Infinity Cache)")
-    ap.add_argument("--streams", type=int, default=3, help="pipeline depth (batches in flight per GPU); "
-                    "GPU_MAX_HW_QUEUES=4 leaves 3 besides the default stream")
+    ap.add_argument("--batch", type=int, default=DEFAULT_BATCH, help="frames per GPU per step (round 6, K = 20, "
+                    "tools/diag/batch_stream_sweep.sh: three streams 768 -> 279.0k, 1024 -> 281.1-283.0k, 1536 -> 283.5k, "
+                    "2048 -> 286.5-290.2k, 4096 -> 287.0-288.3k frames/s; two streams 2048 -> 286.8k, 4096 -> "
+                    "290.1-295.3k, 6144 -> 290.2k, 8192 -> 288.3k: the pipeline's fill and drain and the fixed "
+                    "per-launch costs weigh less, and two batches in flight share the CUs and caches better than three)")
+    ap.add_argument("--pool", type=int, default=2, help="distinct batches resident per GPU (2 x 4096 frames = 3.8 GB > the 256 MB Infinity Cache)")
+    ap.add_argument("--streams", type=int, default=2, help="pipeline depth (batches in flight per GPU; "
+                    "GPU_MAX_HW_QUEUES=4 leaves 3 besides the default stream; at 4096 frames per step 2 beat 3: "
+                    "290.1-295.3k against 287.0-288.3k frames/s)")
     ap.add_argument("--iso-steps", type=int, default=3, help="untimed one-stream steps for roofline_isolated")
     ap.add_argument("--match-stream", action="store_true",
                     help="SearchForInitialization on the default stream beside the extraction streams")
