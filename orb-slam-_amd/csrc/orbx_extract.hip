@@ -2607,13 +2607,16 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
                     dma_va[t] = o;
                 }
             }
-        } else if (l > 0) {
+        } else if (l > 0 && pitch - w >= 16) {
             // Border keypoints of levels >= 1 (about 5% of KITTI's keypoints, 12% at level 7): the same DMA,
             // through a buffer descriptor over the level's rows (pitch x h bytes of the handle's pyramid block),
             // so that the patch bytes outside the level read as zeros instead of touching memory (the range check
             // covers the whole offset: tests/test_gpu_edges.py test_buffer_range_check_covers_soffset); the
             // reflect-101 bytes are copied in from inside the patch at the loop top (desc_border_fixup).  Offsets
-            // of rows above the level wrap to large unsigned values, also out of range.
+            // of rows above the level wrap to large unsigned values, also out of range.  A 16-byte chunk can straddle
+            // the descriptor's end only within the level's last 16 bytes, which pitch - w >= 16 makes row padding,
+            // so whether the range check drops such a chunk whole or by dwords, no pixel is lost (a level with
+            // less padding, e.g. 444 px in a 448-byte pitch, takes the byte path below).
             const long long s0 = (long long)(cy - 21) * pitch + (cx - 21);
             const uint32_t a0 = (uint32_t)(s0 & ~3ll);
             sb = (int)(s0 & 3);
@@ -2633,7 +2636,8 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         } else {
             sb = 0;
             sp = 0;
-            // level-0 border keypoints (the caller's image: no room around it to read past), reflect-101 bytes,
+            // level-0 border keypoints (the caller's image: no room around it to read past) and those of levels
+            // with under 16 bytes of row padding: reflect-101 bytes,
             // lane = column (43 of the 48 per row), the column reflection once per lane,
             // the row's per row (wave-uniform), and 11 rows' loads in flight before their LDS stores
             static_assert(kRawRows >= 44, "rows 0..43 filled");
@@ -2766,7 +2770,8 @@ __global__ __launch_bounds__(64 * kDescWaves, ORBX_DESC_WPE) void k_describe(con
         // whole rows (lane = column), so the corners reflect in both directions.  The patch spans level columns
         // cx - 21 .. cx + 21 and rows cy - 21 .. cy + 21 (patch row 43 repeats row 42), and a keypoint lies >= 19 px
         // inside its level, so one reflection reaches every byte.
-        if (l > 0 && !(cx >= 21 && cy >= 21 && cy + 21 < LG.h && (cx + 31 <= LG.w || (cx + 21 < LG.w && cy + 22 < LG.h)))) {
+        if (l > 0 && LG.pitch - LG.w >= 16 &&
+            !(cx >= 21 && cy >= 21 && cy + 21 < LG.h && (cx + 31 <= LG.w || (cx + 21 < LG.w && cy + 22 < LG.h)))) {
             const int w = LG.w, h = LG.h, x0 = cx - 21, y0 = cy - 21;
             auto at = [&](int r, int c) { return raw + r * kRawP + ((csb + r * csp) & 3) + c; };
             if (x0 < 0 || x0 + 42 >= w) {   // wave-uniform

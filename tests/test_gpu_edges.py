@@ -80,3 +80,17 @@ def test_buffer_range_check_covers_soffset(cuda):
     want0 = np.where(np.arange(64) < 16, 0x1000 + np.arange(64), 0).astype(np.uint32)
     assert np.array_equal(v[0], want0), v[0]                   # the descriptor's 16 dwords, zeros past them
     assert not v[1].any() and not v[2].any(), (v[1], v[2])     # soffset moves every lane past num_records
+
+
+def test_border_patches_of_levels_with_little_row_padding(orbref, cuda):
+    """describe stages a level >= 1 border keypoint's patch by buffer-descriptor DMA only when the level's row
+    padding (pitch - width) is at least 16 bytes, so that a 16-byte chunk straddling the level's end never drops a
+    pixel; levels with less take the reflect-101 byte path.  1224 x 400: level 1 is 1020 px wide in a 1024-byte
+    pitch (4 bytes of padding), level 2 850 in 896 (46), so both paths run in one frame, with the default
+    threshold's keypoints along every edge, bit-exact through the host call and a 10-frame batch."""
+    import orbx_synth
+    img = orbx_synth.gen_image(71, 1224, 400)
+    frames = np.stack([orbx_synth.gen_image(72 + f, 1224, 400) for f in range(10)])
+    ref = _check(orbref, img, 2000, 1.2, 8, 20, 7, "1224 x 400", frames, cuda)
+    lv1 = ref.keypoints[ref.keypoints["octave"] == 1]
+    assert len(lv1) > 0
